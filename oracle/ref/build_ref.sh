@@ -1,0 +1,58 @@
+#!/bin/bash
+# oracle/ref/build_ref.sh -- TEST INFRASTRUCTURE ONLY.
+#
+# Builds the reference renderer's own translation units, where they lie under /root/reference
+# (read-only), together with oracle/ref/harness.cpp into two oracle binaries in oracle/_ref/:
+#
+#   mrt_ref        reference as shipped: clang++ -std=c++20 -O3 -fno-exceptions -fno-rtti
+#                  (clang/clang_build_linux.sh:23-29), default FP contraction, glibc libm.
+#                  -march=x86-64-v3 instead of -march=native so the binary also runs on the GPU
+#                  box's host CPU (it is the cpu_baseline of bench.py).
+#   mrt_ref_exact  same sources with -ffp-contract=off and the float libm calls interposed by
+#                  (float)f((double)x) (harness.cpp, MRT_MATHMATCH).  This is the bit-exact pin for
+#                  the C restatement (oracle/mrt_oracle.c) and, through it, the HIP kernel.
+#
+# Two compile fixes, both applied without writing into /root/reference and without copying the
+# source tree: mrt_math.h:66 is an '#error INSERT LZCNT INTRINSIC HERE' placeholder for non-MSVC
+# compilers -- a patched copy of that one header is mapped over the original with a clang VFS
+# overlay; triangle.h:85 calls memcpy without <cstring> -- fixed with '-include cstring'.
+# The SDL platform layer (platform_linux.cpp) is not compiled: the harness is headless.
+# Nothing is written outside oracle/_ref/ and a private mktemp directory that is removed on exit.
+set -euo pipefail
+REF=${MRT_REFERENCE:-/root/reference}
+HERE=$(cd "$(dirname "$0")" && pwd)
+OUT=$(cd "$HERE/.." && pwd)/_ref
+CXX=${CXX:-/opt/rocm/lib/llvm/bin/clang++}
+if [ ! -f "$REF/main.cpp" ]; then
+    echo "build_ref: reference not present at $REF; skipping (prebuilt oracle/_ref used if present)"
+    exit 0
+fi
+mkdir -p "$OUT"
+TMP=$(mktemp -d /tmp/mrtref.XXXXXX)
+trap 'rm -rf "$TMP"' EXIT
+
+sed 's|^#error INSERT LZCNT INTRINSIC HERE|        uint32 i = (uint32)__builtin_clz(v);|' "$REF/mrt_math.h" > "$TMP/mrt_math.h"
+cat > "$TMP/overlay.yaml" <<EOF
+{ 'version': 0, 'case-sensitive': 'true', 'roots': [ { 'name': '$REF', 'type': 'directory',
+  'contents': [ { 'name': 'mrt_math.h', 'type': 'file', 'external-contents': '$TMP/mrt_math.h' } ] } ] }
+EOF
+
+SRCS="cmdline_parser.cpp mat4.cpp obj_loader.cpp pcg.cpp rect.cpp scene.cpp scene_object.cpp sphere.cpp
+      stb_image.cpp texture.cpp triangle.cpp volumes.cpp work_queue.cpp"
+BASE="-std=c++20 -O3 -march=x86-64-v3 -fno-exceptions -fno-rtti -w -include cstring -ivfsoverlay $TMP/overlay.yaml -I$REF -I$REF/include"
+
+build() {  # name extra-flags
+    local name=$1; shift
+    local odir="$TMP/$name"; mkdir -p "$odir"
+    local pids=()
+    for s in $SRCS; do
+        $CXX $BASE "$@" -c "$REF/$s" -o "$odir/${s%.cpp}.o" & pids+=($!)
+    done
+    $CXX $BASE "$@" -c "$HERE/harness.cpp" -o "$odir/harness.o" & pids+=($!)
+    for p in "${pids[@]}"; do wait "$p"; done
+    $CXX "$odir"/*.o -lpthread -o "$OUT/$name"
+    echo "build_ref: built $OUT/$name"
+}
+
+build mrt_ref
+build mrt_ref_exact -ffp-contract=off -DMRT_MATHMATCH
