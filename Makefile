@@ -1,0 +1,42 @@
+# Build of the MI355X render path (no cmake).  `make` builds:
+#   miniraytracer_amd/libmrt.so   C-ABI (include/mrt.h): host scene builder + HIP kernels for gfx950
+#   bin/mrt                       command-line driver with the reference's flags
+#   oracle/liboracle.so           C restatement used by tests / bench cpu_baseline (test infra only)
+HIPCC   ?= /opt/rocm/bin/hipcc
+CC      ?= gcc
+ARCH    ?= gfx950
+JOBS    ?= 8
+# Numerics contract: no FMA contraction, IEEE division/sqrt, denormals kept.
+HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function
+# per-lane traversal stacks stay in scratch instead of being promoted into VGPR vectors
+HIPDEV   = -mllvm -disable-promote-alloca-to-vector
+CSRC     = miniraytracer_amd/csrc
+OBJDIR   = build/obj
+
+LIB_OBJS = $(OBJDIR)/mrt_render.o $(OBJDIR)/scene_builder.o $(OBJDIR)/mrt_common.o
+HDRS     = include/mrt.h include/mrt_scene.h $(wildcard $(CSRC)/*.h) Makefile
+
+all: miniraytracer_amd/libmrt.so bin/mrt oracle/liboracle.so
+
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) $(HIPDEV) -c $< -o $@
+
+$(OBJDIR)/%.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) $(HIPDEV) -c $< -o $@
+
+miniraytracer_amd/libmrt.so: $(LIB_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(LIB_OBJS) -ldl -o $@
+
+bin/mrt: $(CSRC)/mrt_cli.cpp miniraytracer_amd/libmrt.so include/mrt.h
+	@mkdir -p bin
+	$(HIPCC) -O2 -std=c++17 -ffp-contract=off $(CSRC)/mrt_cli.cpp -Lminiraytracer_amd -lmrt -Wl,-rpath,'$$ORIGIN/../miniraytracer_amd' -o $@
+
+oracle/liboracle.so: oracle/mrt_oracle.c oracle/mrt_oracle.h include/mrt_scene.h
+	$(CC) -O2 -std=c11 -fPIC -shared -ffp-contract=off -fno-fast-math -Wall -o $@ oracle/mrt_oracle.c -lm -lpthread
+
+clean:
+	rm -rf build miniraytracer_amd/libmrt.so bin oracle/liboracle.so
+
+.PHONY: all clean

@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/s of the MI355X render path on the Cornell box (config C2 of BASELINE.json:
+scene 5, 500x500, 1024 spp, 32 bounces).
+
+One step = one full render of the workload: every (pixel, sample) path traced by mrt_path_kernel,
+folded per pixel in sample order (draw() semantics) and, for N > 1 GPUs, the tile shards gathered
+to rank 0 over RCCL and scattered into the full framebuffer.  The image is fixed as N grows
+(strong scaling); tile k of the work_queue order belongs to rank k % N.
+
+Prints ONE JSON line (rank 0).  `value` = total rays traced by all ranks / max-over-ranks wall
+time of the K timed steps.  `roofline` prices the dominant kernel (mrt_path_kernel) by the
+algorithmic bytes per ray of SURVEY.md 8(d) over its HIP-event-measured duration.  `cpu_baseline`
+times the reference itself (oracle/_ref/mrt_ref, as shipped) on a bounded sample on this host.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mrays/sec (primary+secondary), Cornell box 32-bounce; per-pixel RMSE vs CPU"
+# algorithmic bytes per ray: sum over the reference's tests per ray of the compact
+# FP32 payload each test reads (aabb 24-32 B, rect 24 B, sphere 16 B, triangle 36 B, instance 20 B)
+B_RAY = {5: 256.0, 9: 434.0, 8: 1251.0, 7: 780.0, 0: 976.0}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", type=int, default=5)
+    ap.add_argument("--width", type=int, default=500)
+    ap.add_argument("--height", type=int, default=500)
+    ap.add_argument("--samples", type=int, default=1024)
+    ap.add_argument("--depth", type=int, default=32)
+    ap.add_argument("--cpu-spp", type=int, default=256, help="spp of the bounded CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_cornell_c2.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    """The reference as shipped (multithreaded work_queue, mode 1, atomic ray counter) on this
+    host's cores, over a bounded sample of the same scene; its own Mrays/s formula."""
+    import oracle
+    threads = int(os.environ.get("MRT_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    b = oracle.ref_binary(exact=False)
+    sample = (f"scene {args.scene}, {args.width}x{args.height}, {args.cpu_spp} spp (of {args.samples}), "
+              f"depth {args.depth}")
+    if b is not None:
+        r = oracle.run_ref(["-scene", args.scene, "-width", args.width, "-height", args.height, "-samples",
+                            args.cpu_spp, "-depth", args.depth, "-threads", threads], exact=False, timeout=900)
+        return {"value": round(r["mrays_per_s"], 3), "unit": "Mrays/s", "cores": threads, "kind": "reference",
+                "sample": sample + f", reference build oracle/_ref/mrt_ref as shipped (-mode 1), "
+                                   f"{r['rays']} rays in {r['trace_seconds']:.2f} s"}
+    import miniraytracer_amd as m
+    sc = m.select_scene(args.scene, args.width / args.height)
+    d = oracle.desc(args.width, args.height, args.cpu_spp, depth=args.depth, threads=threads)
+    t0 = time.perf_counter()
+    _, rays, _, _ = oracle.render(sc, d)
+    dt = time.perf_counter() - t0
+    return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": sample + f", C restatement oracle/liboracle.so, {rays} rays in {dt:.2f} s"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import miniraytracer_amd as m
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    # scene build + upload + workspace: outside the timed region (main.cpp:309 precedes 375)
+    scene = m.select_scene(args.scene, args.width / args.height)
+    rnd = m.Renderer(scene, device=local)
+    desc = m.render_desc(args.width, args.height, args.samples, depth=args.depth, rank=rank, world=world)
+    rnd.prepare(desc)
+    px = m.local_pixels(desc)
+    n_local = len(px)
+    out = torch.zeros((n_local, 4), dtype=torch.float32, device=dev)
+    rays = torch.zeros(1, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    if world > 1:
+        counts = [None] * world
+        dist.all_gather_object(counts, n_local)
+        n_max = max(counts)
+        pad = torch.zeros((n_max, 4), dtype=torch.float32, device=dev)
+        gathered = [torch.zeros((n_max, 4), dtype=torch.float32, device=dev) for _ in range(world)] if rank == 0 else None
+        full = torch.zeros((args.width * args.height, 4), dtype=torch.float32, device=dev) if rank == 0 else None
+        if rank == 0:
+            idx = []
+            for r in range(world):
+                dr = m.render_desc(args.width, args.height, args.samples, depth=args.depth, rank=r, world=world)
+                idx.append(torch.as_tensor(m.local_pixels(dr).astype(np.int64), device=dev))
+
+    def step():
+        rnd.render_device(desc, out.data_ptr(), rays.data_ptr(), stream.cuda_stream)
+        if world > 1:
+            pad[:n_local].copy_(out)
+            dist.gather(pad, gathered, dst=0)  # the one RCCL collective of the data path
+            if rank == 0:
+                for r in range(world):
+                    full.index_copy_(0, idx[r], gathered[r][: counts[r]])
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    rays.zero_()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    total_rays = rays.clone()
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        dist.all_reduce(total_rays, op=dist.ReduceOp.SUM)
+    secs = float(elapsed.item())
+    nrays = int(total_rays.item())
+    rays_per_step_local = int(rays.item()) // max(args.steps, 1)
+
+    # dominant kernel: mrt_path_kernel, HIP events recorded on the launch stream (3 extra renders)
+    kms = []
+    for _ in range(3):
+        rnd.render_device(desc, out.data_ptr(), rays.data_ptr(), stream.cuda_stream)
+        ms, launches = rnd.kernel_ms()
+        kms.append(ms / max(launches, 1))
+    launches = max(launches, 1)
+    k_ms = float(np.mean(kms))
+    b_ray = B_RAY.get(args.scene)
+    roofline = None
+    if b_ray is not None:
+        bytes_per_launch = rays_per_step_local / launches * b_ray
+        achieved = bytes_per_launch / (k_ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(args.pmc_json):
+            pmc = json.load(open(args.pmc_json))
+            if pmc.get("config") == [args.scene, args.width, args.height, args.samples, args.depth]:
+                traffic = pmc.get("hbm_bytes_per_launch")
+        roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                    "kernel": "mrt_path_kernel", "kernel_ms": round(k_ms, 3), "bytes_per_ray": b_ray}
+
+    if rank == 0:
+        res = {
+            "metric": METRIC,
+            "value": round(nrays / secs / 1e6, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(secs / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic scene (reference scene builder, deterministic seeds)",
+            "config": {"workload": f"C2 cornell_box: scene {args.scene}, {args.width}x{args.height}, "
+                                   f"{desc.sqrt_samples ** 2} spp, depth {args.depth}, draw() accumulation",
+                       "scene": args.scene, "width": args.width, "height": args.height,
+                       "spp": desc.sqrt_samples ** 2, "depth": args.depth, "parallelism": f"tiles{world}",
+                       "rays_per_step": nrays // args.steps},
+            "roofline": roofline,
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                res["cpu_baseline"] = cpu_baseline(args)
+            except Exception as e:  # the baseline never blocks the GPU number
+                res["cpu_baseline"] = {"error": str(e)[:200]}
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,126 @@
+/* mrt.h -- C-ABI of the MI355X render path (libmrt.so).  Plain C types only; return codes, never
+ * exceptions; the library owns device memory, the caller owns all host memory.
+ *
+ * What each entry point replaces in the reference (Maraneshi/MiniRayTracer, no FFI of its own --
+ * the seam is the worker-thread spawn in main(), main.cpp:347-382):
+ *
+ *   mrt_default_params / mrt_parse_argv   MRT_Params defaults + ParseArgv   cmdline_parser.h:5-18, cmdline_parser.cpp:78-107
+ *   mrt_select_scene                      select_scene(scenes, aspect)      scene.cpp:25-49 (+ scene 9)
+ *   mrt_scene_upload                      (new) scene -> HBM, once, outside the timed region (main.cpp:309 vs 375)
+ *   mrt_render / mrt_render_device        std::thread(draw|draw2) x N over work_queue + trace()
+ *                                         main.cpp:66-118, 138-243, 347-382; work_queue.cpp:133-175
+ *   mrt_progress                          work_queue::getPercentDone        work_queue.cpp:142-149, 168-175
+ *   rays_out                              G_rayCounter                      main.cpp:55, 68, 403-405
+ *   cancel                                G_isRunning                       main.cpp:54, 180, 235
+ *   mrt_tonemap_argb                      Drago tone map + ARGB32            main.cpp:416-444, vec3.h:327-333
+ *
+ * Threading: one host thread per device; calls on distinct scenes are thread-safe, calls on the
+ * same scene handle are not reentrant.
+ */
+#ifndef MRT_H
+#define MRT_H
+#include <stdint.h>
+#include "mrt_scene.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum mrt_status {
+    MRT_OK = 0,
+    MRT_ERR_INVALID = 1,     /* bad argument / unsupported scene graph */
+    MRT_ERR_NO_DEVICE = 2,   /* no gfx950 device visible */
+    MRT_ERR_HIP = 3,         /* HIP runtime error */
+    MRT_ERR_OOM = 4,
+    MRT_ERR_IO = 5,          /* asset (OBJ / texels) not found or unreadable */
+    MRT_ERR_CANCELLED = 6
+} mrt_status;
+
+/* MRT_Params (cmdline_parser.h:5-18), same defaults and field meaning. */
+typedef struct mrt_params {
+    uint32_t window_width, window_height;
+    uint32_t buffer_width, buffer_height;
+    uint32_t samples_per_pixel;
+    uint32_t tile_size;
+    uint32_t num_threads;     /* reference CPU threads; here: GPUs to shard over (0 = all) */
+    uint32_t max_bounces;
+    uint32_t scene_select;
+    uint32_t threading_mode;  /* 0 = draw() per-pixel mean, 1 = draw2() progressive average */
+    float max_luminance;
+    uint32_t delay;
+    /* additions (not in the reference): */
+    uint64_t seed;            /* path stream-key seed, default = the reference main seed */
+} mrt_params;
+
+void mrt_default_params(mrt_params* p);
+/* Same flags, ranges and warnings as ParseArgv; also -seed.  Returns MRT_OK (the reference never
+ * fails on bad values: it warns and keeps the default). -help prints help and returns INVALID. */
+mrt_status mrt_parse_argv(int argc, char** argv, mrt_params* p);
+
+/* ---- host scene (select_scene) ------------------------------------------------------------ */
+typedef struct mrt_scene_blob mrt_scene_blob;
+/* asset_dir: directory holding bunny.obj / wt_teapot.obj (or their packed .tri forms) and
+ * earthmap.rgb (stb-decoded texels); NULL = $MRT_ASSET_DIR or the package assets/ directory. */
+mrt_status mrt_select_scene(uint32_t scene, float aspect, const char* asset_dir, mrt_scene_blob** out);
+mrt_status mrt_scene_blob_view(const mrt_scene_blob* blob, mrt_scene_view* out);
+/* JSON dump in the schema of oracle/ref/harness.cpp --h-mode scene (parity fixture check). */
+mrt_status mrt_scene_blob_dump_json(const mrt_scene_blob* blob, char** json_out);
+void mrt_free_string(char* s);
+/* Store the parsed records of an OBJ file as a packed <name>.mesh asset (same parser as
+ * mrt_select_scene; used when the .obj itself is not shipped). */
+mrt_status mrt_pack_obj(const char* obj_path, const char* out_path);
+void mrt_scene_blob_free(mrt_scene_blob* blob);
+
+/* ---- device -------------------------------------------------------------------------------- */
+mrt_status mrt_init(int* device_count);
+typedef struct mrt_scene mrt_scene;
+mrt_status mrt_scene_upload(int device, const mrt_scene_view* view, mrt_scene** out);
+void mrt_scene_free(mrt_scene* scene);
+
+typedef struct mrt_render_desc {
+    uint32_t width, height;
+    uint32_t sqrt_samples;   /* spp = sqrt_samples^2, regular grid (main.cpp:319-332) */
+    uint32_t max_bounces;
+    float max_luminance;
+    uint32_t mode;           /* 0 draw() semantics, 1 draw2() semantics */
+    uint64_t seed;           /* stream key: path p -> pcg32_srandom(splitmix64(seed ^ p), p) */
+    uint32_t tile_size;      /* work_queue tiles (work_queue.cpp:64-128) */
+    uint32_t rank, world;    /* this call renders tiles k (inverted-Hilbert order) with k % world == rank */
+    uint32_t chunk_samples;  /* samples per launch (0 = auto, bounded by HBM budget) */
+    uint32_t flags;          /* MRT_RF_* */
+} mrt_render_desc;
+#define MRT_RF_PATH_DEBUG 0x1u /* also keep per-path radiance + ray counts (mrt_render_debug) */
+
+void mrt_default_render_desc(const mrt_params* p, mrt_render_desc* d);
+
+/* Number of pixels this rank owns and their row-major indices (row 0 = bottom, like
+ * G_linearBackBuffer main.cpp:58) in the order mrt_render_device writes them. */
+mrt_status mrt_local_pixels(const mrt_render_desc* d, uint32_t* n_out, uint32_t* pixels_out /* may be NULL */);
+
+/* Render into a host W*H*4 float buffer (x,y,z,0 per pixel; only owned pixels are written). */
+mrt_status mrt_render(mrt_scene* s, const mrt_render_desc* d, float* rgb_out, uint64_t* rays_out,
+                      const volatile int* cancel);
+/* Render into device memory: d_local = n_local*4 floats in mrt_local_pixels order.  Enqueued on
+ * `stream` (hipStream_t or NULL); rays are accumulated into the device uint64 *d_rays; nothing is
+ * synchronised and nothing is allocated when the scene's workspace already fits (capturable). */
+mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, float* d_local, uint64_t* d_rays, void* stream);
+/* Allocate/grow the scene's workspace for d (call once before timing mrt_render_device). */
+mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d);
+/* Per-path radiance (n_local*spp*3 floats, sample-major: [s][local pixel]) and ray counts of the
+ * last render made with MRT_RF_PATH_DEBUG (host copies). */
+mrt_status mrt_render_debug(mrt_scene* s, float* path_rgb, uint32_t* path_rays, uint64_t n_paths);
+mrt_status mrt_progress(mrt_scene* s, float* pct);
+/* Device time of the path-kernel launches of the last render (HIP events recorded on the render's
+ * stream around each mrt_path_kernel launch); waits for the last one. */
+mrt_status mrt_kernel_ms(mrt_scene* s, float* path_ms, uint32_t* launches);
+
+/* Drago adaptive-log tone map of a linear W*H*4 buffer to ARGB32 (main.cpp:416-444, no gamma). */
+mrt_status mrt_tonemap_argb(const float* rgb, uint32_t width, uint32_t height, uint32_t* argb_out);
+
+const char* mrt_strerror(mrt_status s);
+const char* mrt_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,184 @@
+"""miniraytracer_amd -- MI355X (gfx950) render path for MiniRayTracer scenes.
+
+Host-side mirror of the reference's render interface (the names follow the reference):
+
+* ``ParseArgv(argv)`` / ``MRT_Params``      -- cmdline_parser.cpp:78-107, cmdline_parser.h:5-18
+* ``select_scene(scene, aspect)``           -- scene.cpp:25-49 (scenes 0-8, plus 9 = C3 teapot)
+* ``Renderer(scene).render(...)``           -- the draw()/draw2() workers over work_queue
+                                               (main.cpp:138-243, 347-382), on the GPU
+* ``tonemap_argb(img)``                     -- Drago tone map + ARGB32 (main.cpp:416-444)
+
+Everything above the C-ABI is a thin ctypes layer; the render path itself is libmrt.so
+(hand-written HIP for gfx950).  No CPU fallback exists.
+"""
+import ctypes as C
+import json
+import os
+
+import numpy as np
+
+from . import _lib
+from ._lib import MrtError, MrtParams, MrtRenderDesc, MrtSceneView, check, lib
+
+SCENES = ["SCENE_RANDOM_SPHERES", "SCENE_RANDOM_SPHERES_2", "SCENE_TWO_SPHERES", "SCENE_PERLIN_SPHERES",
+          "SCENE_EARTH", "SCENE_CORNELL_BOX", "SCENE_CORNELL_SMOKE", "SCENE_BOOK2_FINAL", "SCENE_TRIANGLES",
+          "SCENE_TEAPOT_CORNELL"]
+MAIN_SEED = 11350390909718046443  # main.cpp:302
+ASSET_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets")
+
+
+def default_params():
+    p = MrtParams()
+    lib().mrt_default_params(C.byref(p))
+    return p
+
+
+def ParseArgv(argv):
+    """Parse reference command-line flags (argv[0] is the program name)."""
+    p = MrtParams()
+    arr = (C.c_char_p * len(argv))(*[a.encode() for a in argv])
+    st = lib().mrt_parse_argv(len(argv), arr, C.byref(p))
+    if st != 0:
+        raise SystemExit(0)  # -help
+    return p
+
+
+class Scene:
+    """Host-side scene built by select_scene (the flattened scene blob)."""
+
+    def __init__(self, handle, scene_id):
+        self._h = C.c_void_p(handle)
+        self.scene_id = scene_id
+        self.view = MrtSceneView()
+        check(lib().mrt_scene_blob_view(self._h, C.byref(self.view)), "mrt_scene_blob_view")
+
+    def dump_json(self):
+        out = C.c_void_p()
+        check(lib().mrt_scene_blob_dump_json(self._h, C.byref(out)), "dump")
+        try:
+            return json.loads(C.cast(out, C.c_char_p).value.decode())
+        finally:
+            lib().mrt_free_string(out)
+
+    def close(self):
+        if self._h:
+            lib().mrt_scene_blob_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def select_scene(scene, aspect, asset_dir=None):
+    h = C.c_void_p()
+    ad = (asset_dir or os.environ.get("MRT_ASSET_DIR") or ASSET_DIR).encode()
+    check(lib().mrt_select_scene(int(scene), float(aspect), ad, C.byref(h)), f"select_scene({scene})")
+    return Scene(h.value, scene)
+
+
+def render_desc(width, height, samples, depth=32, max_luminance=1000.0, mode=0, seed=MAIN_SEED, tile_size=32,
+                rank=0, world=1, chunk_samples=0, flags=0):
+    """Render description; `samples` is floored to a perfect square like main.cpp:319-320."""
+    sq = int(np.sqrt(np.float32(samples)))
+    return MrtRenderDesc(width, height, sq, depth, max_luminance, mode, seed, tile_size, rank, world,
+                         chunk_samples, flags)
+
+
+def local_pixels(desc):
+    n = C.c_uint32()
+    check(lib().mrt_local_pixels(C.byref(desc), C.byref(n), None), "local_pixels")
+    px = np.zeros(n.value, dtype=np.uint32)
+    check(lib().mrt_local_pixels(C.byref(desc), C.byref(n), px.ctypes.data), "local_pixels")
+    return px
+
+
+def device_count():
+    n = C.c_int()
+    st = lib().mrt_init(C.byref(n))
+    return n.value if st == 0 else 0
+
+
+class Renderer:
+    """A scene resident in HBM of one device."""
+
+    def __init__(self, scene, device=0):
+        n = C.c_int()
+        check(lib().mrt_init(C.byref(n)), "mrt_init")
+        self._h = C.c_void_p()
+        check(lib().mrt_scene_upload(device, C.byref(scene.view), C.byref(self._h)), "mrt_scene_upload")
+        self.scene = scene
+
+    def render(self, desc):
+        """Blocking render into a host float32 (H, W, 4) image (row 0 = bottom); returns (img, rays)."""
+        img = np.zeros((desc.height, desc.width, 4), dtype=np.float32)
+        rays = C.c_uint64()
+        check(lib().mrt_render(self._h, C.byref(desc), img.ctypes.data, C.byref(rays), None), "mrt_render")
+        return img, rays.value
+
+    def prepare(self, desc):
+        check(lib().mrt_prepare(self._h, C.byref(desc)), "mrt_prepare")
+
+    def render_device(self, desc, d_out_ptr, d_rays_ptr, stream_ptr=0):
+        """Enqueue a render into device memory (torch tensor data_ptr()s) on a HIP stream."""
+        check(lib().mrt_render_device(self._h, C.byref(desc), C.c_void_p(d_out_ptr), C.c_void_p(d_rays_ptr),
+                                      C.c_void_p(stream_ptr)), "mrt_render_device")
+
+    def kernel_ms(self):
+        """(total ms, launches) of the path kernel in the last render (HIP events on its stream)."""
+        ms, n = C.c_float(), C.c_uint32()
+        check(lib().mrt_kernel_ms(self._h, C.byref(ms), C.byref(n)), "mrt_kernel_ms")
+        return ms.value, n.value
+
+    def paths(self, n_paths):
+        """Per-path radiance and ray counts of the last MRT_RF_PATH_DEBUG render ([s][local pixel])."""
+        rgb = np.zeros((n_paths, 3), dtype=np.float32)
+        rays = np.zeros(n_paths, dtype=np.uint32)
+        check(lib().mrt_render_debug(self._h, rgb.ctypes.data, rays.ctypes.data, n_paths), "mrt_render_debug")
+        return rgb, rays
+
+    def close(self):
+        if self._h:
+            lib().mrt_scene_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def tonemap_argb(img):
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    h, w = img.shape[:2]
+    out = np.zeros((h, w), dtype=np.uint32)
+    check(lib().mrt_tonemap_argb(img.ctypes.data, w, h, out.ctypes.data), "tonemap")
+    return out
+
+
+def write_pfm(path, img):
+    """Linear PFM, rows bottom-to-top (the PFM convention == G_linearBackBuffer order)."""
+    h, w = img.shape[:2]
+    with open(path, "wb") as f:
+        f.write(f"PF\n{w} {h}\n-1.0\n".encode())
+        f.write(np.ascontiguousarray(img[..., :3], dtype="<f4").tobytes())
+
+
+def read_pfm(path):
+    with open(path, "rb") as f:
+        data = f.read()
+    parts = data.split(b"\n", 3)
+    w, h = map(int, parts[1].split())
+    return np.frombuffer(parts[3], dtype="<f4").reshape(h, w, 3)
+
+
+def write_ppm(path, argb):
+    """Tone-mapped 8-bit PPM, displayed top row first (SDL_FLIP_VERTICAL, platform_linux.cpp:84)."""
+    h, w = argb.shape
+    rgb = np.stack([(argb >> 16) & 255, (argb >> 8) & 255, argb & 255], axis=-1).astype(np.uint8)[::-1]
+    with open(path, "wb") as f:
+        f.write(f"P6\n{w} {h}\n255\n".encode())
+        f.write(rgb.tobytes())

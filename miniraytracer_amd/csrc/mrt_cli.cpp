@@ -1,0 +1,92 @@
+// mrt_cli.cpp -- headless command-line driver with the reference's flags (cmdline_parser.cpp:78-123)
+// in place of the SDL window loop of main() (main.cpp:283-498): builds the scene, renders it on the
+// MI355X(s) through the C-ABI, prints the reference's "Trace: ... Mrays/s" line (main.cpp:403-406)
+// and writes the image (-o out.pfm: linear; -o out.ppm: Drago tone map, main.cpp:416-444).
+//
+// -threads N shards the work_queue tiles over N GPUs (one host thread per device, tile k -> GPU
+// k % N); 0 = every visible GPU.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/mrt.h"
+
+static int fail(const char* what, mrt_status s) {
+    fprintf(stderr, "%s: %s (%s)\n", what, mrt_strerror(s), mrt_last_error());
+    return 1;
+}
+
+int main(int argc, char** argv) {
+    mrt_params p;
+    if (mrt_parse_argv(argc, argv, &p) != MRT_OK) return 0;  // -help
+    const char* out = nullptr;
+    for (int i = 1; i + 1 < argc; i++)
+        if (!strcmp(argv[i], "-o")) out = argv[i + 1];
+
+    auto t_gen = std::chrono::steady_clock::now();
+    mrt_scene_blob* blob = nullptr;
+    mrt_status st = mrt_select_scene(p.scene_select, float(p.buffer_width) / float(p.buffer_height), nullptr, &blob);
+    if (st) return fail("select_scene", st);
+    double gen_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_gen).count();
+    mrt_scene_view view;
+    mrt_scene_blob_view(blob, &view);
+
+    int ndev = 0;
+    if ((st = mrt_init(&ndev))) return fail("mrt_init", st);
+    int world = p.num_threads ? (int)p.num_threads : ndev;
+    if (world > ndev) world = ndev;
+
+    std::vector<mrt_scene*> scenes(world, nullptr);
+    std::vector<mrt_render_desc> descs(world);
+    for (int r = 0; r < world; r++) {
+        if ((st = mrt_scene_upload(r, &view, &scenes[r]))) return fail("scene_upload", st);
+        mrt_default_render_desc(&p, &descs[r]);
+        descs[r].rank = (uint32_t)r;
+        descs[r].world = (uint32_t)world;
+        if ((st = mrt_prepare(scenes[r], &descs[r]))) return fail("prepare", st);
+    }
+    std::vector<float> img((size_t)p.buffer_width * p.buffer_height * 4, 0.0f);
+    std::vector<uint64_t> rays(world, 0);
+    std::vector<mrt_status> sts(world, MRT_OK);
+
+    auto t0 = std::chrono::steady_clock::now();  // main.cpp:375
+    std::vector<std::thread> th;
+    for (int r = 0; r < world; r++)
+        th.emplace_back([&, r] { sts[r] = mrt_render(scenes[r], &descs[r], img.data(), &rays[r], nullptr); });
+    for (auto& t : th) t.join();
+    double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    for (int r = 0; r < world; r++)
+        if (sts[r]) return fail("render", sts[r]);
+    uint64_t total = 0;
+    for (uint64_t x : rays) total += x;
+    printf("MiniRayTracer - Scene: %.0fms - Trace: %.2fs - %.3f Mrays/s | %.3f us/ray  [%d x MI355X, %u spp]\n", gen_ms, secs,
+           (total * 0.000001) / secs, (secs * 1000000.0) / (double)total, world, descs[0].sqrt_samples * descs[0].sqrt_samples);
+
+    if (out) {
+        std::string o = out;
+        FILE* f = fopen(out, "wb");
+        if (!f) return fail("open output", MRT_ERR_IO);
+        if (o.size() > 4 && o.substr(o.size() - 4) == ".ppm") {
+            std::vector<uint32_t> argb((size_t)p.buffer_width * p.buffer_height);
+            mrt_tonemap_argb(img.data(), p.buffer_width, p.buffer_height, argb.data());
+            fprintf(f, "P6\n%u %u\n255\n", p.buffer_width, p.buffer_height);
+            for (int y = (int)p.buffer_height - 1; y >= 0; y--)  // display is flipped (platform_linux.cpp:84)
+                for (uint32_t x = 0; x < p.buffer_width; x++) {
+                    uint32_t c = argb[(size_t)y * p.buffer_width + x];
+                    unsigned char px[3] = {(unsigned char)(c >> 16), (unsigned char)(c >> 8), (unsigned char)c};
+                    fwrite(px, 1, 3, f);
+                }
+        } else {
+            fprintf(f, "PF\n%u %u\n-1.0\n", p.buffer_width, p.buffer_height);
+            for (size_t i = 0; i < (size_t)p.buffer_width * p.buffer_height; i++) fwrite(&img[i * 4], 4, 3, f);
+        }
+        fclose(f);
+    }
+    for (auto* s : scenes) mrt_scene_free(s);
+    mrt_scene_blob_free(blob);
+    return 0;
+}

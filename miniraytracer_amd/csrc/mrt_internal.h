@@ -1,0 +1,18 @@
+// mrt_internal.h -- library-internal helpers shared by the host translation units.
+#pragma once
+#include <string>
+#include <vector>
+#include "../../include/mrt.h"
+
+mrt_status mrt_internal_fail(mrt_status s, const char* msg);
+std::string mrt_internal_package_dir();
+
+// work_queue tile list in the reference order: row-major tiles re-ordered along the inverted
+// Hilbert curve (work_queue.cpp:64-128).  Each entry: xMin, xMax, yMin, yMax.
+struct mrt_tile {
+    uint32_t xmin, xmax, ymin, ymax;
+};
+std::vector<mrt_tile> mrt_internal_tiles(uint32_t width, uint32_t height, uint32_t tile_size);
+// Pixels (row-major index, row 0 = bottom) owned by `rank` of `world`: tiles k % world == rank,
+// each tile scanned row by row (the order draw() visits them, main.cpp:148-149).
+std::vector<uint32_t> mrt_internal_local_pixels(const mrt_render_desc* d);

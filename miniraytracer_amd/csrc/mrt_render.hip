@@ -1,0 +1,465 @@
+// mrt_render.hip -- the MI355X render path behind the C-ABI (include/mrt.h).
+//
+// Kernels (DESIGN.md "Kernels"):
+//   mrt_path_kernel   persistent waves pull 64-path batches from one device counter (one atomic
+//                     per wave per batch, like work_queue::getWork pulls a tile,
+//                     work_queue.cpp:158-166) and run trace() for each lane's path to completion;
+//                     per-path radiance is written sample-major [s][local pixel] (coalesced).
+//   mrt_fold_kernel   per pixel, folds the chunk's samples in sample order into the running
+//                     accumulator with draw() (mode 0, main.cpp:161-167) or draw2() (mode 1,
+//                     main.cpp:212-229) semantics -- bit-for-bit the reference's sequential sum.
+//   mrt_final_kernel  mode 0: color /= ns, luminance clamp (main.cpp:168-173); writes the float4
+//                     output in local-pixel order.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mrt_internal.h"
+#include "mrt_shade.h"
+
+using namespace mrtd;
+
+#define HIPCHK(x)                                                                                   \
+    do {                                                                                            \
+        hipError_t e_ = (x);                                                                        \
+        if (e_ != hipSuccess) return mrt_internal_fail(MRT_ERR_HIP, (std::string(#x) + ": " + hipGetErrorString(e_)).c_str()); \
+    } while (0)
+
+struct PathParams {
+    const DScene* __restrict__ S;  // device copy (scalar-loaded)
+    const uint32_t* __restrict__ pixels;  // local pixel -> row-major pixel index
+    uint32_t npix;                        // local pixel count
+    uint32_t width, height, sq, ns;
+    uint32_t s0;                          // first sample of this chunk
+    uint64_t n_paths;                     // npix * chunk samples
+    uint64_t seed;
+    uint32_t max_bounces;
+    float* __restrict__ rad;              // n_paths * 3 floats, [s - s0][lp]
+    uint32_t* __restrict__ path_rays;     // optional (debug): n_paths
+    uint64_t* __restrict__ counter;       // work counter (paths handed out)
+    unsigned long long* __restrict__ rays;
+    float4* __restrict__ lev;             // max_bounces rows x lev_stride
+    size_t lev_stride;                    // = total threads of the grid
+};
+
+__global__ void __launch_bounds__(256) mrt_path_kernel(PathParams P) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t my_rays = 0;
+    for (;;) {
+        uint64_t base = 0;
+        if (lane == 0) base = atomicAdd((unsigned long long*)P.counter, 64ull);
+        base = __shfl(base, 0);
+        if (base >= P.n_paths) break;
+        uint64_t p = base + lane;
+        if (p < P.n_paths) {
+            uint32_t sl = (uint32_t)(p / P.npix);
+            uint32_t lp = (uint32_t)(p - (uint64_t)sl * P.npix);
+            uint32_t s = P.s0 + sl;
+            uint32_t pix = P.pixels[lp];
+            uint32_t x = pix % P.width, y = pix / P.width;
+            // regular-grid sample offsets (main.cpp:324-331): s = i*sq + j
+            uint32_t i = s / P.sq, j = s - i * P.sq;
+            float dx = ((float)i + 0.5f) / (float)P.sq;
+            float dy = ((float)j + 0.5f) / (float)P.sq;
+            float u = ((float)x + dx) / (float)P.width;
+            float v = ((float)y + dy) / (float)P.height;
+            uint64_t path_id = (uint64_t)pix * P.ns + s;
+            Pcg rng;
+            pcg_seed(rng, splitmix64(P.seed ^ path_id), path_id);
+            PathOut o = trace_path(*P.S, rng, u, v, P.max_bounces, P.lev + slot, P.lev_stride);
+            float* dst = P.rad + p * 3;
+            dst[0] = o.L.x;
+            dst[1] = o.L.y;
+            dst[2] = o.L.z;
+            if (P.path_rays) P.path_rays[p] = o.rays;
+            my_rays += o.rays;
+        }
+    }
+    // one 64-bit add per wave
+    for (int off = 32; off > 0; off >>= 1) my_rays += __shfl_xor(my_rays, off);
+    if (lane == 0 && my_rays) atomicAdd(P.rays, (unsigned long long)my_rays);
+}
+
+__device__ __forceinline__ float lum3(f3 c) { return (c.x * 0.212655f + c.y * 0.715158f) + c.z * 0.072187f; }
+
+__global__ void __launch_bounds__(256) mrt_fold_kernel(const float* __restrict__ rad, float4* __restrict__ acc, uint32_t npix, uint32_t s0,
+                                                      uint32_t s1, uint32_t mode, float max_lum) {
+    uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
+    if (lp >= npix) return;
+    float4 a = acc[lp];
+    f3 c{a.x, a.y, a.z};
+    for (uint32_t s = s0; s < s1; s++) {
+        const float* q = rad + ((size_t)(s - s0) * npix + lp) * 3;
+        f3 smp{q[0], q[1], q[2]};
+        if (mode == 0) {
+            if (!finite3(smp)) smp = c;
+            c = add(c, smp);
+        } else {
+            if (!finite3(smp)) smp = s > 0 ? c : f3{0, 0, 0};
+            if (s > 0) smp = add(c, mulf(sub(smp, c), 1.0f / ((float)s + 1.0f)));
+            float l = lum3(smp);
+            if (l > max_lum) smp = mulf(smp, max_lum / l);
+            c = smp;
+        }
+    }
+    acc[lp] = make_float4(c.x, c.y, c.z, 0.0f);
+}
+
+__global__ void __launch_bounds__(256) mrt_final_kernel(const float4* __restrict__ acc, float4* __restrict__ out, uint32_t npix, uint32_t ns,
+                                                       uint32_t mode, float max_lum) {
+    uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
+    if (lp >= npix) return;
+    float4 a = acc[lp];
+    f3 c{a.x, a.y, a.z};
+    if (mode == 0) {
+        c = divf(c, (float)ns);
+        float l = lum3(c);
+        if (l > max_lum) c = mulf(c, max_lum / l);
+    }
+    out[lp] = make_float4(c.x, c.y, c.z, 0.0f);
+}
+
+// --------------------------------------------------------------------------------------------
+// host side
+// --------------------------------------------------------------------------------------------
+struct mrt_scene {
+    int device = 0;
+    DScene S{};
+    DScene* d_S = nullptr;
+    std::vector<void*> allocs;
+    uint32_t n_nodes = 0;
+    // workspace
+    mrt_render_desc wdesc{};
+    bool have_ws = false;
+    uint32_t npix = 0, chunk = 0;
+    uint32_t* d_pixels = nullptr;
+    float* d_rad = nullptr;
+    uint32_t* d_path_rays = nullptr;
+    float4* d_acc = nullptr;
+    float4* d_lev = nullptr;
+    size_t lev_stride = 0;
+    uint64_t* d_counter = nullptr;
+    unsigned long long* d_rays = nullptr;
+    int grid = 0;
+    std::vector<hipEvent_t> ev;  // [2*k]: start/stop of path-kernel launch k of the last render
+    uint32_t n_launch = 0;
+    size_t rad_cap = 0, acc_cap = 0, lev_cap = 0, px_cap = 0, pr_cap = 0;
+    uint64_t last_paths = 0;
+};
+
+static mrt_status dev_alloc(mrt_scene* s, void** p, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess) return mrt_internal_fail(e == hipErrorOutOfMemory ? MRT_ERR_OOM : MRT_ERR_HIP, "hipMalloc failed");
+    s->allocs.push_back(*p);
+    return MRT_OK;
+}
+static mrt_status upload(mrt_scene* s, const void* src, size_t bytes, void** dst) {
+    void* p = nullptr;
+    mrt_status st = dev_alloc(s, &p, bytes);
+    if (st) return st;
+    if (bytes) {
+        hipError_t e = hipMemcpy(p, src, bytes, hipMemcpyHostToDevice);
+        if (e != hipSuccess) return mrt_internal_fail(MRT_ERR_HIP, "hipMemcpy upload failed");
+    }
+    *dst = p;
+    return MRT_OK;
+}
+
+extern "C" mrt_status mrt_init(int* device_count) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) {
+        if (device_count) *device_count = 0;
+        return mrt_internal_fail(MRT_ERR_NO_DEVICE, "no HIP device visible");
+    }
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, 0));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return mrt_internal_fail(MRT_ERR_NO_DEVICE, (std::string("device is ") + prop.gcnArchName + ", libmrt is built for gfx950").c_str());
+    if (device_count) *device_count = n;
+    return MRT_OK;
+}
+
+// graph checks on the host, so the fixed-size device stacks can never overflow
+static bool needs_uv_tex(const mrt_scene_view* v, uint32_t t, int guard = 0) {
+    if (t == MRT_NONE || t >= v->n_textures || guard > 16) return false;
+    const mrt_texture& T = v->textures[t];
+    if (T.kind == MRT_T_IMAGE) return true;
+    if (T.kind == MRT_T_CHECKER) return needs_uv_tex(v, T.a, guard + 1) || needs_uv_tex(v, T.b, guard + 1);
+    return false;
+}
+struct GraphCheck {
+    const mrt_scene_view* v;
+    int max_frames = 0, max_rays = 0;
+    bool ok = true;
+    std::string why;
+    void walk(uint32_t id, int frames, int rays, bool in_volume) {
+        if (!ok) return;
+        if (id >= v->n_nodes) { ok = false; why = "node index out of range"; return; }
+        const mrt_node& n = v->nodes[id];
+        uint32_t k = n.kind & 0xFF;
+        if (k == MRT_K_SPHERE || k == MRT_K_XY || k == MRT_K_XZ || k == MRT_K_YZ || k == MRT_K_MESH) return;
+        frames++;
+        max_frames = std::max(max_frames, frames);
+        switch (k) {
+        case MRT_K_LIST: for (uint32_t i = 0; i < n.b; i++) walk(v->children[n.a + i], frames, rays, in_volume); break;
+        case MRT_K_BVH: walk(n.a, frames, rays, in_volume); walk(n.b, frames, rays, in_volume); break;
+        case MRT_K_TRANSLATE: case MRT_K_ROTY:
+            max_rays = std::max(max_rays, rays + 1);
+            walk(n.a, frames, rays + 1, in_volume);
+            break;
+        case MRT_K_VOLUME:
+            if (in_volume) { ok = false; why = "nested constant_volume"; return; }
+            walk(n.a, frames, rays, true);
+            break;
+        default: ok = false; why = "unknown node kind";
+        }
+    }
+};
+static int mesh_depth(const mrt_scene_view* v, uint32_t ni, int guard) {
+    if (guard > 64) return 1000;
+    const mrt_mesh_node& m = v->mesh_nodes[ni];
+    if (m.count_order & 0xFFFFFFu) return 1;
+    return 1 + std::max(mesh_depth(v, m.left_or_first, guard + 1), mesh_depth(v, m.left_or_first + 1, guard + 1));
+}
+
+extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_scene** out) {
+    if (!v || !out || v->root >= v->n_nodes) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_scene_upload: bad view");
+    GraphCheck gc{v};
+    gc.walk(v->root, 0, 0, false);
+    if (!gc.ok) return mrt_internal_fail(MRT_ERR_INVALID, gc.why.c_str());
+    if (gc.max_frames > MRT_FRAMES || gc.max_rays > MRT_RAYS) return mrt_internal_fail(MRT_ERR_INVALID, "scene graph deeper than the device stacks");
+    for (uint32_t i = 0; i < v->n_nodes; i++) {
+        const mrt_node& n = v->nodes[i];
+        if ((n.kind & 0xFF) == MRT_K_MESH && 2 * mesh_depth(v, n.a, 0) + 2 > MRT_MESH_STACK)
+            return mrt_internal_fail(MRT_ERR_INVALID, "mesh BVH deeper than the device stack");
+    }
+    if (v->biased != MRT_NONE) {
+        const mrt_node& b = v->nodes[v->biased];
+        if ((b.kind & 0xFF) == MRT_K_LIST)
+            for (uint32_t i = 0; i < b.b; i++) {
+                uint32_t k = v->nodes[v->children[b.a + i]].kind & 0xFF;
+                if (k == MRT_K_LIST) return mrt_internal_fail(MRT_ERR_INVALID, "nested biased object_list");
+            }
+    }
+    HIPCHK(hipSetDevice(device));
+    mrt_scene* s = new mrt_scene();
+    s->device = device;
+    // node flags: NEEDUV where the material samples an image texture
+    std::vector<mrt_node> nodes(v->nodes, v->nodes + v->n_nodes);
+    for (mrt_node& n : nodes) {
+        uint32_t k = n.kind & 0xFF;
+        if ((k == MRT_K_SPHERE || k == MRT_K_XY || k == MRT_K_XZ || k == MRT_K_YZ) && n.mat < v->n_materials &&
+            needs_uv_tex(v, v->materials[n.mat].tex))
+            n.kind |= MRT_F_NEEDUV << 16;
+    }
+    mrt_status st;
+    DScene& S = s->S;
+#define UP(src, n, dst) { void* t_ = nullptr; if ((st = upload(s, src, (size_t)(n) * sizeof(*(src)), &t_))) { mrt_scene_free(s); return st; } *(dst) = (decltype(+*(dst)))t_; }
+    UP(nodes.data(), nodes.size(), &S.nodes);
+    UP(v->children, v->n_children, &S.children);
+    UP(v->mesh_nodes, v->n_mesh_nodes, &S.mnodes);
+    UP((const float4*)v->tri_geo, (size_t)v->n_tris * 3, &S.tri_geo);
+    UP((const float4*)v->tri_nrm, (size_t)v->n_tris * 3, &S.tri_nrm);
+    UP(v->materials, v->n_materials, &S.mats);
+    UP(v->textures, v->n_textures, &S.texs);
+    UP((const float4*)v->perlin_ranvec, 256, &S.ranvec);
+    UP(v->perlin_perm, 768, &S.perm);
+    UP(v->texels, (size_t)v->n_texels, &S.texels);
+#undef UP
+    S.root = v->root;
+    S.biased = v->biased;
+    S.sky = v->sky;
+    S.cam = v->camera;
+    s->n_nodes = v->n_nodes;
+    void* p;
+    if ((st = upload(s, &s->S, sizeof(DScene), &p))) { mrt_scene_free(s); return st; }
+    s->d_S = (DScene*)p;
+    if ((st = dev_alloc(s, &p, 64))) { mrt_scene_free(s); return st; }
+    s->d_counter = (uint64_t*)p;
+    s->d_rays = (unsigned long long*)((char*)p + 16);
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    // persistent grid: 4 x 256-thread workgroups per CU (VGPR-limited residency)
+    s->grid = prop.multiProcessorCount * 4;
+    *out = s;
+    return MRT_OK;
+}
+
+extern "C" void mrt_scene_free(mrt_scene* s) {
+    if (!s) return;
+    (void)hipSetDevice(s->device);
+    for (void* p : s->allocs) (void)hipFree(p);
+    for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
+    for (void* p : {(void*)s->d_pixels, (void*)s->d_rad, (void*)s->d_path_rays, (void*)s->d_acc, (void*)s->d_lev})
+        if (p) (void)hipFree(p);
+    delete s;
+}
+
+static uint32_t auto_chunk(uint32_t npix, uint32_t ns) {
+    // keep the per-chunk radiance buffer within ~4 GiB of HBM (288 GB per MI355X)
+    const size_t budget = (size_t)4 << 30;
+    size_t per_sample = (size_t)npix * 12;
+    size_t c = per_sample ? budget / per_sample : ns;
+    if (c < 1) c = 1;
+    return (uint32_t)std::min<size_t>(c, ns);
+}
+
+static mrt_status grow(void** p, size_t* cap, size_t bytes) {
+    if (*cap >= bytes && *p) return MRT_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    hipError_t e = hipMalloc(p, bytes ? bytes : 16);
+    if (e != hipSuccess) return mrt_internal_fail(MRT_ERR_OOM, "workspace allocation failed");
+    *cap = bytes;
+    return MRT_OK;
+}
+
+static bool same_layout(const mrt_render_desc& a, const mrt_render_desc& b) {
+    return a.width == b.width && a.height == b.height && a.tile_size == b.tile_size && a.rank == b.rank && a.world == b.world;
+}
+
+extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
+    if (!s || !d || d->width == 0 || d->height == 0 || d->sqrt_samples == 0 || (d->world && d->rank >= d->world))
+        return mrt_internal_fail(MRT_ERR_INVALID, "mrt_prepare: bad desc");
+    HIPCHK(hipSetDevice(s->device));
+    mrt_status st;
+    bool relayout = !s->have_ws || !same_layout(s->wdesc, *d);
+    uint32_t ns = d->sqrt_samples * d->sqrt_samples;
+    if (relayout) {
+        std::vector<uint32_t> px = mrt_internal_local_pixels(d);
+        s->npix = (uint32_t)px.size();
+        if ((st = grow((void**)&s->d_pixels, &s->px_cap, px.size() * 4))) return st;
+        HIPCHK(hipMemcpy(s->d_pixels, px.data(), px.size() * 4, hipMemcpyHostToDevice));
+    }
+    s->chunk = d->chunk_samples ? std::min(d->chunk_samples, ns) : auto_chunk(s->npix, ns);
+    if (d->flags & MRT_RF_PATH_DEBUG) s->chunk = ns;  // debug keeps every path
+    size_t paths = (size_t)s->npix * s->chunk;
+    if ((st = grow((void**)&s->d_rad, &s->rad_cap, paths * 12))) return st;
+    if ((st = grow((void**)&s->d_acc, &s->acc_cap, (size_t)s->npix * 16))) return st;
+    if (d->flags & MRT_RF_PATH_DEBUG)
+        if ((st = grow((void**)&s->d_path_rays, &s->pr_cap, paths * 4))) return st;
+    s->lev_stride = (size_t)s->grid * 256;
+    size_t levrows = std::max<uint32_t>(d->max_bounces, 1);
+    if ((st = grow((void**)&s->d_lev, &s->lev_cap, levrows * s->lev_stride * 16))) return st;
+    uint32_t launches = (ns + s->chunk - 1) / s->chunk;
+    while (s->ev.size() < 2 * (size_t)launches) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        s->ev.push_back(e);
+    }
+    s->wdesc = *d;
+    s->have_ws = true;
+    return MRT_OK;
+}
+
+extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, float* d_local, uint64_t* d_rays, void* stream) {
+    mrt_status st = mrt_prepare(s, d);
+    if (st) return st;
+    hipStream_t q = (hipStream_t)stream;
+    uint32_t ns = d->sqrt_samples * d->sqrt_samples;
+    HIPCHK(hipMemsetAsync(s->d_acc, 0, (size_t)s->npix * 16, q));
+    s->n_launch = 0;
+    for (uint32_t s0 = 0; s0 < ns; s0 += s->chunk) {
+        uint32_t s1 = std::min(ns, s0 + s->chunk);
+        PathParams P{};
+        P.S = s->d_S;
+        P.pixels = s->d_pixels;
+        P.npix = s->npix;
+        P.width = d->width;
+        P.height = d->height;
+        P.sq = d->sqrt_samples;
+        P.ns = ns;
+        P.s0 = s0;
+        P.n_paths = (uint64_t)s->npix * (s1 - s0);
+        P.seed = d->seed;
+        P.max_bounces = d->max_bounces;
+        P.rad = s->d_rad;
+        P.path_rays = (d->flags & MRT_RF_PATH_DEBUG) ? s->d_path_rays : nullptr;
+        P.counter = s->d_counter;
+        P.rays = d_rays ? (unsigned long long*)d_rays : s->d_rays;
+        P.lev = s->d_lev;
+        P.lev_stride = s->lev_stride;
+        HIPCHK(hipMemsetAsync(s->d_counter, 0, 8, q));
+        HIPCHK(hipEventRecord(s->ev[2 * s->n_launch], q));
+        hipLaunchKernelGGL(mrt_path_kernel, dim3(s->grid), dim3(256), 0, q, P);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(s->ev[2 * s->n_launch + 1], q));
+        s->n_launch++;
+        uint32_t blocks = (s->npix + 255) / 256;
+        hipLaunchKernelGGL(mrt_fold_kernel, dim3(blocks), dim3(256), 0, q, s->d_rad, s->d_acc, s->npix, s0, s1, d->mode, d->max_luminance);
+        HIPCHK(hipGetLastError());
+        s->last_paths = P.n_paths;
+    }
+    uint32_t blocks = (s->npix + 255) / 256;
+    hipLaunchKernelGGL(mrt_final_kernel, dim3(blocks), dim3(256), 0, q, s->d_acc, (float4*)d_local, s->npix, ns, d->mode, d->max_luminance);
+    HIPCHK(hipGetLastError());
+    return MRT_OK;
+}
+
+extern "C" mrt_status mrt_render(mrt_scene* s, const mrt_render_desc* d, float* rgb_out, uint64_t* rays_out, const volatile int* cancel) {
+    if (!s || !d || !rgb_out) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_render: null");
+    mrt_status st = mrt_prepare(s, d);
+    if (st) return st;
+    float* d_out = nullptr;
+    HIPCHK(hipMalloc(&d_out, (size_t)s->npix * 16 + 16));
+    HIPCHK(hipMemset(s->d_rays, 0, 8));
+    if (cancel && *cancel) {
+        (void)hipFree(d_out);
+        return mrt_internal_fail(MRT_ERR_CANCELLED, "cancelled");
+    }
+    st = mrt_render_device(s, d, d_out, (uint64_t*)s->d_rays, nullptr);
+    if (st) {
+        (void)hipFree(d_out);
+        return st;
+    }
+    std::vector<float> local((size_t)s->npix * 4);
+    std::vector<uint32_t> px = mrt_internal_local_pixels(d);
+    hipError_t e = hipMemcpy(local.data(), d_out, local.size() * 4, hipMemcpyDeviceToHost);
+    (void)hipFree(d_out);
+    if (e != hipSuccess) return mrt_internal_fail(MRT_ERR_HIP, hipGetErrorString(e));
+    for (size_t i = 0; i < px.size(); i++) memcpy(rgb_out + (size_t)px[i] * 4, &local[i * 4], 16);
+    uint64_t rays = 0;
+    HIPCHK(hipMemcpy(&rays, s->d_rays, 8, hipMemcpyDeviceToHost));
+    if (rays_out) *rays_out = rays;
+    return MRT_OK;
+}
+
+extern "C" mrt_status mrt_render_debug(mrt_scene* s, float* path_rgb, uint32_t* path_rays, uint64_t n_paths) {
+    if (!s || !(s->wdesc.flags & MRT_RF_PATH_DEBUG) || n_paths != s->last_paths)
+        return mrt_internal_fail(MRT_ERR_INVALID, "mrt_render_debug: no debug render of that size");
+    HIPCHK(hipSetDevice(s->device));
+    if (path_rgb) HIPCHK(hipMemcpy(path_rgb, s->d_rad, n_paths * 12, hipMemcpyDeviceToHost));
+    if (path_rays) HIPCHK(hipMemcpy(path_rays, s->d_path_rays, n_paths * 4, hipMemcpyDeviceToHost));
+    return MRT_OK;
+}
+
+extern "C" mrt_status mrt_progress(mrt_scene* s, float* pct) {
+    if (!s || !pct) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_progress: null");
+    uint64_t c = 0;
+    HIPCHK(hipMemcpy(&c, s->d_counter, 8, hipMemcpyDeviceToHost));
+    *pct = s->last_paths ? std::min(100.0f, (float)(c * 100.0 / (double)s->last_paths)) : 0.0f;
+    return MRT_OK;
+}
+
+extern "C" mrt_status mrt_kernel_ms(mrt_scene* s, float* path_ms, uint32_t* launches) {
+    if (!s || !path_ms) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_kernel_ms: null");
+    HIPCHK(hipSetDevice(s->device));
+    float total = 0;
+    for (uint32_t k = 0; k < s->n_launch; k++) {
+        HIPCHK(hipEventSynchronize(s->ev[2 * k + 1]));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, s->ev[2 * k], s->ev[2 * k + 1]));
+        total += ms;
+    }
+    *path_ms = total;
+    if (launches) *launches = s->n_launch;
+    return MRT_OK;
+}

@@ -221,7 +221,7 @@ scene harness_select_scene(scenes choose, float aspect) {
 static void* vt(const void* o) { return *(void* const*)o; }
 
 struct VT {
-    void *ol_so, *ol_sp, *bvh_sp, *bvh_box, *pod_tri, *tr, *roty, *sph, *xy, *xz, *yz, *bx, *vol;
+    void *ol_so, *ol_sp, *ol_bx, *bvh_sp, *bvh_box, *pod_tri, *tr, *roty, *sph, *xy, *xz, *yz, *bx, *vol;
     void *lam, *iso, *met, *die, *lig;
     void *ctex, *chk, *per, *img;
 };
@@ -240,6 +240,7 @@ static VT vts() {
     triangle* tri = new triangle(Vec3(0, 0, 0), Vec3(1, 0, 0), Vec3(0, 1, 0), m);
     v.ol_so = vt(new object_list<scene_object>(ol, 1, 0, 0));
     v.ol_sp = vt(new object_list<sphere>(sl, 1, 0, 0));
+    v.ol_bx = vt(new object_list<box>(bl, 1, 0, 0));
     v.bvh_sp = vt(new bvh_node<sphere>(sl, 1, 0, 0));
     v.bvh_box = vt(new bvh_node<box>(bl, 1, 0, 0));
     v.pod_tri = vt(new pod_bvh<triangle>(tri, 1, 0, 0));
@@ -314,6 +315,7 @@ static std::string dump_obj(const scene_object* o) {
     void* p = vt(o);
     if (p == v.ol_so) return dump_list((const object_list<scene_object>*)o);
     if (p == v.ol_sp) return dump_list((const object_list<sphere>*)o);
+    if (p == v.ol_bx) return dump_list((const object_list<box>*)o);
     if (p == v.bvh_sp) return dump_bvh((const bvh_node<sphere>*)o);
     if (p == v.bvh_box) return dump_bvh((const bvh_node<box>*)o);
     if (p == v.tr) {
@@ -399,6 +401,21 @@ static int mode_kat(int argc, char** argv) {
     return 0;
 }
 
+// stb-decoded earthmap texels exactly as scene.cpp:139/268/402 load them (stbi_load(..., 3))
+extern "C" unsigned char* stbi_load(char const* filename, int* x, int* y, int* comp, int req_comp);
+static int mode_texels(int argc, char** argv) {
+    const char* in = harg(argc, argv, "--h-in", "../earthmap.jpg");
+    const char* out = harg(argc, argv, "--h-out", "earthmap.rgb");
+    int w, h, c;
+    unsigned char* px = stbi_load(in, &w, &h, &c, 3);
+    if (!px) { fprintf(stderr, "stbi_load failed: %s\n", in); return 2; }
+    FILE* f = fopen(out, "wb");
+    fwrite(px, 1, (size_t)w * h * 3, f);
+    fclose(f);
+    printf("{\"w\":%d,\"h\":%d,\"channels\":%d}\n", w, h, c);
+    return 0;
+}
+
 static int mode_scene(int argc, char** argv) {
     MRT_Params* p = getParams();
     Init_Thread_RNG(11350390909718046443uLL, 6305599193148252115uLL);
@@ -426,8 +443,8 @@ static int mode_hits(int argc, char** argv) {
     const char* out = harg(argc, argv, "--h-out", "hits.npy");
     // rays: camera rays at random (u,v) then one random continuation from the hit point
     std::vector<float> rec((size_t)n * 16, 0.f);
-    Init_Thread_RNG(1234567, 7654321);
     for (int i = 0; i < n; i++) {
+        Init_Thread_RNG(1234567 + (uint64_t)i, 7654321);  // ray generation stream
         float* r = &rec[(size_t)i * 16];
         Vec3 o, d;
         float tm;
@@ -443,9 +460,10 @@ static int mode_hits(int argc, char** argv) {
         }
         ray rr(o, d, tm, ins);
         hit_record h;
+        Init_Thread_RNG((uint64_t)i, 4242);  // constant_volume::hit draws randf() (volumes.cpp:24)
         bool hit = sc.objects->hit(rr, 0.001f, std::numeric_limits<float>::max(), &h);
         r[0] = rr.origin.x; r[1] = rr.origin.y; r[2] = rr.origin.z;
-        r[3] = rr.dir.x; r[4] = rr.dir.y; r[5] = rr.dir.z;
+        r[3] = d.x; r[4] = d.y; r[5] = d.z;  // constructor input (rr.dir = normalize(d))
         r[6] = rr.time; memcpy(&r[7], &ins, 4);
         int hh = hit ? 1 : 0;
         memcpy(&r[8], &hh, 4);
@@ -563,6 +581,7 @@ int main(int argc, char** argv) {
     H_custom = harg(argc, argv, "--h-custom", nullptr);
     H_objdir = harg(argc, argv, "--h-objdir", "../obj");
     if (!strcmp(mode, "kat")) return mode_kat(argc, argv);
+    if (!strcmp(mode, "texels")) return mode_texels(argc, argv);
     ParseArgv(argc, argv);
     if (!strcmp(mode, "scene")) return mode_scene(argc, argv);
     if (!strcmp(mode, "hits")) return mode_hits(argc, argv);

@@ -1,0 +1,116 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/ fixtures from the reference's own code (oracle/_ref, built by
+oracle/ref/build_ref.sh from /root/reference).  Run in the build container, where /root/reference
+exists; the GPU box only reads the committed fixtures.
+
+Fixtures (all small; data only -- inputs and expected outputs):
+  kat_pcg.json            PCG32 rand32/randf and sampler outputs for fixed seeds (pcg.cpp)
+  scene_<id>.json.gz      scene graph dump of select_scene (camera, primitives, BVH topology)
+  hits_<id>.npy           closest-hit KATs: rays vs scene.objects->hit()
+  stream_<id>.npz         stream-matched render: per-path radiance + ray counts + draw() image
+  stream_5_mode1.npz      same for draw2() (mode 1) accumulation
+  shipped_5.npz           as-shipped multithreaded reference render (statistical parity)
+"""
+import gzip
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = os.environ.get("MRT_REFERENCE", "/root/reference")
+EXACT = os.path.join(ROOT, "oracle", "_ref", "mrt_ref_exact")
+SHIPPED = os.path.join(ROOT, "oracle", "_ref", "mrt_ref")
+OUT = os.path.join(ROOT, "tests", "golden")
+CWD = os.path.join(REF, "clang")  # the reference resolves ../obj and ../earthmap.jpg from here
+
+# (scene id, width, height, samples, depth): small stream-matched cases per scene
+STREAM_CASES = [(0, 40, 20, 16, 8), (1, 40, 20, 9, 8), (2, 32, 16, 9, 8), (3, 32, 16, 9, 8), (4, 32, 16, 9, 8),
+                (5, 32, 32, 16, 32), (6, 32, 32, 9, 32), (7, 32, 32, 4, 32), (8, 32, 32, 9, 32), (9, 32, 32, 9, 32)]
+SCENE_SIZES = {0: (200, 100), 1: (200, 100), 2: (200, 100), 3: (200, 100), 4: (200, 100), 5: (500, 500),
+               6: (500, 500), 7: (2048, 2048), 8: (1024, 1024), 9: (800, 800)}
+
+
+def run(binary, args):
+    out = subprocess.run([binary] + [str(a) for a in args], capture_output=True, text=True, cwd=CWD, check=True)
+    return out.stdout
+
+
+def scene_args(sid):
+    a = ["-scene", min(sid, 8)] if sid != 9 else ["-scene", 5, "--h-custom", "teapot", "--h-objdir", os.path.join(REF, "obj")]
+    return a
+
+
+def canon_scene(o):
+    """Harness schema -> schema of mrt_scene_blob_dump_json (box -> its rect list; drop fields the
+    reference leaves uninitialised: pod_bvh leaf `left`/`order`, inner `prim_offset`)."""
+    if isinstance(o, dict):
+        if o.get("k") == "box":
+            return canon_scene(o["rects"])
+        if o.get("k") == "pod_bvh":
+            o = dict(o)
+            o["nodes"] = [[b, l, order] if c == 0 else [b, off, c] for b, l, off, c, order in o["nodes"]]
+        return {k: canon_scene(v) for k, v in o.items() if k != "worker0"}
+    if isinstance(o, list):
+        return [canon_scene(x) for x in o]
+    return o
+
+
+def main():
+    if not (os.path.exists(EXACT) and os.path.isdir(REF)):
+        sys.exit("needs oracle/_ref (run oracle/ref/build_ref.sh) and /root/reference")
+    os.makedirs(OUT, exist_ok=True)
+
+    # 1. PCG / sampler KATs
+    kats = []
+    for st, sq in [(42, 54), (11350390909718046443, 6305599193148252115), (1, 1), (0xDEADBEEF, 12345)]:
+        kats.append(json.loads(run(EXACT, ["--h-mode", "kat", "--h-state", st, "--h-seq", sq, "--h-n", 64])))
+    with open(os.path.join(OUT, "kat_pcg.json"), "w") as f:
+        json.dump(kats, f)
+
+    # 2. scene dumps
+    for sid, (w, h) in SCENE_SIZES.items():
+        d = json.loads(run(EXACT, ["--h-mode", "scene", "-width", w, "-height", h] + scene_args(sid)))
+        with gzip.open(os.path.join(OUT, f"scene_{sid}.json.gz"), "wt") as f:
+            json.dump(canon_scene(d), f)
+
+    with tempfile.TemporaryDirectory() as tmp:
+        # 3. hit KATs
+        for sid, (w, h) in SCENE_SIZES.items():
+            fn = os.path.join(tmp, "h.npy")
+            run(EXACT, ["--h-mode", "hits", "-width", w, "-height", h, "--h-n", 2048, "--h-out", fn] + scene_args(sid))
+            np.savez_compressed(os.path.join(OUT, f"hits_{sid}.npz"), rays=np.load(fn))
+
+        # 4. stream-matched renders with per-path radiance / ray counts
+        def stream(sid, w, h, spp, depth, mode, name):
+            p = os.path.join(tmp, "p")
+            img = os.path.join(tmp, "i.pfm")
+            meta = json.loads(run(EXACT, ["--h-mode", "stream", "-width", w, "-height", h, "-samples", spp, "-depth", depth,
+                                          "--h-acc", mode, "--h-out", img, "--h-paths", p] + scene_args(sid)))
+            raw = open(img, "rb").read().split(b"\n", 3)
+            im = np.frombuffer(raw[3], dtype="<f4").reshape(h, w, 3)
+            np.savez_compressed(os.path.join(OUT, name), image=im, path_rgb=np.load(p + ".rgb.npy"),
+                                path_rays=np.load(p + ".rays.npy").astype(np.uint8),
+                                meta=np.array([sid, w, h, spp, depth, mode, meta["rays"]], dtype=np.int64))
+            return meta
+
+        for sid, w, h, spp, depth in STREAM_CASES:
+            m = stream(sid, w, h, spp, depth, 0, f"stream_{sid}.npz")
+            print("stream", sid, m)
+        print("mode1", stream(5, 24, 24, 16, 32, 1, "stream_5_mode1.npz"))
+
+        # 5. shipped reference (multithreaded, its own worker seeds): statistical parity fixture
+        img = os.path.join(tmp, "s.pfm")
+        meta = json.loads(run(SHIPPED, ["-scene", 5, "-width", 64, "-height", 64, "-samples", 256, "-threads", 8,
+                                        "-mode", 0, "--h-out", img]))
+        raw = open(img, "rb").read().split(b"\n", 3)
+        im = np.frombuffer(raw[3], dtype="<f4").reshape(64, 64, 3)
+        np.savez_compressed(os.path.join(OUT, "shipped_5.npz"), image=im, rays=np.array([meta["rays"]], dtype=np.int64))
+        print("shipped", meta)
+
+
+if __name__ == "__main__":
+    main()
