@@ -8,11 +8,13 @@
 //   normalize  = v / sqrt(sdot(v)) (true division per lane)        vec3.h:137-144
 //   vmin/vmax  = SSE minps/maxps: a<b ? a : b / a>b ? a : b        vec3.h:157-171
 //   cross      = (a.yzx*b.zxy) - (a.zxy*b.yzx)                     vec3.h:252-266
-// Transcendentals are (float)f((double)x) everywhere in this project (DESIGN.md "Numerics").
+// Transcendentals follow the numerics contract of include/mrt_mathfn.h (DESIGN.md "Numerics").
 #pragma once
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+
+#include "../../include/mrt_mathfn.h"
 
 namespace mrt {
 
@@ -48,9 +50,9 @@ static inline int max_dim(V3 a) {
 static const float PI_F = 3.14159265358979323846f;  // M_PI_F (mrt_math.h:11)
 static inline float rad(float a) { return a * (PI_F / 180.0f); }
 
-static inline float sin_(float x) { return (float)std::sin((double)x); }
-static inline float cos_(float x) { return (float)std::cos((double)x); }
-static inline float tan_(float x) { return (float)std::tan((double)x); }
+static inline float sin_(float x) { return mrt_sinf(x); }
+static inline float cos_(float x) { return mrt_cosf(x); }
+static inline float tan_(float x) { return mrt_tanf(x); }
 
 // PCG32 XSH-RR (pcg.cpp:13-35)
 struct Pcg {

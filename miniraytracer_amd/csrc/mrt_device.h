@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/mrt_mathfn.h"
 #include "../../include/mrt_scene.h"
 
 namespace mrtd {
@@ -46,12 +47,19 @@ __device__ __forceinline__ bool finite3(f3 a) { return isfinite(a.x) && isfinite
 static constexpr float PI_F = 3.14159265358979323846f;
 static constexpr float FLT_MAX_ = 3.402823466e+38f;
 
-__device__ __noinline__ float sin_(float x) { return (float)sin((double)x); }
-__device__ __noinline__ float cos_(float x) { return (float)cos((double)x); }
-__device__ __noinline__ float log_(float x) { return (float)log((double)x); }
-__device__ __noinline__ float pow_(float x, float y) { return (float)pow((double)x, (double)y); }
-__device__ __noinline__ float atan2_(float y, float x) { return (float)atan2((double)y, (double)x); }
-__device__ __noinline__ float asin_(float x) { return (float)asin((double)x); }
+// transcendentals: the numerics contract of include/mrt_mathfn.h (same bits as host and oracle)
+__device__ __forceinline__ float sin_(float x) { return mrt_sinf(x); }
+__device__ __forceinline__ float cos_(float x) { return mrt_cosf(x); }
+__device__ __forceinline__ void sincos_(float x, float* s, float* c) {
+    double ds, dc;
+    mrt_sincos_d((double)x, &ds, &dc);
+    *s = (float)ds;
+    *c = (float)dc;
+}
+__device__ __forceinline__ float log_(float x) { return mrt_logf(x); }
+__device__ __forceinline__ float pow5_(float x) { return mrt_pow5f(x); }
+__device__ __forceinline__ float atan2_(float y, float x) { return mrt_atan2f(y, x); }
+__device__ __forceinline__ float asin_(float x) { return mrt_asinf(x); }
 
 // ---------------------------------------------------------------- PCG32 (pcg.cpp:13-62)
 struct Pcg {
@@ -103,14 +111,18 @@ __device__ __forceinline__ f3 random_cosine_direction(Pcg& r) {
     float z = __builtin_sqrtf(1 - r2);
     float phi = (2 * PI_F) * r1;
     float s2 = __builtin_sqrtf(r2);
-    return f3{(cos_(phi) * 2) * s2, (sin_(phi) * 2) * s2, z};
+    float sp, cp;
+    sincos_(phi, &sp, &cp);
+    return f3{(cp * 2) * s2, (sp * 2) * s2, z};
 }
 __device__ __forceinline__ f3 random_towards_sphere(Pcg& r, float radius, float dist_sq) {
     float r1 = randf(r), r2 = randf(r);
     float z = 1 + r2 * (__builtin_sqrtf(1 - (radius * radius) / dist_sq) - 1);
     float phi = (2 * PI_F) * r1;
     float q = __builtin_sqrtf(1 - z * z);
-    return f3{cos_(phi) * q, sin_(phi) * q, z};
+    float sp, cp;
+    sincos_(phi, &sp, &cp);
+    return f3{cp * q, sp * q, z};
 }
 
 // ---------------------------------------------------------------- ray (ray.h:18-56)

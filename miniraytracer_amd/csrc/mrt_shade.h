@@ -211,7 +211,7 @@ __device__ __forceinline__ PathOut trace_path(const DScene& S, Pcg& rng, float s
                 float cs = cosI < 0 ? __builtin_sqrtf(1.0f - (nio * nio) * (1.0f - cosI * cosI)) : cosI;
                 float r0 = (1 - ref) / (1 + ref);
                 r0 = r0 * r0;
-                float reflect_prob = r0 + (1 - r0) * pow_((1 - cs), 5);
+                float reflect_prob = r0 + (1 - r0) * pow5_((1 - cs));
                 if (randf(rng) < reflect_prob) {
                     nd = reflected;
                 } else {

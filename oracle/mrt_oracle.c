@@ -4,11 +4,12 @@
  * reference's virtual calls so that it shares no structure with the HIP kernel's explicit-stack
  * walk.  Every function cites the reference code it restates.  Float operations follow the
  * reference's order; build with -ffp-contract=off (the reference's SSE intrinsics never fuse).
- * sin/cos/log/pow/atan2/asin are (float)f((double)x) -- the definition the exact reference build
- * (oracle/_ref/mrt_ref_exact) interposes, so the two agree bit for bit.
+ * sin/cos/log/pow/atan2/asin follow the numerics contract of include/mrt_mathfn.h -- the functions
+ * the exact reference build (oracle/_ref/mrt_ref_exact) interposes, so the two agree bit for bit.
  */
 #define _GNU_SOURCE
 #include "mrt_oracle.h"
+#include "../include/mrt_mathfn.h"
 
 #include <float.h>
 #include <math.h>
@@ -32,12 +33,13 @@ static float maxps(float a, float b) { return a > b ? a : b; }
 static float minps(float a, float b) { return a < b ? a : b; }
 static const float PI_F = 3.14159265358979323846f;
 
-static float sin_(float x) { return (float)sin((double)x); }
-static float cos_(float x) { return (float)cos((double)x); }
-static float log_(float x) { return (float)log((double)x); }
-static float pow_(float x, float y) { return (float)pow((double)x, (double)y); }
-static float atan2_(float y, float x) { return (float)atan2((double)y, (double)x); }
-static float asin_(float x) { return (float)asin((double)x); }
+/* transcendentals: the numerics contract (include/mrt_mathfn.h) */
+static float sin_(float x) { return mrt_sinf(x); }
+static float cos_(float x) { return mrt_cosf(x); }
+static float log_(float x) { return mrt_logf(x); }
+static float pow_(float x, float y) { return y == 5.0f ? mrt_pow5f(x) : (float)pow((double)x, (double)y); }
+static float atan2_(float y, float x) { return mrt_atan2f(y, x); }
+static float asin_(float x) { return mrt_asinf(x); }
 
 /* ---------------------------------------------------------------- PCG (pcg.cpp:11-136) */
 typedef struct { uint64_t state, inc; } pcg;

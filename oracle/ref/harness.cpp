@@ -18,7 +18,7 @@
 // The reference's platform layer (SDL / GDI) is not compiled; the MRT_* entry points declared in
 // platform.h:4-19 are implemented below as a headless driver.  With -DMRT_MATHMATCH the float
 // libm entry points the reference calls (sinf, cosf, tanf, logf, powf, atan2f, asinf, ...) are
-// interposed by double-evaluated versions, (float)f((double)x) -- the same definition the
+// interposed by the numerics-contract functions of include/mrt_mathfn.h -- the definition the
 // product and the C restatement use -- so the oracle can be compared bit-for-bit.
 
 #include <atomic>
@@ -43,17 +43,18 @@
 #include <x86intrin.h>
 
 #ifdef MRT_MATHMATCH
+#include "../../include/mrt_mathfn.h"  // the project's numerics contract for transcendentals
 extern "C" {
-float sinf(float x) { return (float)sin((double)x); }
-float cosf(float x) { return (float)cos((double)x); }
-void sincosf(float x, float* s, float* c) { *s = (float)sin((double)x); *c = (float)cos((double)x); }
-float tanf(float x) { return (float)tan((double)x); }
-float logf(float x) { return (float)log((double)x); }
+float sinf(float x) { return mrt_sinf(x); }
+float cosf(float x) { return mrt_cosf(x); }
+void sincosf(float x, float* s, float* c) { *s = mrt_sinf(x); *c = mrt_cosf(x); }
+float tanf(float x) { return mrt_tanf(x); }
+float logf(float x) { return mrt_logf(x); }
 float log10f(float x) { return (float)log10((double)x); }
 float expf(float x) { return (float)exp((double)x); }
-float powf(float x, float y) { return (float)pow((double)x, (double)y); }
-float atan2f(float y, float x) { return (float)atan2((double)y, (double)x); }
-float asinf(float x) { return (float)asin((double)x); }
+float powf(float x, float y) { return y == 5.0f ? mrt_pow5f(x) : (float)pow((double)x, (double)y); }
+float atan2f(float y, float x) { return mrt_atan2f(y, x); }
+float asinf(float x) { return mrt_asinf(x); }
 }
 #endif
 

@@ -74,8 +74,9 @@ def main():
     # 2. scene dumps
     for sid, (w, h) in SCENE_SIZES.items():
         d = json.loads(run(EXACT, ["--h-mode", "scene", "-width", w, "-height", h] + scene_args(sid)))
-        with gzip.open(os.path.join(OUT, f"scene_{sid}.json.gz"), "wt") as f:
-            json.dump(canon_scene(d), f)
+        with open(os.path.join(OUT, f"scene_{sid}.json.gz"), "wb") as raw:
+            with gzip.GzipFile(fileobj=raw, mode="wb", mtime=0) as f:  # reproducible bytes
+                f.write(json.dumps(canon_scene(d)).encode())
 
     with tempfile.TemporaryDirectory() as tmp:
         # 3. hit KATs
@@ -103,6 +104,8 @@ def main():
         print("mode1", stream(5, 24, 24, 16, 32, 1, "stream_5_mode1.npz"))
 
         # 5. shipped reference (multithreaded, its own worker seeds): statistical parity fixture
+        if os.path.exists(os.path.join(OUT, "shipped_5.npz")) and "--force" not in sys.argv:
+            return
         img = os.path.join(tmp, "s.pfm")
         meta = json.loads(run(SHIPPED, ["-scene", 5, "-width", 64, "-height", 64, "-samples", 256, "-threads", 8,
                                         "-mode", 0, "--h-out", img]))
