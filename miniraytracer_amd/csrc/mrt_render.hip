@@ -30,59 +30,121 @@ using namespace mrtd;
     } while (0)
 
 struct PathParams {
-    const DScene* __restrict__ S;  // device copy (scalar-loaded)
+    const DScene* __restrict__ S;         // device copy (scalar-loaded)
     const uint32_t* __restrict__ pixels;  // local pixel -> row-major pixel index
     uint32_t npix;                        // local pixel count
     uint32_t width, height, sq, ns;
     uint32_t s0;                          // first sample of this chunk
-    uint64_t n_paths;                     // npix * chunk samples
+    uint32_t n_paths;                     // npix * chunk samples (< 2^32, enforced on the host)
     uint64_t seed;
     uint32_t max_bounces;
     float* __restrict__ rad;              // n_paths * 3 floats, [s - s0][lp]
     uint32_t* __restrict__ path_rays;     // optional (debug): n_paths
-    uint64_t* __restrict__ counter;       // work counter (paths handed out)
+    uint32_t* __restrict__ counter;       // work counter (paths handed out)
     unsigned long long* __restrict__ rays;
-    float4* __restrict__ lev;             // max_bounces rows x lev_stride
+    float4* __restrict__ lev;             // fold levels: max_bounces rows x lev_stride
     size_t lev_stride;                    // = total threads of the grid
+    uint32_t lds_frames, lds_rays, lds_mesh;  // LDS stack slots per lane
 };
 
+// Persistent waves with per-lane path regeneration: every loop iteration advances each busy lane
+// by one segment (one trace() call); a lane whose path ended takes the next path index from its
+// wave's pool at once (ballot + mbcnt compaction), and a wave refills its pool 64 paths at a time
+// with one atomic (work_queue::getWork, work_queue.cpp:158-166).  Lanes stay busy until the pool
+// runs dry instead of idling until the longest path of a 64-path batch finishes.
+template <uint32_t F>
 __global__ void __launch_bounds__(256) mrt_path_kernel(PathParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t words = (P.lds_frames * 2 + P.lds_rays * 11 + P.lds_mesh) * 64;
+    uint32_t* wb = lds + wave * words;
+    const LStack Ls{wb, (float*)(wb + P.lds_frames * 128), wb + P.lds_frames * 128 + P.lds_rays * 704, lane};
+    const DScene& S = *P.S;
     const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint64_t my_rays = 0;
+    float4* __restrict__ lev = P.lev + slot;
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+
+    bool active = false;
+    uint32_t idx = 0;
+    PathState ps;
+    uint32_t pool_next = 0, pool_end = 0;  // wave-uniform
+    bool exhausted = false;
+    uint32_t done_rays = 0;
     for (;;) {
-        uint64_t base = 0;
-        if (lane == 0) base = atomicAdd((unsigned long long*)P.counter, 64ull);
-        base = __shfl(base, 0);
-        if (base >= P.n_paths) break;
-        uint64_t p = base + lane;
-        if (p < P.n_paths) {
-            uint32_t sl = (uint32_t)(p / P.npix);
-            uint32_t lp = (uint32_t)(p - (uint64_t)sl * P.npix);
-            uint32_t s = P.s0 + sl;
-            uint32_t pix = P.pixels[lp];
-            uint32_t x = pix % P.width, y = pix / P.width;
-            // regular-grid sample offsets (main.cpp:324-331): s = i*sq + j
-            uint32_t i = s / P.sq, j = s - i * P.sq;
-            float dx = ((float)i + 0.5f) / (float)P.sq;
-            float dy = ((float)j + 0.5f) / (float)P.sq;
-            float u = ((float)x + dx) / (float)P.width;
-            float v = ((float)y + dy) / (float)P.height;
-            uint64_t path_id = (uint64_t)pix * P.ns + s;
-            Pcg rng;
-            pcg_seed(rng, splitmix64(P.seed ^ path_id), path_id);
-            PathOut o = trace_path(*P.S, rng, u, v, P.max_bounces, P.lev + slot, P.lev_stride);
-            float* dst = P.rad + p * 3;
-            dst[0] = o.L.x;
-            dst[1] = o.L.y;
-            dst[2] = o.L.z;
-            if (P.path_rays) P.path_rays[p] = o.rays;
-            my_rays += o.rays;
+        const uint64_t need = __ballot(!active);
+        if (need && !exhausted) {
+            const uint32_t c = (uint32_t)__popcll(need);
+            const uint32_t have = pool_end - pool_next;
+            uint32_t nb = 0;
+            if (have < c) {
+                if (lane == 0) nb = atomicAdd(P.counter, 64u);
+                nb = __shfl(nb, 0);
+            }
+            if (!active) {
+                const uint32_t rank = (uint32_t)__popcll(need & lt_mask);
+                const uint64_t i = rank < have ? (uint64_t)pool_next + rank : (uint64_t)nb + (rank - have);
+                if (i < P.n_paths) {
+                    idx = (uint32_t)i;
+                    const uint32_t sl = idx / P.npix;
+                    const uint32_t lp = idx - sl * P.npix;
+                    const uint32_t s = P.s0 + sl;
+                    const uint32_t pix = P.pixels[lp];
+                    const uint32_t x = pix % P.width, y = pix / P.width;
+                    // regular-grid sample offsets (main.cpp:324-331): s = i*sq + j
+                    const uint32_t gi = s / P.sq, gj = s - gi * P.sq;
+                    const float dx = ((float)gi + 0.5f) / (float)P.sq;
+                    const float dy = ((float)gj + 0.5f) / (float)P.sq;
+                    const float u = ((float)x + dx) / (float)P.width;
+                    const float v = ((float)y + dy) / (float)P.height;
+                    const uint64_t path_id = (uint64_t)pix * P.ns + s;
+                    pcg_seed(ps.rng, splitmix64(P.seed ^ path_id), path_id);
+                    ps.r = camera_ray(S, ps.rng, u, v);
+                    ps.depth = 0;
+                    ps.nlev = 0;
+                    ps.rays = 0;
+                    active = true;
+                }
+            }
+            if (have < c) {
+                pool_next = nb + (c - have);
+                pool_end = nb + 64u;
+                if (nb >= P.n_paths) exhausted = true;
+            } else {
+                pool_next += c;
+            }
+            if (pool_next >= P.n_paths) exhausted = true;
+        }
+        if (!__any(active)) break;
+        if (active) {
+            f3 L;
+            if (trace_segment<F>(S, ps, P.max_bounces, lev, P.lev_stride, Ls, &L)) {
+                L = fold_levels(lev, P.lev_stride, ps.nlev, L);
+                float* dst = P.rad + (size_t)idx * 3;
+                dst[0] = L.x;
+                dst[1] = L.y;
+                dst[2] = L.z;
+                if (P.path_rays) P.path_rays[idx] = ps.rays;
+                done_rays += ps.rays;
+                active = false;
+            }
         }
     }
     // one 64-bit add per wave
-    for (int off = 32; off > 0; off >>= 1) my_rays += __shfl_xor(my_rays, off);
-    if (lane == 0 && my_rays) atomicAdd(P.rays, (unsigned long long)my_rays);
+    uint64_t my = done_rays;
+    for (int off = 32; off > 0; off >>= 1) my += __shfl_xor(my, off);
+    if (lane == 0 && my) atomicAdd(P.rays, (unsigned long long)my);
+}
+
+// kernel variants by scene features (the smallest instantiated superset is launched)
+static const uint32_t kVariants[] = {FT_INST, FT_INST | FT_MESH | FT_METAL, FT_ALL};
+typedef void (*path_kernel_t)(PathParams);
+static path_kernel_t kernel_for(uint32_t v) {
+    switch (v) {
+    case 0: return mrt_path_kernel<FT_INST>;
+    case 1: return mrt_path_kernel<FT_INST | FT_MESH | FT_METAL>;
+    default: return mrt_path_kernel<FT_ALL>;
+    }
 }
 
 __device__ __forceinline__ float lum3(f3 c) { return (c.x * 0.212655f + c.y * 0.715158f) + c.z * 0.072187f; }
@@ -146,6 +208,9 @@ struct mrt_scene {
     uint64_t* d_counter = nullptr;
     unsigned long long* d_rays = nullptr;
     int grid = 0;
+    uint32_t features = 0, variant = 0;
+    uint32_t lds_frames = 0, lds_rays = 0, lds_mesh = 0;
+    size_t lds_bytes = 0;
     std::vector<hipEvent_t> ev;  // [2*k]: start/stop of path-kernel launch k of the last render
     uint32_t n_launch = 0;
     size_t rad_cap = 0, acc_cap = 0, lev_cap = 0, px_cap = 0, pr_cap = 0;
@@ -186,7 +251,7 @@ extern "C" mrt_status mrt_init(int* device_count) {
     return MRT_OK;
 }
 
-// graph checks on the host, so the fixed-size device stacks can never overflow
+// graph checks on the host: every device stack is sized from them, so none can overflow
 static bool needs_uv_tex(const mrt_scene_view* v, uint32_t t, int guard = 0) {
     if (t == MRT_NONE || t >= v->n_textures || guard > 16) return false;
     const mrt_texture& T = v->textures[t];
@@ -195,63 +260,82 @@ static bool needs_uv_tex(const mrt_scene_view* v, uint32_t t, int guard = 0) {
     return false;
 }
 struct GraphCheck {
+    const std::vector<mrt_node>& nodes;
     const mrt_scene_view* v;
-    int max_frames = 0, max_rays = 0;
+    int max_frames = 0, max_rays = 0, max_mesh = 0;
     bool ok = true;
     std::string why;
-    void walk(uint32_t id, int frames, int rays, bool in_volume) {
+    int mesh_depth(uint32_t ni, int guard) {
+        if (guard > 1000 || ni >= v->n_mesh_nodes) return 100000;
+        const mrt_mesh_node& m = v->mesh_nodes[ni];
+        if (m.count_order & 0xFFFFFFu) return 1;
+        return 1 + std::max(mesh_depth(m.left_or_first, guard + 1), mesh_depth(m.left_or_first + 1, guard + 1));
+    }
+    void walk(uint32_t id, int frames, int rays, bool in_volume, int guard) {
         if (!ok) return;
-        if (id >= v->n_nodes) { ok = false; why = "node index out of range"; return; }
-        const mrt_node& n = v->nodes[id];
+        if (id >= nodes.size() || guard > 4096) { ok = false; why = "bad node index / cyclic scene graph"; return; }
+        const mrt_node& n = nodes[id];
         uint32_t k = n.kind & 0xFF;
-        if (k == MRT_K_SPHERE || k == MRT_K_XY || k == MRT_K_XZ || k == MRT_K_YZ || k == MRT_K_MESH) return;
+        if (k == MRT_K_SPHERE || k == MRT_K_XY || k == MRT_K_XZ || k == MRT_K_YZ) return;
+        if (k == MRT_K_MESH) {
+            max_mesh = std::max(max_mesh, mesh_depth(n.a, 0));
+            return;
+        }
         frames++;
         max_frames = std::max(max_frames, frames);
         switch (k) {
-        case MRT_K_LIST: for (uint32_t i = 0; i < n.b; i++) walk(v->children[n.a + i], frames, rays, in_volume); break;
-        case MRT_K_BVH: walk(n.a, frames, rays, in_volume); walk(n.b, frames, rays, in_volume); break;
-        case MRT_K_TRANSLATE: case MRT_K_ROTY:
+        case MRT_K_LIST:
+            for (uint32_t i = 0; i < n.b; i++) walk(v->children[n.a + i], frames, rays, in_volume, guard + 1);
+            break;
+        case MRT_K_BVH:
+            walk(n.a, frames, rays, in_volume, guard + 1);
+            walk(n.b, frames, rays, in_volume, guard + 1);
+            break;
+        case MRT_K_TRANSLATE: case MRT_K_ROTY: case MRT_K_TRROTY:
             max_rays = std::max(max_rays, rays + 1);
-            walk(n.a, frames, rays + 1, in_volume);
+            walk(n.a, frames, rays + 1, in_volume, guard + 1);
             break;
         case MRT_K_VOLUME:
             if (in_volume) { ok = false; why = "nested constant_volume"; return; }
-            walk(n.a, frames, rays, true);
+            walk(n.a, frames, rays, true, guard + 1);
             break;
         default: ok = false; why = "unknown node kind";
         }
     }
 };
-static int mesh_depth(const mrt_scene_view* v, uint32_t ni, int guard) {
-    if (guard > 64) return 1000;
-    const mrt_mesh_node& m = v->mesh_nodes[ni];
-    if (m.count_order & 0xFFFFFFu) return 1;
-    return 1 + std::max(mesh_depth(v, m.left_or_first, guard + 1), mesh_depth(v, m.left_or_first + 1, guard + 1));
+
+static uint32_t scene_features(const mrt_scene_view* v, const std::vector<mrt_node>& nodes) {
+    uint32_t f = 0;
+    for (const mrt_node& n : nodes) {
+        switch (n.kind & 0xFF) {
+        case MRT_K_BVH: f |= FT_BVH; break;
+        case MRT_K_MESH: f |= FT_MESH; break;
+        case MRT_K_VOLUME: f |= FT_VOLUME; break;
+        case MRT_K_TRANSLATE: case MRT_K_ROTY: case MRT_K_TRROTY: f |= FT_INST; break;
+        case MRT_K_SPHERE: if ((n.kind >> 16) & MRT_F_MOVING) f |= FT_MOVING; break;
+        }
+        if ((n.kind >> 16) & MRT_F_NEEDUV) f |= FT_UV;
+    }
+    for (uint32_t i = 0; i < v->n_textures; i++)
+        if (v->textures[i].kind != MRT_T_COLOR) f |= FT_TEX;
+    for (uint32_t i = 0; i < v->n_materials; i++) {
+        if (v->materials[i].kind == MRT_M_METAL) f |= FT_METAL;
+        if (v->materials[i].kind == MRT_M_ISOTROPIC) f |= FT_ISO;
+    }
+    if (v->sky) f |= FT_SKY;
+    if (v->biased != MRT_NONE) {
+        const mrt_node& b = nodes[v->biased];
+        if ((b.kind & 0xFF) == MRT_K_SPHERE) f |= FT_BSPHERE;
+        if ((b.kind & 0xFF) == MRT_K_LIST)
+            for (uint32_t i = 0; i < b.b; i++)
+                if ((nodes[v->children[b.a + i]].kind & 0xFF) == MRT_K_SPHERE) f |= FT_BSPHERE;
+    }
+    return f;
 }
 
 extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_scene** out) {
     if (!v || !out || v->root >= v->n_nodes) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_scene_upload: bad view");
-    GraphCheck gc{v};
-    gc.walk(v->root, 0, 0, false);
-    if (!gc.ok) return mrt_internal_fail(MRT_ERR_INVALID, gc.why.c_str());
-    if (gc.max_frames > MRT_FRAMES || gc.max_rays > MRT_RAYS) return mrt_internal_fail(MRT_ERR_INVALID, "scene graph deeper than the device stacks");
-    for (uint32_t i = 0; i < v->n_nodes; i++) {
-        const mrt_node& n = v->nodes[i];
-        if ((n.kind & 0xFF) == MRT_K_MESH && 2 * mesh_depth(v, n.a, 0) + 2 > MRT_MESH_STACK)
-            return mrt_internal_fail(MRT_ERR_INVALID, "mesh BVH deeper than the device stack");
-    }
-    if (v->biased != MRT_NONE) {
-        const mrt_node& b = v->nodes[v->biased];
-        if ((b.kind & 0xFF) == MRT_K_LIST)
-            for (uint32_t i = 0; i < b.b; i++) {
-                uint32_t k = v->nodes[v->children[b.a + i]].kind & 0xFF;
-                if (k == MRT_K_LIST) return mrt_internal_fail(MRT_ERR_INVALID, "nested biased object_list");
-            }
-    }
-    HIPCHK(hipSetDevice(device));
-    mrt_scene* s = new mrt_scene();
-    s->device = device;
-    // node flags: NEEDUV where the material samples an image texture
+    // device node table: NEEDUV flags; translate(rotate_y(x)) fused into one instance node
     std::vector<mrt_node> nodes(v->nodes, v->nodes + v->n_nodes);
     for (mrt_node& n : nodes) {
         uint32_t k = n.kind & 0xFF;
@@ -259,6 +343,33 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
             needs_uv_tex(v, v->materials[n.mat].tex))
             n.kind |= MRT_F_NEEDUV << 16;
     }
+    for (mrt_node& n : nodes) {
+        if ((n.kind & 0xFF) != MRT_K_TRANSLATE || n.a >= nodes.size()) continue;
+        const mrt_node& c = nodes[n.a];
+        if ((c.kind & 0xFF) != MRT_K_ROTY) continue;
+        mrt_node f{};
+        f.kind = MRT_K_TRROTY | (c.kind & (MRT_F_HASBOX << 16));
+        f.a = c.a;
+        f.b = MRT_NONE;
+        f.mat = MRT_NONE;
+        for (int i = 0; i < 8; i++) f.f[i] = c.f[i];  // bbox, sin, cos
+        f.f[8] = n.f[0]; f.f[9] = n.f[1]; f.f[10] = n.f[2];
+        n = f;
+    }
+    GraphCheck gc{nodes, v};
+    gc.walk(v->root, 0, 0, false, 0);
+    if (!gc.ok) return mrt_internal_fail(MRT_ERR_INVALID, gc.why.c_str());
+    if (v->biased != MRT_NONE) {
+        if (v->biased >= nodes.size()) return mrt_internal_fail(MRT_ERR_INVALID, "bad biased node");
+        const mrt_node& b = nodes[v->biased];
+        if ((b.kind & 0xFF) == MRT_K_LIST)
+            for (uint32_t i = 0; i < b.b; i++)
+                if ((nodes[v->children[b.a + i]].kind & 0xFF) == MRT_K_LIST)
+                    return mrt_internal_fail(MRT_ERR_INVALID, "nested biased object_list");
+    }
+    HIPCHK(hipSetDevice(device));
+    mrt_scene* s = new mrt_scene();
+    s->device = device;
     mrt_status st;
     DScene& S = s->S;
 #define UP(src, n, dst) { void* t_ = nullptr; if ((st = upload(s, src, (size_t)(n) * sizeof(*(src)), &t_))) { mrt_scene_free(s); return st; } *(dst) = (decltype(+*(dst)))t_; }
@@ -284,10 +395,22 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     if ((st = dev_alloc(s, &p, 64))) { mrt_scene_free(s); return st; }
     s->d_counter = (uint64_t*)p;
     s->d_rays = (unsigned long long*)((char*)p + 16);
+    // kernel variant + LDS stacks sized from the scene graph (top frame lives in registers)
+    s->features = scene_features(v, nodes);
+    s->variant = 2;
+    for (uint32_t i = 0; i < sizeof(kVariants) / sizeof(kVariants[0]); i++)
+        if ((s->features & ~kVariants[i]) == 0) { s->variant = i; break; }
+    s->lds_frames = (uint32_t)std::max(gc.max_frames - 1, 0);
+    s->lds_rays = (uint32_t)gc.max_rays;
+    s->lds_mesh = (uint32_t)gc.max_mesh;
+    s->lds_bytes = (size_t)4 * 64 * 4 * (s->lds_frames * 2 + s->lds_rays * 11 + s->lds_mesh);
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
-    // persistent grid: 4 x 256-thread workgroups per CU (VGPR-limited residency)
-    s->grid = prop.multiProcessorCount * 4;
+    if (s->lds_bytes > (size_t)prop.sharedMemPerBlock) { mrt_scene_free(s); return mrt_internal_fail(MRT_ERR_INVALID, "scene graph too deep for the LDS stacks"); }
+    int nb = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kernel_for(s->variant)), 256, s->lds_bytes));
+    if (nb < 1) nb = 1;
+    s->grid = prop.multiProcessorCount * nb;
     *out = s;
     return MRT_OK;
 }
@@ -340,6 +463,8 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
         HIPCHK(hipMemcpy(s->d_pixels, px.data(), px.size() * 4, hipMemcpyHostToDevice));
     }
     s->chunk = d->chunk_samples ? std::min(d->chunk_samples, ns) : auto_chunk(s->npix, ns);
+    s->chunk = (uint32_t)std::min<uint64_t>(s->chunk, 0xFFFFFFFFull / std::max<uint32_t>(s->npix, 1));  // 32-bit path index
+    if (s->chunk == 0) return mrt_internal_fail(MRT_ERR_INVALID, "image too large for one launch");
     if (d->flags & MRT_RF_PATH_DEBUG) s->chunk = ns;  // debug keeps every path
     size_t paths = (size_t)s->npix * s->chunk;
     if ((st = grow((void**)&s->d_rad, &s->rad_cap, paths * 12))) return st;
@@ -371,6 +496,9 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         uint32_t s1 = std::min(ns, s0 + s->chunk);
         PathParams P{};
         P.S = s->d_S;
+        P.lds_frames = s->lds_frames;
+        P.lds_rays = s->lds_rays;
+        P.lds_mesh = s->lds_mesh;
         P.pixels = s->d_pixels;
         P.npix = s->npix;
         P.width = d->width;
@@ -378,18 +506,18 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.sq = d->sqrt_samples;
         P.ns = ns;
         P.s0 = s0;
-        P.n_paths = (uint64_t)s->npix * (s1 - s0);
+        P.n_paths = s->npix * (s1 - s0);
         P.seed = d->seed;
         P.max_bounces = d->max_bounces;
         P.rad = s->d_rad;
         P.path_rays = (d->flags & MRT_RF_PATH_DEBUG) ? s->d_path_rays : nullptr;
-        P.counter = s->d_counter;
+        P.counter = (uint32_t*)s->d_counter;
         P.rays = d_rays ? (unsigned long long*)d_rays : s->d_rays;
         P.lev = s->d_lev;
         P.lev_stride = s->lev_stride;
         HIPCHK(hipMemsetAsync(s->d_counter, 0, 8, q));
         HIPCHK(hipEventRecord(s->ev[2 * s->n_launch], q));
-        hipLaunchKernelGGL(mrt_path_kernel, dim3(s->grid), dim3(256), 0, q, P);
+        hipLaunchKernelGGL(kernel_for(s->variant), dim3(s->grid), dim3(256), s->lds_bytes, q, P);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(s->ev[2 * s->n_launch + 1], q));
         s->n_launch++;

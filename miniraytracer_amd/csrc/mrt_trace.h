@@ -1,4 +1,5 @@
-// mrt_trace.h -- scene traversal (scene_object::hit tree), shading and one full path (trace()).
+// mrt_trace.h -- scene traversal: the scene_object::hit virtual-call tree as a per-lane
+// explicit-stack machine with its stacks in LDS.
 #pragma once
 #include "mrt_device.h"
 
@@ -23,9 +24,38 @@ struct DScene {
 #define MRT_NODE_KIND(n) ((n).kind & 0xFFu)
 #define MRT_NODE_ORDER(n) (((n).kind >> 8) & 0xFFu)
 #define MRT_NODE_FLAGS(n) (((n).kind >> 16) & 0xFFu)
-#define MRT_F_NEEDUV 0x4u /* set by the device upload when the node's material samples uv */
+#define MRT_F_NEEDUV 0x4u   /* set on upload when the node's material samples uv */
+#define MRT_K_TRROTY 11u    /* upload fuses translate(rotate_y(x)) into one instance node */
 
-__device__ __forceinline__ bool is_prim(uint32_t kind) { return kind == MRT_K_SPHERE || kind == MRT_K_XY || kind == MRT_K_XZ || kind == MRT_K_YZ || kind == MRT_K_MESH; }
+// Scene features; kernels are instantiated for feature subsets so that Cornell-like scenes run
+// without the code (and registers) of BVH/mesh/volume/texture paths they never take.
+enum : uint32_t {
+    FT_BVH = 1u << 0,
+    FT_MESH = 1u << 1,
+    FT_VOLUME = 1u << 2,
+    FT_INST = 1u << 3,
+    FT_TEX = 1u << 4,      // checker / perlin / image textures
+    FT_METAL = 1u << 5,
+    FT_ISO = 1u << 6,      // isotropic phase function
+    FT_MOVING = 1u << 7,   // moving spheres
+    FT_SKY = 1u << 8,
+    FT_BSPHERE = 1u << 9,  // sphere in the biased (light-sampling) list
+    FT_UV = 1u << 10,      // uv sampled on spheres / rects
+    FT_ALL = (1u << 11) - 1,
+};
+
+// Per-wave LDS stacks, lane-interleaved ([slot][word][lane]) so every access is conflict-free.
+struct LStack {
+    uint32_t* frames;  // 2 words per slot: node, state
+    float* rays;       // 11 words per slot: o.xyz, d.xyz, inv.xyz, inside, mask
+    uint32_t* mesh;    // 1 word per slot
+    uint32_t lane;
+};
+
+template <uint32_t F>
+__device__ __forceinline__ bool is_prim(uint32_t kind) {
+    return kind == MRT_K_SPHERE || kind == MRT_K_XY || kind == MRT_K_XZ || kind == MRT_K_YZ || ((F & FT_MESH) && kind == MRT_K_MESH);
+}
 
 // get_sphere_uv (sphere.cpp:6-11)
 __device__ __forceinline__ void sphere_uv(f3 p, float* u, float* v) {
@@ -35,15 +65,18 @@ __device__ __forceinline__ void sphere_uv(f3 p, float* u, float* v) {
     *v = 0.5f + theta * (1.0f / PI_F);
 }
 
+template <uint32_t F>
 __device__ __forceinline__ f3 sphere_center(const mrt_node& n, float time) {
     f3 c0 = ld3(n.f);
-    if (MRT_NODE_FLAGS(n) & MRT_F_MOVING) return add(c0, fmul((time - n.f[6]) / (n.f[7] - n.f[6]), sub(ld3(n.f + 3), c0)));
+    if ((F & FT_MOVING) && (MRT_NODE_FLAGS(n) & MRT_F_MOVING))
+        return add(c0, fmul((time - n.f[6]) / (n.f[7] - n.f[6]), sub(ld3(n.f + 3), c0)));
     return c0;
 }
 
 // sphere::hit (sphere.cpp:13-46).  `full` = write p/n/uv (false inside volume boundary queries).
+template <uint32_t F>
 __device__ __forceinline__ bool sphere_hit(const mrt_node& n, const Ray& r, float tmin, float tmax, HitRec& rec, bool full) {
-    f3 cen = sphere_center(n, r.time);
+    f3 cen = sphere_center<F>(n, r.time);
     float radius = n.f[8];
     f3 oc = sub(r.o, cen);
     float b = dot(oc, r.d);
@@ -63,7 +96,7 @@ __device__ __forceinline__ bool sphere_hit(const mrt_node& n, const Ray& r, floa
                 rec.p = eval(r, t);
                 rec.n = divf(sub(rec.p, cen), radius);
                 rec.mat = n.mat;
-                if (MRT_NODE_FLAGS(n) & MRT_F_NEEDUV) sphere_uv(rec.n, &rec.u, &rec.v);
+                if ((F & FT_UV) && (MRT_NODE_FLAGS(n) & MRT_F_NEEDUV)) sphere_uv(rec.n, &rec.u, &rec.v);
             }
             return true;
         }
@@ -71,8 +104,8 @@ __device__ __forceinline__ bool sphere_hit(const mrt_node& n, const Ray& r, floa
     return false;
 }
 
-// xy/xz/yz_rect::hit (rect.cpp:24-152): axis a (plane normal), b, c (in-plane)
-template <int AX>
+// xy/xz/yz_rect::hit (rect.cpp:24-152); AX = plane axis (2: xy, 1: xz, 0: yz)
+template <uint32_t F, int AX>
 __device__ __forceinline__ bool rect_hit(const mrt_node& n, const Ray& r, float tmin, float tmax, HitRec& rec, bool full) {
     const float ns = n.f[5];
     // dot(r.dir, normal) with the zero lanes kept (NaN directions behave as in the reference)
@@ -84,7 +117,6 @@ __device__ __forceinline__ bool rect_hit(const mrt_node& n, const Ray& r, float 
     float da = AX == 2 ? r.d.z : AX == 1 ? r.d.y : r.d.x;
     float t = (n.f[4] - oa) / da;
     if (t < tmin || t > tmax) return false;
-    // in-plane axes: xy -> (x,y), xz -> (x,z), yz -> (y,z)
     float ob = AX == 0 ? r.o.y : r.o.x, db = AX == 0 ? r.d.y : r.d.x;
     float oc = AX == 2 ? r.o.y : r.o.z, dc = AX == 2 ? r.d.y : r.d.z;
     float pb = ob + t * db;
@@ -92,7 +124,7 @@ __device__ __forceinline__ bool rect_hit(const mrt_node& n, const Ray& r, float 
     if (pb < n.f[0] || pb > n.f[1] || pc < n.f[2] || pc > n.f[3]) return false;
     rec.t = t;
     if (full) {
-        if (MRT_NODE_FLAGS(n) & MRT_F_NEEDUV) {
+        if ((F & FT_UV) && (MRT_NODE_FLAGS(n) & MRT_F_NEEDUV)) {
             rec.u = (pb - n.f[0]) / (n.f[1] - n.f[0]);
             rec.v = (pc - n.f[2]) / (n.f[3] - n.f[2]);
         }
@@ -105,7 +137,8 @@ __device__ __forceinline__ bool rect_hit(const mrt_node& n, const Ray& r, float 
 
 // triangle::hit (triangle.cpp:222-265) without the normal (deferred to the closest hit)
 __device__ __forceinline__ bool tri_hit(const DScene& S, uint32_t i, const Ray& r, float tmin, float tmax, float* tout, float* uout, float* vout) {
-    f3 m = ld3(S.tri_geo[i * 3 + 0]), u = ld3(S.tri_geo[i * 3 + 1]), v = ld3(S.tri_geo[i * 3 + 2]);
+    const float4* g = S.tri_geo + (size_t)i * 3;
+    f3 m = ld3(g[0]), u = ld3(g[1]), v = ld3(g[2]);
     f3 pvec = cross(r.d, v);
     float det = dot(u, pvec);
     float sign = 1.0f;
@@ -128,63 +161,108 @@ __device__ __forceinline__ bool tri_hit(const DScene& S, uint32_t i, const Ray& 
     return true;
 }
 
-// pod_bvh::hit (triangle.h:171-221): DFS, closer child first (node_order & dirMask); the first
-// leaf that reports a hit ends the walk (every ancestor returns on hit_closer / hit_farther).
-#define MRT_MESH_STACK 48
-__device__ __noinline__ bool mesh_hit(const DScene& S, const mrt_node& n, const Ray& r, float tmin, float tmax, HitRec& rec, bool full) {
-    uint32_t stack[MRT_MESH_STACK];
-    int sp = 0;
-    stack[sp++] = n.a;
-    while (sp > 0) {
-        uint32_t ni = stack[--sp];
+// pod_bvh::hit (triangle.h:171-221): depth-first, closer child first (node_order & dirMask); the
+// first leaf that reports a hit ends the walk (every ancestor returns on hit_closer/hit_farther).
+// Short stack in LDS: only the farther child of each visited inner node is pushed.
+__device__ __forceinline__ bool mesh_hit(const DScene& S, const mrt_node& n, const Ray& r, float tmin, float tmax, HitRec& rec, bool full,
+                                         const LStack& L) {
+    uint32_t ni = n.a, msp = 0;
+    for (;;) {
         const mrt_mesh_node& mn = S.mnodes[ni];
-        if (!aabb_hit(mn.bmin, mn.bmax, r, tmin, tmax)) continue;
-        uint32_t cnt = mn.count_order & 0xFFFFFFu;
-        if (cnt) {
-            bool has = false;
-            uint32_t best = 0;
-            float bu = 0, bv = 0, tt = tmax;
-            for (uint32_t k = 0; k < cnt; k++) {
-                float t, uu, vv;
-                if (tri_hit(S, mn.left_or_first + k, r, tmin, tt, &t, &uu, &vv)) {
-                    has = true;
-                    tt = t;
-                    best = mn.left_or_first + k;
-                    bu = uu;
-                    bv = vv;
+        bool go = aabb_hit(mn.bmin, mn.bmax, r, tmin, tmax);
+        if (go) {
+            uint32_t cnt = mn.count_order & 0xFFFFFFu;
+            if (cnt) {
+                bool has = false;
+                uint32_t best = 0;
+                float bu = 0, bv = 0, tt = tmax;
+                for (uint32_t k = 0; k < cnt; k++) {
+                    float t, uu, vv;
+                    if (tri_hit(S, mn.left_or_first + k, r, tmin, tt, &t, &uu, &vv)) {
+                        has = true;
+                        tt = t;
+                        best = mn.left_or_first + k;
+                        bu = uu;
+                        bv = vv;
+                    }
                 }
-            }
-            if (has) {
-                rec.t = tt;
-                if (full) {
-                    f3 nm = ld3(S.tri_nrm[best * 3 + 0]), nu = ld3(S.tri_nrm[best * 3 + 1]), nv = ld3(S.tri_nrm[best * 3 + 2]);
-                    rec.p = eval(r, tt);
-                    rec.n = normalize(add(add(mulf(nm, (1 - bu) - bv), mulf(nu, bu)), mulf(nv, bv)));
-                    rec.u = bu;
-                    rec.v = bv;
-                    rec.mat = n.mat;
+                if (has) {
+                    rec.t = tt;
+                    if (full) {
+                        const float4* q = S.tri_nrm + (size_t)best * 3;
+                        f3 nm = ld3(q[0]), nu = ld3(q[1]), nv = ld3(q[2]);
+                        rec.p = eval(r, tt);
+                        rec.n = normalize(add(add(mulf(nm, (1 - bu) - bv), mulf(nu, bu)), mulf(nv, bv)));
+                        rec.u = bu;
+                        rec.v = bv;
+                        rec.mat = n.mat;
+                    }
+                    return true;
                 }
-                return true;
+            } else {
+                uint32_t l = mn.left_or_first;
+                bool left_first = ((mn.count_order >> 24) & r.mask) != 0;
+                L.mesh[msp * 64 + L.lane] = left_first ? l + 1 : l;  // farther
+                msp++;
+                ni = left_first ? l : l + 1;  // closer
+                continue;
             }
-        } else {
-            uint32_t l = mn.left_or_first;
-            bool left_first = ((mn.count_order >> 24) & r.mask) != 0;
-            if (sp + 2 > MRT_MESH_STACK) __builtin_trap();
-            stack[sp++] = left_first ? l + 1 : l;  // farther
-            stack[sp++] = left_first ? l : l + 1;  // closer (popped first)
         }
+        if (msp == 0) return false;
+        msp--;
+        ni = L.mesh[msp * 64 + L.lane];
     }
-    return false;
 }
 
-__device__ __forceinline__ bool prim_hit(const DScene& S, const mrt_node& n, uint32_t kind, const Ray& r, float tmin, float tmax, HitRec& rec, bool full) {
+template <uint32_t F>
+__device__ __forceinline__ bool prim_hit(const DScene& S, const mrt_node& n, uint32_t kind, const Ray& r, float tmin, float tmax, HitRec& rec,
+                                         bool full, const LStack& L) {
     switch (kind) {
-    case MRT_K_SPHERE: return sphere_hit(n, r, tmin, tmax, rec, full);
-    case MRT_K_XY: return rect_hit<2>(n, r, tmin, tmax, rec, full);
-    case MRT_K_XZ: return rect_hit<1>(n, r, tmin, tmax, rec, full);
-    case MRT_K_YZ: return rect_hit<0>(n, r, tmin, tmax, rec, full);
-    default: return mesh_hit(S, n, r, tmin, tmax, rec, full);
+    case MRT_K_SPHERE: return sphere_hit<F>(n, r, tmin, tmax, rec, full);
+    case MRT_K_XY: return rect_hit<F, 2>(n, r, tmin, tmax, rec, full);
+    case MRT_K_XZ: return rect_hit<F, 1>(n, r, tmin, tmax, rec, full);
+    case MRT_K_YZ: return rect_hit<F, 0>(n, r, tmin, tmax, rec, full);
+    default:
+        if constexpr ((F & FT_MESH) != 0) return mesh_hit(S, n, r, tmin, tmax, rec, full, L);
+        return false;
     }
+}
+
+__device__ __forceinline__ void push_ray(const LStack& L, uint32_t slot, const Ray& r) {
+    float* b = L.rays + slot * 11 * 64 + L.lane;
+    b[0] = r.o.x; b[64] = r.o.y; b[128] = r.o.z;
+    b[192] = r.d.x; b[256] = r.d.y; b[320] = r.d.z;
+    b[384] = r.inv.x; b[448] = r.inv.y; b[512] = r.inv.z;
+    b[576] = __int_as_float(r.inside);
+    b[640] = __uint_as_float(r.mask);
+}
+__device__ __forceinline__ void pop_ray(const LStack& L, uint32_t slot, Ray& r) {
+    const float* b = L.rays + slot * 11 * 64 + L.lane;
+    r.o = f3{b[0], b[64], b[128]};
+    r.d = f3{b[192], b[256], b[320]};
+    r.inv = f3{b[384], b[448], b[512]};
+    r.inside = __float_as_int(b[576]);
+    r.mask = __float_as_uint(b[640]);
+}
+
+// rotate_y::hit ray transform (scene_object.cpp:75-82)
+__device__ __forceinline__ Ray rotate_ray(const Ray& ray, float s, float c) {
+    f3 o = ray.o, d = ray.d;
+    o.x = c * ray.o.x - s * ray.o.z;
+    o.z = c * ray.o.z + s * ray.o.x;
+    d.x = c * ray.d.x - s * ray.d.z;
+    d.z = c * ray.d.z + s * ray.d.x;
+    return make_ray(o, d, ray.time, 0);
+}
+// ... and the record back (scene_object.cpp:85-93)
+__device__ __forceinline__ void unrotate_rec(HitRec& rec, float s, float c) {
+    f3 p = rec.p, nn = rec.n;
+    p.x = c * rec.p.x + s * rec.p.z;
+    p.z = c * rec.p.z - s * rec.p.x;
+    nn.x = c * rec.n.x + s * rec.n.z;
+    nn.z = c * rec.n.z - s * rec.n.x;
+    rec.p = p;
+    rec.n = nn;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -193,16 +271,13 @@ __device__ __forceinline__ bool prim_hit(const DScene& S, const mrt_node& n, uin
 // the list's closest, bvh_node children its tmax, which is unchanged until a hit ends the node).
 // constant_volume runs its two boundary queries as a nested context whose hits only record t;
 // volumes never nest (checked on upload).  The top frame lives in registers; frames below it and
-// saved instance rays live in per-lane scratch.  Primitives have exactly one evaluation site.
+// saved instance rays live in LDS.  Primitives have exactly one evaluation site.
 // ------------------------------------------------------------------------------------------
-#define MRT_FRAMES 32
-#define MRT_RAYS 6
 enum : uint32_t { ST_ENTER = 0xFFFFFFFFu, ST_PH1 = 0x40000000u, ST_PH2 = 0x40000001u };
 
-__device__ __forceinline__ bool scene_hit(const DScene& S, Ray ray, float tmin0, HitRec& rec, Pcg& rng) {
-    uint32_t fnode[MRT_FRAMES], fstate[MRT_FRAMES];
-    Ray rstk[MRT_RAYS];
-    int depth = 0, rsp = 0;
+template <uint32_t F>
+__device__ __forceinline__ bool scene_hit(const DScene& S, Ray ray, float tmin0, HitRec& rec, Pcg& rng, const LStack& L) {
+    uint32_t depth = 0, rsp = 0;
     uint32_t tnode = 0, tstate = 0;  // top frame
     float closest = FLT_MAX_, tmin = tmin0;
     bool insub = false;  // inside a constant_volume boundary query
@@ -215,34 +290,33 @@ __device__ __forceinline__ bool scene_hit(const DScene& S, Ray ray, float tmin0,
         if (req != MRT_NONE) {
             const mrt_node& C = S.nodes[req];
             const uint32_t ck = MRT_NODE_KIND(C);
-            req = MRT_NONE;
-            if (is_prim(ck)) {
-                HitRec* R = insub ? &subrec : &rec;
-                ret = prim_hit(S, C, ck, ray, tmin, closest, *R, !insub);
+            if (is_prim<F>(ck)) {
+                HitRec* R = ((F & FT_VOLUME) && insub) ? &subrec : &rec;
+                ret = prim_hit<F>(S, C, ck, ray, tmin, closest, *R, !((F & FT_VOLUME) && insub), L);
                 if (ret) closest = R->t;
+                req = MRT_NONE;
                 if (depth == 0) break;
             } else {
                 if (depth > 0) {
-                    fnode[depth - 1] = tnode;
-                    fstate[depth - 1] = tstate;
+                    L.frames[(depth - 1) * 128 + L.lane] = tnode;
+                    L.frames[(depth - 1) * 128 + 64 + L.lane] = tstate;
                 }
-                tnode = (uint32_t)(&C - S.nodes);
+                tnode = req;
                 tstate = ST_ENTER;
                 depth++;
+                req = MRT_NONE;
             }
         }
         const mrt_node& N = S.nodes[tnode];
         const uint32_t kind = MRT_NODE_KIND(N);
         const uint32_t st = tstate;
         bool pop = false;
-        switch (kind) {
-        case MRT_K_LIST: {  // object_list::hit (scene_object.h:79-103)
+        if (kind == MRT_K_LIST) {  // object_list::hit (scene_object.h:79-103)
             uint32_t cursor, flag;
             if (st == ST_ENTER) {
                 if ((MRT_NODE_FLAGS(N) & MRT_F_HASBOX) && !aabb_hit(N.f, N.f + 3, ray, tmin, closest)) {
                     ret = false;
                     pop = true;
-                    break;
                 }
                 cursor = 0;
                 flag = 0;
@@ -250,77 +324,73 @@ __device__ __forceinline__ bool scene_hit(const DScene& S, Ray ray, float tmin0,
                 cursor = st & 0x3FFFFFFFu;
                 flag = (st >> 31) | (ret ? 1u : 0u);
             }
-            if (cursor < N.b) {
-                req = S.children[N.a + cursor];
-                tstate = (cursor + 1) | (flag << 31);
+            if (!pop) {
+                if (cursor < N.b) {
+                    req = S.children[N.a + cursor];
+                    tstate = (cursor + 1) | (flag << 31);
+                } else {
+                    ret = flag != 0;
+                    pop = true;
+                }
+            }
+        } else if ((F & FT_INST) && kind == MRT_K_TRROTY) {  // translate(rotate_y(x)) fused
+            const float s = N.f[6], c = N.f[7];
+            if (st == ST_ENTER) {
+                Ray moved = make_ray(sub(ray.o, ld3(N.f + 8)), ray.d, ray.time, 0);  // translate::hit
+                if ((MRT_NODE_FLAGS(N) & MRT_F_HASBOX) && !aabb_hit(N.f, N.f + 3, moved, tmin, closest)) {
+                    ret = false;
+                    pop = true;
+                } else {
+                    push_ray(L, rsp++, ray);
+                    ray = rotate_ray(moved, s, c);
+                    req = N.a;
+                    tstate = ST_PH1;
+                }
             } else {
-                ret = flag != 0;
+                pop_ray(L, --rsp, ray);
+                if (ret && !insub) {
+                    unrotate_rec(rec, s, c);
+                    rec.p = add(rec.p, ld3(N.f + 8));
+                }
                 pop = true;
             }
-            break;
-        }
-        case MRT_K_BVH: {  // bvh_node::hit (scene_object.h:208-244)
+        } else if ((F & FT_INST) && (kind == MRT_K_TRANSLATE || kind == MRT_K_ROTY)) {  // scene_object.cpp:9-18, 70-98
+            const bool roty = kind == MRT_K_ROTY;
+            if (st == ST_ENTER) {
+                if (roty && (MRT_NODE_FLAGS(N) & MRT_F_HASBOX) && !aabb_hit(N.f, N.f + 3, ray, tmin, closest)) {
+                    ret = false;
+                    pop = true;
+                } else {
+                    push_ray(L, rsp++, ray);
+                    ray = roty ? rotate_ray(ray, N.f[6], N.f[7]) : make_ray(sub(ray.o, ld3(N.f)), ray.d, ray.time, 0);
+                    req = N.a;
+                    tstate = ST_PH1;
+                }
+            } else {
+                pop_ray(L, --rsp, ray);
+                if (ret && !insub) {
+                    if (!roty) rec.p = add(rec.p, ld3(N.f));
+                    else unrotate_rec(rec, N.f[6], N.f[7]);
+                }
+                pop = true;
+            }
+        } else if ((F & FT_BVH) && kind == MRT_K_BVH) {  // bvh_node::hit (scene_object.h:208-244)
             const bool left_first = (MRT_NODE_ORDER(N) & ray.mask) != 0;
             if (st == ST_ENTER) {
                 if (!aabb_hit(N.f, N.f + 3, ray, tmin, closest)) {
                     ret = false;
                     pop = true;
-                    break;
+                } else {
+                    req = left_first ? N.a : N.b;
+                    tstate = ST_PH1;
                 }
-                req = left_first ? N.a : N.b;
-                tstate = ST_PH1;
             } else if (st == ST_PH1 && !ret) {
                 req = left_first ? N.b : N.a;
                 tstate = ST_PH2;
             } else {
                 pop = true;  // closer hit (ret true) or farther done
             }
-            break;
-        }
-        case MRT_K_TRANSLATE:
-        case MRT_K_ROTY: {  // scene_object.cpp:9-18, 70-98
-            const bool roty = kind == MRT_K_ROTY;
-            if (st == ST_ENTER) {
-                if (roty && (MRT_NODE_FLAGS(N) & MRT_F_HASBOX) && !aabb_hit(N.f, N.f + 3, ray, tmin, closest)) {
-                    ret = false;
-                    pop = true;
-                    break;
-                }
-                rstk[rsp++] = ray;
-                if (!roty) {
-                    ray = make_ray(sub(ray.o, ld3(N.f)), ray.d, ray.time, 0);
-                } else {
-                    const float s = N.f[6], c = N.f[7];
-                    f3 o = ray.o, d = ray.d;
-                    o.x = c * ray.o.x - s * ray.o.z;
-                    o.z = c * ray.o.z + s * ray.o.x;
-                    d.x = c * ray.d.x - s * ray.d.z;
-                    d.z = c * ray.d.z + s * ray.d.x;
-                    ray = make_ray(o, d, ray.time, 0);
-                }
-                req = N.a;
-                tstate = ST_PH1;
-            } else {
-                ray = rstk[--rsp];
-                if (ret && !insub) {
-                    if (!roty) {
-                        rec.p = add(rec.p, ld3(N.f));
-                    } else {
-                        const float s = N.f[6], c = N.f[7];
-                        f3 p = rec.p, nn = rec.n;
-                        p.x = c * rec.p.x + s * rec.p.z;
-                        p.z = c * rec.p.z - s * rec.p.x;
-                        nn.x = c * rec.n.x + s * rec.n.z;
-                        nn.z = c * rec.n.z - s * rec.n.x;
-                        rec.p = p;
-                        rec.n = nn;
-                    }
-                }
-                pop = true;
-            }
-            break;
-        }
-        case MRT_K_VOLUME: {  // constant_volume::hit (volumes.cpp:5-35)
+        } else if ((F & FT_VOLUME) && kind == MRT_K_VOLUME) {  // constant_volume::hit (volumes.cpp:5-35)
             if (st == ST_ENTER) {
                 save_closest = closest;
                 save_tmin = tmin;
@@ -340,37 +410,36 @@ __device__ __forceinline__ bool scene_hit(const DScene& S, Ray ray, float tmin0,
                 closest = save_closest;
                 tmin = save_tmin;
                 pop = true;
-                if (!ret) break;
-                float t1 = vt1, t2 = subrec.t;
-                if (t1 < tmin) t1 = tmin;
-                if (t2 > closest) t2 = closest;
-                if (t1 >= t2) {
-                    ret = false;
-                    break;
-                }
-                if (t1 < 0) t1 = 0;
-                const float inside_dist = t2 - t1;
-                const float hit_dist = -(1 / N.f[0]) * log_(randf(rng));
-                ret = hit_dist < inside_dist;
                 if (ret) {
-                    rec.t = t1 + hit_dist;
-                    rec.p = eval(ray, rec.t);
-                    rec.n = f3{1, 0, 0};
-                    rec.mat = N.mat;
-                    closest = rec.t;
+                    float t1 = vt1, t2 = subrec.t;
+                    if (t1 < tmin) t1 = tmin;
+                    if (t2 > closest) t2 = closest;
+                    if (t1 >= t2) {
+                        ret = false;
+                    } else {
+                        if (t1 < 0) t1 = 0;
+                        const float inside_dist = t2 - t1;
+                        const float hit_dist = -(1 / N.f[0]) * log_(randf(rng));
+                        ret = hit_dist < inside_dist;
+                        if (ret) {
+                            rec.t = t1 + hit_dist;
+                            rec.p = eval(ray, rec.t);
+                            rec.n = f3{1, 0, 0};
+                            rec.mat = N.mat;
+                            closest = rec.t;
+                        }
+                    }
                 }
             }
-            break;
-        }
-        default:
+        } else {
             ret = false;
             pop = true;
         }
         if (pop) {
             depth--;
             if (depth == 0) break;
-            tnode = fnode[depth - 1];
-            tstate = fstate[depth - 1];
+            tnode = L.frames[(depth - 1) * 128 + L.lane];
+            tstate = L.frames[(depth - 1) * 128 + 64 + L.lane];
         }
     }
     return ret;
