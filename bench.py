@@ -98,26 +98,14 @@ def main():
     stream = torch.cuda.current_stream(dev)
 
     if world > 1:
-        counts = [None] * world
-        dist.all_gather_object(counts, n_local)
-        n_max = max(counts)
-        pad = torch.zeros((n_max, 4), dtype=torch.float32, device=dev)
-        gathered = [torch.zeros((n_max, 4), dtype=torch.float32, device=dev) for _ in range(world)] if rank == 0 else None
-        full = torch.zeros((args.width * args.height, 4), dtype=torch.float32, device=dev) if rank == 0 else None
-        if rank == 0:
-            idx = []
-            for r in range(world):
-                dr = m.render_desc(args.width, args.height, args.samples, depth=args.depth, rank=r, world=world)
-                idx.append(torch.as_tensor(m.local_pixels(dr).astype(np.int64), device=dev))
+        from miniraytracer_amd.dist import TileGather
+        tg = TileGather(args.width, args.height, args.samples, args.depth, world, rank, dev)
+        assert tg.n_local == n_local
 
     def step():
         rnd.render_device(desc, out.data_ptr(), rays.data_ptr(), stream.cuda_stream)
         if world > 1:
-            pad[:n_local].copy_(out)
-            dist.gather(pad, gathered, dst=0)  # the one RCCL collective of the data path
-            if rank == 0:
-                for r in range(world):
-                    full.index_copy_(0, idx[r], gathered[r][: counts[r]])
+            tg.gather(out)  # the one RCCL collective of the data path (tile shards -> rank 0)
 
     for _ in range(args.warmup):
         step()
