@@ -114,6 +114,13 @@ mrt_status mrt_progress(mrt_scene* s, float* pct);
  * stream around each mrt_path_kernel launch); waits for the last one. */
 mrt_status mrt_kernel_ms(mrt_scene* s, float* path_ms, uint32_t* launches);
 
+/* Which path kernel the scene runs: feature bits of the scene (FT_* of mrt_trace.h; bit 11 =
+ * linear hit program, DESIGN.md "Kernels"), dynamic LDS bytes per workgroup and grid size. */
+typedef struct mrt_kernel_info {
+    uint32_t features, kernel_features, lds_bytes, grid, prog_ops;
+} mrt_kernel_info;
+mrt_status mrt_scene_kernel_info(const mrt_scene* s, mrt_kernel_info* out);
+
 /* Drago adaptive-log tone map of a linear W*H*4 buffer to ARGB32 (main.cpp:416-444, no gamma). */
 mrt_status mrt_tonemap_argb(const float* rgb, uint32_t width, uint32_t height, uint32_t* argb_out);
 

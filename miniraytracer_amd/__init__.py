@@ -126,6 +126,12 @@ class Renderer:
         check(lib().mrt_render_device(self._h, C.byref(desc), C.c_void_p(d_out_ptr), C.c_void_p(d_rays_ptr),
                                       C.c_void_p(stream_ptr)), "mrt_render_device")
 
+    def kernel_info(self):
+        """dict(features, kernel_features, lds_bytes, grid, prog_ops) of the path kernel this scene runs."""
+        ki = _lib.KernelInfo()
+        check(lib().mrt_scene_kernel_info(self._h, C.byref(ki)), "mrt_scene_kernel_info")
+        return {k: getattr(ki, k) for k, _ in ki._fields_}
+
     def kernel_ms(self):
         """(total ms, launches) of the path kernel in the last render (HIP events on its stream)."""
         ms, n = C.c_float(), C.c_uint32()

@@ -49,6 +49,14 @@ class MrtSceneView(C.Structure):
                 ("texels", C.c_void_p), ("n_texels", C.c_uint64)]
 
 
+class KernelInfo(C.Structure):
+    _fields_ = [("features", C.c_uint32), ("kernel_features", C.c_uint32), ("lds_bytes", C.c_uint32),
+                ("grid", C.c_uint32), ("prog_ops", C.c_uint32)]
+
+
+FT_LIN = 1 << 11  # kernel feature bit: linear hit program (mrt_lin.h)
+
+
 class MrtError(RuntimeError):
     pass
 
@@ -94,6 +102,8 @@ def lib():
     L.mrt_render_debug.restype = st
     L.mrt_progress.argtypes = [C.c_void_p, C.POINTER(C.c_float)]
     L.mrt_progress.restype = st
+    L.mrt_scene_kernel_info.argtypes = [C.c_void_p, C.POINTER(KernelInfo)]
+    L.mrt_scene_kernel_info.restype = st
     L.mrt_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_uint32)]
     L.mrt_kernel_ms.restype = st
     L.mrt_pack_obj.argtypes = [C.c_char_p, C.c_char_p]
@@ -120,4 +130,5 @@ EXPORTS = [
     "mrt_scene_upload", "mrt_scene_free", "mrt_default_render_desc", "mrt_local_pixels",
     "mrt_render", "mrt_render_device", "mrt_prepare", "mrt_render_debug", "mrt_progress",
     "mrt_tonemap_argb", "mrt_strerror", "mrt_last_error", "mrt_kernel_ms", "mrt_pack_obj",
+    "mrt_scene_kernel_info",
 ]

@@ -1,0 +1,211 @@
+// mrt_lin.h -- scene_object::hit for scene graphs WITHOUT per-ray traversal order (object_list
+// trees, instances, primitives, meshes; no bvh_node and no constant_volume) compiled on upload
+// into a linear program that every lane of a wave walks in lockstep.
+//
+// In such graphs the reference visits children in a fixed order (object_list::hit,
+// scene_object.h:79-103); only which subtrees a ray enters differs per lane (list / rotate_y boxes).
+// The program is that visit order, flattened: the op index is wave-uniform, so op and node data
+// come through scalar loads and every branch on the op is a scalar branch; a lane that failed a
+// box is masked until the matching END op (its bit in `act` is clear), and the whole wave jumps
+// over a subtree no lane entered.  Hits record only (t, node); p/n/uv are derived once from the
+// winning primitive in its own instance frame -- the same operations on the same inputs as the
+// primitive's hit() (rect.cpp:24-45, sphere.cpp:13-46), so the record is bit-identical.
+#pragma once
+#include "mrt_trace.h"
+
+namespace mrtd {
+
+enum : uint32_t {
+    LOP_END = 0,
+    LOP_PRIM = 1,      // sphere / rect
+    LOP_MESH = 2,      // pod_bvh<triangle> (per-lane traversal, mesh_hit)
+    LOP_LIST = 3,      // object_list enter (box test), skip = index of its LOP_LIST_END
+    LOP_LIST_END = 4,
+    LOP_INST = 5,      // translate / rotate_y / fused translate(rotate_y) enter, skip = its LOP_INST_END
+    LOP_INST_END = 6,
+};
+
+// one op = the node's own record (no second load): code = op | kind << 8 | flags << 16
+struct LinOp {
+    uint32_t code, node, skip, mat;
+    float f[12];
+};
+static_assert(sizeof(LinOp) == 64, "LinOp is one 64 B scalar load");
+
+#define LOP_OP(o) ((o).code & 0xFFu)
+#define LOP_KIND(o) (((o).code >> 8) & 0xFFu)
+#define LOP_FLAGS(o) (((o).code >> 16) & 0xFFu)
+
+// t of the primitive's hit() or a miss; no record written.  KIND is wave-uniform at the call.
+template <uint32_t F, uint32_t KIND>
+__device__ __forceinline__ bool lin_prim_t(const LinOp& o, const Ray& r, float tmin, float tmax, float* tout) {
+    if constexpr (KIND == MRT_K_SPHERE) {  // sphere::hit (sphere.cpp:13-46)
+        f3 cen = f3{o.f[0], o.f[1], o.f[2]};
+        if ((F & FT_MOVING) && (LOP_FLAGS(o) & MRT_F_MOVING))
+            cen = add(cen, fmul((r.time - o.f[6]) / (o.f[7] - o.f[6]), sub(f3{o.f[3], o.f[4], o.f[5]}, cen)));
+        const float radius = o.f[8];
+        const f3 oc = sub(r.o, cen);
+        const float b = dot(oc, r.d);
+        const float c = sdot(oc) - radius * radius;
+        const float disc = b * b - c;
+        if (!(disc > 0)) return false;
+        const float sq = __builtin_sqrtf(disc);
+        float t = (-b - sq);
+        bool ok = t < tmax && t > tmin;
+        if (!ok && r.inside) {
+            t = (-b + sq);
+            ok = t < tmax && t > tmin;
+        }
+        *tout = t;
+        return ok;
+    } else {
+        // xy/xz/yz_rect::hit (rect.cpp:24-45, 69-90, 130-151)
+        constexpr int AX = KIND == MRT_K_XY ? 2 : KIND == MRT_K_XZ ? 1 : 0;
+        const float ns = o.f[5];
+        const float dn = AX == 2 ? (r.d.x * 0.0f + r.d.y * 0.0f) + r.d.z * ns
+                       : AX == 1 ? (r.d.x * 0.0f + r.d.y * ns) + r.d.z * 0.0f
+                                 : (r.d.x * ns + r.d.y * 0.0f) + r.d.z * 0.0f;
+        if (dn > 0.0f) return false;
+        const float oa = AX == 2 ? r.o.z : AX == 1 ? r.o.y : r.o.x;
+        const float da = AX == 2 ? r.d.z : AX == 1 ? r.d.y : r.d.x;
+        const float t = (o.f[4] - oa) / da;
+        if (t < tmin || t > tmax) return false;
+        const float ob = AX == 0 ? r.o.y : r.o.x, db = AX == 0 ? r.d.y : r.d.x;
+        const float oc = AX == 2 ? r.o.y : r.o.z, dc = AX == 2 ? r.d.y : r.d.z;
+        const float pb = ob + t * db;
+        const float pc = oc + t * dc;
+        if (pb < o.f[0] || pb > o.f[1] || pc < o.f[2] || pc > o.f[3]) return false;
+        *tout = t;
+        return true;
+    }
+}
+
+// the record the primitive's hit() writes for a hit at t (per-lane node: loaded from the table)
+template <uint32_t F>
+__device__ __forceinline__ void lin_prim_rec(const DScene& S, uint32_t node, const Ray& r, float t, HitRec& rec) {
+    const mrt_node& n = S.nodes[node];
+    const uint32_t kind = MRT_NODE_KIND(n);
+    rec.t = t;
+    rec.mat = n.mat;
+    rec.p = eval(r, t);
+    if (kind == MRT_K_SPHERE) {
+        const f3 cen = sphere_center<F>(n, r.time);
+        rec.n = divf(sub(rec.p, cen), n.f[8]);
+        if ((F & FT_UV) && (MRT_NODE_FLAGS(n) & MRT_F_NEEDUV)) sphere_uv(rec.n, &rec.u, &rec.v);
+        return;
+    }
+    const float ns = n.f[5];
+    if (kind == MRT_K_XY) {
+        rec.n = f3{0, 0, ns};
+        if ((F & FT_UV) && (MRT_NODE_FLAGS(n) & MRT_F_NEEDUV)) {
+            rec.u = ((r.o.x + t * r.d.x) - n.f[0]) / (n.f[1] - n.f[0]);
+            rec.v = ((r.o.y + t * r.d.y) - n.f[2]) / (n.f[3] - n.f[2]);
+        }
+    } else if (kind == MRT_K_XZ) {
+        rec.n = f3{0, ns, 0};
+        if ((F & FT_UV) && (MRT_NODE_FLAGS(n) & MRT_F_NEEDUV)) {
+            rec.u = ((r.o.x + t * r.d.x) - n.f[0]) / (n.f[1] - n.f[0]);
+            rec.v = ((r.o.z + t * r.d.z) - n.f[2]) / (n.f[3] - n.f[2]);
+        }
+    } else {
+        rec.n = f3{ns, 0, 0};
+        if ((F & FT_UV) && (MRT_NODE_FLAGS(n) & MRT_F_NEEDUV)) {
+            rec.u = ((r.o.y + t * r.d.y) - n.f[0]) / (n.f[1] - n.f[0]);
+            rec.v = ((r.o.z + t * r.d.z) - n.f[2]) / (n.f[3] - n.f[2]);
+        }
+    }
+}
+
+template <uint32_t F>
+__device__ __forceinline__ bool scene_hit_lin(const DScene& S, const Ray& ray0, float tmin, HitRec& rec, const LStack& L) {
+    Ray cur = ray0;
+    float closest = FLT_MAX_;
+    uint32_t act = 1u;            // bit l: this lane takes part at nesting level l
+    uint32_t lvl = 0;             // wave-uniform
+    uint32_t inst = MRT_NONE;     // wave-uniform: op index of the enclosing instance
+    uint32_t hnode = MRT_NONE;    // node of the closest hit so far (MRT_NONE: none)
+    uint32_t hinst = MRT_NONE;    // instance op it was found under
+    bool hdone = false;           // rec already holds the closest hit (mesh, or materialised)
+    for (uint32_t pc = 0;; pc++) {
+        const LinOp& o = S.prog[pc];
+        const uint32_t op = LOP_OP(o);
+        if (op == LOP_END) break;
+        const bool on = (act >> lvl) & 1u;
+        if (op == LOP_PRIM) {
+            if (on) {
+                float t;
+                bool h;
+                switch (LOP_KIND(o)) {  // uniform: a scalar branch
+                case MRT_K_SPHERE: h = lin_prim_t<F, MRT_K_SPHERE>(o, cur, tmin, closest, &t); break;
+                case MRT_K_XY: h = lin_prim_t<F, MRT_K_XY>(o, cur, tmin, closest, &t); break;
+                case MRT_K_XZ: h = lin_prim_t<F, MRT_K_XZ>(o, cur, tmin, closest, &t); break;
+                default: h = lin_prim_t<F, MRT_K_YZ>(o, cur, tmin, closest, &t); break;
+                }
+                if (h) {
+                    closest = t;
+                    hnode = o.node;
+                    hinst = inst;
+                    hdone = false;
+                }
+            }
+        } else if ((F & FT_MESH) && op == LOP_MESH) {
+            if (on && mesh_hit(S, S.nodes[o.node], cur, tmin, closest, rec, true, L)) {
+                closest = rec.t;
+                hnode = o.node;
+                hinst = inst;
+                hdone = true;
+            }
+        } else if (op == LOP_LIST) {  // object_list::hit box reject (scene_object.h:83)
+            bool in = on;
+            if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = aabb_hit(o.f, o.f + 3, cur, tmin, closest);
+            lvl++;
+            act = (act & ~(1u << lvl)) | ((uint32_t)in << lvl);
+            if (!__any(in)) pc = o.skip - 1;
+        } else if (op == LOP_LIST_END) {
+            lvl--;
+        } else if ((F & FT_INST) && op == LOP_INST) {
+            const uint32_t kind = LOP_KIND(o);
+            bool in = on;
+            Ray t;
+            if (kind == MRT_K_TRROTY) {  // translate::hit then rotate_y::hit (scene_object.cpp:9-18, 70-98)
+                const Ray moved = make_ray(sub(ray0.o, f3{o.f[8], o.f[9], o.f[10]}), ray0.d, ray0.time, 0);
+                if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = aabb_hit(o.f, o.f + 3, moved, tmin, closest);
+                t = rotate_ray(moved, o.f[6], o.f[7]);
+            } else if (kind == MRT_K_ROTY) {
+                if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = aabb_hit(o.f, o.f + 3, ray0, tmin, closest);
+                t = rotate_ray(ray0, o.f[6], o.f[7]);
+            } else {
+                t = make_ray(sub(ray0.o, f3{o.f[0], o.f[1], o.f[2]}), ray0.d, ray0.time, 0);
+            }
+            cur = t;
+            inst = pc;
+            lvl++;
+            act = (act & ~(1u << lvl)) | ((uint32_t)in << lvl);
+            if (!__any(in)) pc = o.skip - 1;
+        } else if ((F & FT_INST) && op == LOP_INST_END) {
+            // hits inside the instance: record in the instance frame, then back to the world
+            const LinOp& io = S.prog[inst];
+            if (hinst == inst) {
+                if (!hdone) lin_prim_rec<F>(S, hnode, cur, closest, rec);
+                const uint32_t kind = LOP_KIND(io);
+                if (kind == MRT_K_TRROTY) {
+                    unrotate_rec(rec, io.f[6], io.f[7]);
+                    rec.p = add(rec.p, f3{io.f[8], io.f[9], io.f[10]});
+                } else if (kind == MRT_K_ROTY) {
+                    unrotate_rec(rec, io.f[6], io.f[7]);
+                } else {
+                    rec.p = add(rec.p, f3{io.f[0], io.f[1], io.f[2]});
+                }
+                hdone = true;
+            }
+            cur = ray0;
+            inst = MRT_NONE;
+            lvl--;
+        }
+    }
+    if (hnode == MRT_NONE) return false;
+    if (!hdone) lin_prim_rec<F>(S, hnode, ray0, closest, rec);
+    return true;
+}
+
+}  // namespace mrtd

@@ -136,14 +136,17 @@ __global__ void __launch_bounds__(256) mrt_path_kernel(PathParams P) {
     if (lane == 0 && my) atomicAdd(P.rays, (unsigned long long)my);
 }
 
-// kernel variants by scene features (the smallest instantiated superset is launched)
-static const uint32_t kVariants[] = {FT_INST, FT_INST | FT_MESH | FT_METAL, FT_ALL};
+// kernel variants by scene features (the first instantiated superset is launched); FT_LIN
+// variants need the scene's linear hit program (mrt_lin.h), FT_ALL runs any graph
+static constexpr uint32_t kVariants[] = {FT_LIN | FT_INST, FT_LIN | FT_INST | FT_MESH | FT_METAL, FT_LIN | FT_ALL, FT_ALL};
+static constexpr uint32_t kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 typedef void (*path_kernel_t)(PathParams);
 static path_kernel_t kernel_for(uint32_t v) {
     switch (v) {
-    case 0: return mrt_path_kernel<FT_INST>;
-    case 1: return mrt_path_kernel<FT_INST | FT_MESH | FT_METAL>;
-    default: return mrt_path_kernel<FT_ALL>;
+    case 0: return mrt_path_kernel<kVariants[0]>;
+    case 1: return mrt_path_kernel<kVariants[1]>;
+    case 2: return mrt_path_kernel<kVariants[2]>;
+    default: return mrt_path_kernel<kVariants[3]>;
     }
 }
 
@@ -215,6 +218,7 @@ struct mrt_scene {
     uint32_t n_launch = 0;
     size_t rad_cap = 0, acc_cap = 0, lev_cap = 0, px_cap = 0, pr_cap = 0;
     uint64_t last_paths = 0;
+    uint32_t prog_ops = 0;  // linear hit program length (0: generic machine)
 };
 
 static mrt_status dev_alloc(mrt_scene* s, void** p, size_t bytes) {
@@ -304,6 +308,59 @@ struct GraphCheck {
     }
 };
 
+// Linear hit program (mrt_lin.h): object_list trees of primitives / meshes with at most one
+// instance level.  Returns false (generic kernel) for bvh_node, constant_volume, nested instances.
+struct LinCompiler {
+    const std::vector<mrt_node>& nodes;
+    const mrt_scene_view* v;
+    std::vector<LinOp> prog;
+    int max_lvl = 0;
+    LinOp op_of(uint32_t code, uint32_t id) {
+        const mrt_node& n = nodes[id];
+        LinOp o{};
+        o.code = code | ((n.kind & 0xFFu) << 8) | (n.kind & 0xFF0000u);
+        o.node = id;
+        o.skip = 0;
+        o.mat = n.mat;
+        for (int i = 0; i < 12; i++) o.f[i] = n.f[i];
+        return o;
+    }
+    bool emit(uint32_t id, int inst_depth, int lvl, int guard) {
+        if (id >= nodes.size() || guard > 256 || lvl > 30) return false;
+        const mrt_node& n = nodes[id];
+        const uint32_t k = n.kind & 0xFFu;
+        max_lvl = std::max(max_lvl, lvl);
+        switch (k) {
+        case MRT_K_SPHERE: case MRT_K_XY: case MRT_K_XZ: case MRT_K_YZ:
+            prog.push_back(op_of(LOP_PRIM, id));
+            return true;
+        case MRT_K_MESH:
+            prog.push_back(op_of(LOP_MESH, id));
+            return true;
+        case MRT_K_LIST: {
+            size_t at = prog.size();
+            prog.push_back(op_of(LOP_LIST, id));
+            for (uint32_t i = 0; i < n.b; i++)
+                if (!emit(v->children[n.a + i], inst_depth, lvl + 1, guard + 1)) return false;
+            prog[at].skip = (uint32_t)prog.size();
+            prog.push_back(op_of(LOP_LIST_END, id));
+            return true;
+        }
+        case MRT_K_TRANSLATE: case MRT_K_ROTY: case MRT_K_TRROTY: {
+            if (inst_depth > 0) return false;
+            size_t at = prog.size();
+            prog.push_back(op_of(LOP_INST, id));
+            if (!emit(n.a, inst_depth + 1, lvl + 1, guard + 1)) return false;
+            prog[at].skip = (uint32_t)prog.size();
+            prog.push_back(op_of(LOP_INST_END, id));
+            return true;
+        }
+        default:
+            return false;
+        }
+    }
+};
+
 static uint32_t scene_features(const mrt_scene_view* v, const std::vector<mrt_node>& nodes) {
     uint32_t f = 0;
     for (const mrt_node& n : nodes) {
@@ -383,12 +440,20 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     UP((const float4*)v->perlin_ranvec, 256, &S.ranvec);
     UP(v->perlin_perm, 768, &S.perm);
     UP(v->texels, (size_t)v->n_texels, &S.texels);
+    LinCompiler lc{nodes, v, {}};
+    const char* force_generic = getenv("MRT_FORCE_GENERIC");  // test hook: run the generic machine
+    const bool lin = !(force_generic && *force_generic && *force_generic != '0') && lc.emit(v->root, 0, 0, 0);
+    if (!lin) lc.prog.clear();
+    const uint32_t prog_ops = (uint32_t)lc.prog.size();
+    lc.prog.push_back(LinOp{});  // LOP_END
+    UP(lc.prog.data(), lc.prog.size(), &S.prog);
 #undef UP
     S.root = v->root;
     S.biased = v->biased;
     S.sky = v->sky;
     S.cam = v->camera;
     s->n_nodes = v->n_nodes;
+    s->prog_ops = prog_ops;
     void* p;
     if ((st = upload(s, &s->S, sizeof(DScene), &p))) { mrt_scene_free(s); return st; }
     s->d_S = (DScene*)p;
@@ -397,11 +462,13 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     s->d_rays = (unsigned long long*)((char*)p + 16);
     // kernel variant + LDS stacks sized from the scene graph (top frame lives in registers)
     s->features = scene_features(v, nodes);
-    s->variant = 2;
-    for (uint32_t i = 0; i < sizeof(kVariants) / sizeof(kVariants[0]); i++)
-        if ((s->features & ~kVariants[i]) == 0) { s->variant = i; break; }
-    s->lds_frames = (uint32_t)std::max(gc.max_frames - 1, 0);
-    s->lds_rays = (uint32_t)gc.max_rays;
+    if (lin) s->features |= FT_LIN;
+    s->variant = kNumVariants - 1;
+    for (uint32_t i = 0; i < kNumVariants; i++)
+        if ((s->features & ~kVariants[i]) == 0 && (kVariants[i] & FT_LIN) == (s->features & FT_LIN)) { s->variant = i; break; }
+    const bool lin_kernel = (kVariants[s->variant] & FT_LIN) != 0;
+    s->lds_frames = lin_kernel ? 0 : (uint32_t)std::max(gc.max_frames - 1, 0);
+    s->lds_rays = lin_kernel ? 0 : (uint32_t)gc.max_rays;
     s->lds_mesh = (uint32_t)gc.max_mesh;
     s->lds_bytes = (size_t)4 * 64 * 4 * (s->lds_frames * 2 + s->lds_rays * 11 + s->lds_mesh);
     hipDeviceProp_t prop;
@@ -574,6 +641,16 @@ extern "C" mrt_status mrt_progress(mrt_scene* s, float* pct) {
     uint64_t c = 0;
     HIPCHK(hipMemcpy(&c, s->d_counter, 8, hipMemcpyDeviceToHost));
     *pct = s->last_paths ? std::min(100.0f, (float)(c * 100.0 / (double)s->last_paths)) : 0.0f;
+    return MRT_OK;
+}
+
+extern "C" mrt_status mrt_scene_kernel_info(const mrt_scene* s, mrt_kernel_info* out) {
+    if (!s || !out) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_scene_kernel_info: null");
+    out->features = s->features;
+    out->kernel_features = kVariants[s->variant];
+    out->lds_bytes = (uint32_t)s->lds_bytes;
+    out->grid = (uint32_t)s->grid;
+    out->prog_ops = s->prog_ops;
     return MRT_OK;
 }
 

@@ -1,6 +1,6 @@
 // mrt_shade.h -- textures, materials, pdfs and one trace() segment (main.cpp:66-118)
 #pragma once
-#include "mrt_trace.h"
+#include "mrt_lin.h"
 
 namespace mrtd {
 
@@ -174,7 +174,10 @@ __device__ __forceinline__ bool trace_segment(const DScene& S, PathState& ps, ui
     ps.rays++;
     HitRec rec;
     Ray& r = ps.r;
-    if (!scene_hit<F>(S, r, 0.001f, rec, ps.rng, Ls)) {
+    bool hit;
+    if constexpr ((F & FT_LIN) != 0) hit = scene_hit_lin<F>(S, r, 0.001f, rec, Ls);
+    else hit = scene_hit<F>(S, r, 0.001f, rec, ps.rng, Ls);
+    if (!hit) {
         if ((F & FT_SKY) && S.sky) {  // main.cpp:113-115
             float tt = 0.5f * (r.d.y + 1.0f);
             float o = 1.0f - tt;

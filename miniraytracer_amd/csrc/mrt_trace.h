@@ -5,6 +5,8 @@
 
 namespace mrtd {
 
+struct LinOp;  // mrt_lin.h
+
 // Device-side scene: the mrt_scene_view arrays resident in HBM.
 struct DScene {
     const mrt_node* __restrict__ nodes;
@@ -17,6 +19,7 @@ struct DScene {
     const float4* __restrict__ ranvec;
     const int32_t* __restrict__ perm;
     const uint8_t* __restrict__ texels;
+    const LinOp* __restrict__ prog;  // linear hit program (FT_LIN kernels), mrt_lin.h
     uint32_t root, biased, sky;
     mrt_camera cam;
 };
@@ -42,6 +45,7 @@ enum : uint32_t {
     FT_BSPHERE = 1u << 9,  // sphere in the biased (light-sampling) list
     FT_UV = 1u << 10,      // uv sampled on spheres / rects
     FT_ALL = (1u << 11) - 1,
+    FT_LIN = 1u << 11,     // scene graph compiled to a linear hit program (mrt_lin.h)
 };
 
 // Per-wave LDS stacks, lane-interleaved ([slot][word][lane]) so every access is conflict-free.

@@ -122,3 +122,34 @@ def test_full_size_cornell_properties(gpu, orc):
     assert 2.9 < rays / (w * h * spp) < 3.2
     oimg, _, _, _ = orc.render(sc, orc.desc(w, h, spp, threads=16, y0=230, y1=270))
     assert np.array_equal(img[230:270].view(np.uint32), oimg[230:270].view(np.uint32))
+
+
+@pytest.mark.parametrize("sid,w,h,spp", [(5, 64, 64, 16), (9, 40, 40, 9), (8, 40, 40, 9), (2, 48, 24, 9),
+                                         (3, 48, 24, 9), (4, 48, 24, 9)])
+def test_linear_program_equals_generic_machine(gpu, sid, w, h, spp, monkeypatch):
+    """Scenes without bvh_node/constant_volume run the linear hit program (mrt_lin.h); the generic
+    explicit-stack machine (MRT_FORCE_GENERIC=1 at upload) must give the same bits per path."""
+    sc = gpu.select_scene(sid, w / h)
+    lin = gpu.Renderer(sc, 0)
+    info = lin.kernel_info()
+    assert info["kernel_features"] & gpu._lib.FT_LIN and info["prog_ops"] > 0
+    monkeypatch.setenv("MRT_FORCE_GENERIC", "1")
+    gen = gpu.Renderer(sc, 0)
+    assert not gen.kernel_info()["kernel_features"] & gpu._lib.FT_LIN
+    d = gpu.render_desc(w, h, spp, flags=gpu._lib.RF_PATH_DEBUG)
+    a, ra = lin.render(d)
+    pa = lin.paths(w * h * (int(spp ** 0.5) ** 2))
+    b, rb = gen.render(d)
+    pb = gen.paths(w * h * (int(spp ** 0.5) ** 2))
+    assert ra == rb
+    assert np.array_equal(pa[1], pb[1])
+    assert np.array_equal(pa[0].view(np.uint32), pb[0].view(np.uint32))
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_kernel_selection(gpu):
+    """BVH / volume scenes fall back to the generic machine; the Cornell box runs a linear program."""
+    for sid, want_lin in [(0, False), (6, False), (7, False), (5, True), (9, True)]:
+        sc = gpu.select_scene(sid, 1.0)
+        info = gpu.Renderer(sc, 0).kernel_info()
+        assert bool(info["kernel_features"] & gpu._lib.FT_LIN) == want_lin, (sid, info)
