@@ -159,6 +159,18 @@ __device__ __forceinline__ bool aabb_hit(const float* bmin, const float* bmax, c
     return hi > lo;
 }
 
+__device__ __forceinline__ bool aabb_hit(f3 bmin, f3 bmax, const Ray& r, float tmin, float tmax) {
+    const float b[6] = {bmin.x, bmin.y, bmin.z, bmax.x, bmax.y, bmax.z};
+    return aabb_hit(b, b + 3, r, tmin, tmax);
+}
+
+// uniform-address reads of scene tables through the constant address space -> s_load
+#define MRT_CONST_AS __attribute__((address_space(4)))
+template <typename T>
+__device__ __forceinline__ const MRT_CONST_AS T* const_ptr(const T* p) {
+    return (const MRT_CONST_AS T*)p;
+}
+
 struct HitRec {
     float t;
     f3 p, n;

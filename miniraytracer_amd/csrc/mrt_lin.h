@@ -37,8 +37,8 @@ static_assert(sizeof(LinOp) == 64, "LinOp is one 64 B scalar load");
 #define LOP_FLAGS(o) (((o).code >> 16) & 0xFFu)
 
 // t of the primitive's hit() or a miss; no record written.  KIND is wave-uniform at the call.
-template <uint32_t F, uint32_t KIND>
-__device__ __forceinline__ bool lin_prim_t(const LinOp& o, const Ray& r, float tmin, float tmax, float* tout) {
+template <uint32_t F, uint32_t KIND, typename OP>
+__device__ __forceinline__ bool lin_prim_t(const OP& o, const Ray& r, float tmin, float tmax, float* tout) {
     if constexpr (KIND == MRT_K_SPHERE) {  // sphere::hit (sphere.cpp:13-46)
         f3 cen = f3{o.f[0], o.f[1], o.f[2]};
         if ((F & FT_MOVING) && (LOP_FLAGS(o) & MRT_F_MOVING))
@@ -126,8 +126,9 @@ __device__ __forceinline__ bool scene_hit_lin(const DScene& S, const Ray& ray0, 
     uint32_t hnode = MRT_NONE;    // node of the closest hit so far (MRT_NONE: none)
     uint32_t hinst = MRT_NONE;    // instance op it was found under
     bool hdone = false;           // rec already holds the closest hit (mesh, or materialised)
+    const MRT_CONST_AS LinOp* prog = const_ptr(S.prog);
     for (uint32_t pc = 0;; pc++) {
-        const LinOp& o = S.prog[pc];
+        const MRT_CONST_AS LinOp& o = prog[pc];
         const uint32_t op = LOP_OP(o);
         if (op == LOP_END) break;
         const bool on = (act >> lvl) & 1u;
@@ -157,7 +158,7 @@ __device__ __forceinline__ bool scene_hit_lin(const DScene& S, const Ray& ray0, 
             }
         } else if (op == LOP_LIST) {  // object_list::hit box reject (scene_object.h:83)
             bool in = on;
-            if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = aabb_hit(o.f, o.f + 3, cur, tmin, closest);
+            if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = aabb_hit(f3{o.f[0], o.f[1], o.f[2]}, f3{o.f[3], o.f[4], o.f[5]}, cur, tmin, closest);
             lvl++;
             act = (act & ~(1u << lvl)) | ((uint32_t)in << lvl);
             if (!__any(in)) pc = o.skip - 1;
@@ -166,25 +167,26 @@ __device__ __forceinline__ bool scene_hit_lin(const DScene& S, const Ray& ray0, 
         } else if ((F & FT_INST) && op == LOP_INST) {
             const uint32_t kind = LOP_KIND(o);
             bool in = on;
-            Ray t;
+            Ray moved;
             if (kind == MRT_K_TRROTY) {  // translate::hit then rotate_y::hit (scene_object.cpp:9-18, 70-98)
-                const Ray moved = make_ray(sub(ray0.o, f3{o.f[8], o.f[9], o.f[10]}), ray0.d, ray0.time, 0);
-                if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = aabb_hit(o.f, o.f + 3, moved, tmin, closest);
-                t = rotate_ray(moved, o.f[6], o.f[7]);
+                moved = make_ray(sub(ray0.o, f3{o.f[8], o.f[9], o.f[10]}), ray0.d, ray0.time, 0);
+                if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = aabb_hit(f3{o.f[0], o.f[1], o.f[2]}, f3{o.f[3], o.f[4], o.f[5]}, moved, tmin, closest);
             } else if (kind == MRT_K_ROTY) {
-                if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = aabb_hit(o.f, o.f + 3, ray0, tmin, closest);
-                t = rotate_ray(ray0, o.f[6], o.f[7]);
-            } else {
-                t = make_ray(sub(ray0.o, f3{o.f[0], o.f[1], o.f[2]}), ray0.d, ray0.time, 0);
+                if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = aabb_hit(f3{o.f[0], o.f[1], o.f[2]}, f3{o.f[3], o.f[4], o.f[5]}, ray0, tmin, closest);
             }
-            cur = t;
-            inst = pc;
             lvl++;
             act = (act & ~(1u << lvl)) | ((uint32_t)in << lvl);
-            if (!__any(in)) pc = o.skip - 1;
+            inst = pc;
+            if (!__any(in)) {
+                pc = o.skip - 1;
+                continue;
+            }
+            if (kind == MRT_K_TRROTY) cur = rotate_ray(moved, o.f[6], o.f[7]);
+            else if (kind == MRT_K_ROTY) cur = rotate_ray(ray0, o.f[6], o.f[7]);
+            else cur = make_ray(sub(ray0.o, f3{o.f[0], o.f[1], o.f[2]}), ray0.d, ray0.time, 0);
         } else if ((F & FT_INST) && op == LOP_INST_END) {
             // hits inside the instance: record in the instance frame, then back to the world
-            const LinOp& io = S.prog[inst];
+            const MRT_CONST_AS LinOp& io = prog[inst];
             if (hinst == inst) {
                 if (!hdone) lin_prim_rec<F>(S, hnode, cur, closest, rec);
                 const uint32_t kind = LOP_KIND(io);

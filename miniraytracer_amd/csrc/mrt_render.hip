@@ -30,9 +30,11 @@ using namespace mrtd;
     } while (0)
 
 struct PathParams {
-    const DScene* __restrict__ S;         // device copy (scalar-loaded)
-    const uint32_t* __restrict__ pixels;  // local pixel -> row-major pixel index
+    DScene sc;                            // by value: kernarg (constant) memory, scalar-loaded
+    const uint2* __restrict__ pixels;     // local pixel -> (x, y), row 0 = bottom
+    const float2* __restrict__ sdist;     // sample s -> grid offsets (main.cpp:324-331)
     uint32_t npix;                        // local pixel count
+    double inv_npix;                      // 1.0 / npix (path index -> sample row without a divide)
     uint32_t width, height, sq, ns;
     uint32_t s0;                          // first sample of this chunk
     uint32_t n_paths;                     // npix * chunk samples (< 2^32, enforced on the host)
@@ -52,15 +54,20 @@ struct PathParams {
 // wave's pool at once (ballot + mbcnt compaction), and a wave refills its pool 64 paths at a time
 // with one atomic (work_queue::getWork, work_queue.cpp:158-166).  Lanes stay busy until the pool
 // runs dry instead of idling until the longest path of a 64-path batch finishes.
+#ifdef MRT_WPE  // experiment hook: minimum waves per SIMD (caps VGPRs)
+#define MRT_PATH_ATTR __attribute__((amdgpu_waves_per_eu(MRT_WPE)))
+#else
+#define MRT_PATH_ATTR
+#endif
 template <uint32_t F>
-__global__ void __launch_bounds__(256) mrt_path_kernel(PathParams P) {
+__global__ void __launch_bounds__(256) MRT_PATH_ATTR mrt_path_kernel(PathParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t words = (P.lds_frames * 2 + P.lds_rays * 11 + P.lds_mesh) * 64;
     uint32_t* wb = lds + wave * words;
     const LStack Ls{wb, (float*)(wb + P.lds_frames * 128), wb + P.lds_frames * 128 + P.lds_rays * 704, lane};
-    const DScene& S = *P.S;
+    const DScene& S = P.sc;
     const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     float4* __restrict__ lev = P.lev + slot;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
@@ -86,17 +93,18 @@ __global__ void __launch_bounds__(256) mrt_path_kernel(PathParams P) {
                 const uint64_t i = rank < have ? (uint64_t)pool_next + rank : (uint64_t)nb + (rank - have);
                 if (i < P.n_paths) {
                     idx = (uint32_t)i;
-                    const uint32_t sl = idx / P.npix;
-                    const uint32_t lp = idx - sl * P.npix;
+                    // idx = sl * npix + lp; the double estimate is off by at most one either way
+                    uint32_t sl = (uint32_t)((double)idx * P.inv_npix);
+                    uint32_t lp = idx - sl * P.npix;
+                    if ((int32_t)lp < 0) { sl--; lp += P.npix; }
+                    if (lp >= P.npix) { sl++; lp -= P.npix; }
                     const uint32_t s = P.s0 + sl;
-                    const uint32_t pix = P.pixels[lp];
-                    const uint32_t x = pix % P.width, y = pix / P.width;
-                    // regular-grid sample offsets (main.cpp:324-331): s = i*sq + j
-                    const uint32_t gi = s / P.sq, gj = s - gi * P.sq;
-                    const float dx = ((float)gi + 0.5f) / (float)P.sq;
-                    const float dy = ((float)gj + 0.5f) / (float)P.sq;
-                    const float u = ((float)x + dx) / (float)P.width;
-                    const float v = ((float)y + dy) / (float)P.height;
+                    const uint2 xy = P.pixels[lp];
+                    const uint32_t x = xy.x, y = xy.y;
+                    const uint32_t pix = x + y * P.width;
+                    const float2 dd = P.sdist[s];  // ((i + 0.5) / sq, (j + 0.5) / sq), s = i*sq + j
+                    const float u = ((float)x + dd.x) / (float)P.width;
+                    const float v = ((float)y + dd.y) / (float)P.height;
                     const uint64_t path_id = (uint64_t)pix * P.ns + s;
                     pcg_seed(ps.rng, splitmix64(P.seed ^ path_id), path_id);
                     ps.r = camera_ray(S, ps.rng, u, v);
@@ -202,7 +210,9 @@ struct mrt_scene {
     mrt_render_desc wdesc{};
     bool have_ws = false;
     uint32_t npix = 0, chunk = 0;
-    uint32_t* d_pixels = nullptr;
+    uint2* d_pixels = nullptr;
+    float2* d_sdist = nullptr;
+    uint32_t sdist_sq = 0;
     float* d_rad = nullptr;
     uint32_t* d_path_rays = nullptr;
     float4* d_acc = nullptr;
@@ -216,7 +226,7 @@ struct mrt_scene {
     size_t lds_bytes = 0;
     std::vector<hipEvent_t> ev;  // [2*k]: start/stop of path-kernel launch k of the last render
     uint32_t n_launch = 0;
-    size_t rad_cap = 0, acc_cap = 0, lev_cap = 0, px_cap = 0, pr_cap = 0;
+    size_t rad_cap = 0, acc_cap = 0, lev_cap = 0, px_cap = 0, pr_cap = 0, sd_cap = 0;
     uint64_t last_paths = 0;
     uint32_t prog_ops = 0;  // linear hit program length (0: generic machine)
 };
@@ -487,7 +497,7 @@ extern "C" void mrt_scene_free(mrt_scene* s) {
     (void)hipSetDevice(s->device);
     for (void* p : s->allocs) (void)hipFree(p);
     for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
-    for (void* p : {(void*)s->d_pixels, (void*)s->d_rad, (void*)s->d_path_rays, (void*)s->d_acc, (void*)s->d_lev})
+    for (void* p : {(void*)s->d_pixels, (void*)s->d_sdist, (void*)s->d_rad, (void*)s->d_path_rays, (void*)s->d_acc, (void*)s->d_lev})
         if (p) (void)hipFree(p);
     delete s;
 }
@@ -526,8 +536,20 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
     if (relayout) {
         std::vector<uint32_t> px = mrt_internal_local_pixels(d);
         s->npix = (uint32_t)px.size();
-        if ((st = grow((void**)&s->d_pixels, &s->px_cap, px.size() * 4))) return st;
-        HIPCHK(hipMemcpy(s->d_pixels, px.data(), px.size() * 4, hipMemcpyHostToDevice));
+        std::vector<uint2> xy(px.size());
+        for (size_t i = 0; i < px.size(); i++) xy[i] = make_uint2(px[i] % d->width, px[i] / d->width);
+        if ((st = grow((void**)&s->d_pixels, &s->px_cap, xy.size() * 8))) return st;
+        HIPCHK(hipMemcpy(s->d_pixels, xy.data(), xy.size() * 8, hipMemcpyHostToDevice));
+    }
+    if (s->sdist_sq != d->sqrt_samples) {  // sample grid of main.cpp:319-332, in float like the reference
+        const uint32_t sq = d->sqrt_samples;
+        std::vector<float2> sd((size_t)sq * sq);
+        for (uint32_t i = 0; i < sq; i++)
+            for (uint32_t j = 0; j < sq; j++)
+                sd[(size_t)i * sq + j] = make_float2(((float)i + 0.5f) / (float)sq, ((float)j + 0.5f) / (float)sq);
+        if ((st = grow((void**)&s->d_sdist, &s->sd_cap, sd.size() * 8))) return st;
+        HIPCHK(hipMemcpy(s->d_sdist, sd.data(), sd.size() * 8, hipMemcpyHostToDevice));
+        s->sdist_sq = sq;
     }
     s->chunk = d->chunk_samples ? std::min(d->chunk_samples, ns) : auto_chunk(s->npix, ns);
     s->chunk = (uint32_t)std::min<uint64_t>(s->chunk, 0xFFFFFFFFull / std::max<uint32_t>(s->npix, 1));  // 32-bit path index
@@ -562,12 +584,14 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
     for (uint32_t s0 = 0; s0 < ns; s0 += s->chunk) {
         uint32_t s1 = std::min(ns, s0 + s->chunk);
         PathParams P{};
-        P.S = s->d_S;
+        P.sc = s->S;
         P.lds_frames = s->lds_frames;
         P.lds_rays = s->lds_rays;
         P.lds_mesh = s->lds_mesh;
         P.pixels = s->d_pixels;
+        P.sdist = s->d_sdist;
         P.npix = s->npix;
+        P.inv_npix = 1.0 / (double)std::max<uint32_t>(s->npix, 1);
         P.width = d->width;
         P.height = d->height;
         P.sq = d->sqrt_samples;
