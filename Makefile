@@ -14,7 +14,7 @@ CSRC     = miniraytracer_amd/csrc
 OBJDIR   = build/obj
 
 LIB_OBJS = $(OBJDIR)/mrt_render.o $(OBJDIR)/scene_builder.o $(OBJDIR)/mrt_common.o
-HDRS     = include/mrt.h include/mrt_scene.h $(wildcard $(CSRC)/*.h) Makefile
+HDRS     = include/mrt.h include/mrt_scene.h include/mrt_mathfn.h $(wildcard $(CSRC)/*.h) Makefile
 
 all: miniraytracer_amd/libmrt.so bin/mrt oracle/liboracle.so
 

@@ -150,7 +150,8 @@ def main():
                 traffic = pmc.get("hbm_bytes_per_launch")
         roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                    "kernel": "mrt_path_kernel", "kernel_ms": round(k_ms, 3), "bytes_per_ray": b_ray}
+                    "kernel": "mrt_path_kernel", "kernel_ms": round(k_ms, 3), "bytes_per_ray": b_ray,
+                    **{k: rnd.kernel_info()[k] for k in ("grid", "lds_bytes", "vgprs")}}
 
     if rank == 0:
         res = {

@@ -23,34 +23,50 @@
 #include <string.h>
 #endif
 
+/* Polynomial coefficients.  On the device each is materialised in an SGPR pair at its use (an
+ * opaque move the compiler cannot hoist): double literals cannot be instruction operands on gfx9,
+ * and hoisted out of the path loop they would pin ~30 VGPRs for the whole kernel.  The value is
+ * the same double either way. */
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ static inline double mrt_dc_dev(double c) {
+    unsigned long long b = __builtin_bit_cast(unsigned long long, c);
+    unsigned int lo = (unsigned int)b, hi = (unsigned int)(b >> 32);
+    asm volatile("" : "+s"(lo), "+s"(hi));
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+#define MRT_DC(x) mrt_dc_dev(x)
+#else
+#define MRT_DC(x) (x)
+#endif
+
 /* ---- sin / cos: Cody-Waite reduction by pi/2 (|x| < 2^20), Taylor kernels on [-pi/4, pi/4] ---- */
 MRT_HD void mrt_sincos_d(double x, double* s, double* c) {
     const double two_over_pi = 6.36619772367581382433e-01;
     const double pio2_1 = 1.57079632673412561417e+00;  /* first 33 bits of pi/2 */
     const double pio2_1t = 6.07710050650619224932e-11; /* pi/2 - pio2_1 */
-    double k = rint(x * two_over_pi);
-    double r = fma(-k, pio2_1, x);
-    r = fma(-k, pio2_1t, r);
+    double k = rint(x * MRT_DC(two_over_pi));
+    double r = fma(-k, MRT_DC(pio2_1), x);
+    r = fma(-k, MRT_DC(pio2_1t), r);
     double z = r * r;
     /* sin r = r + r^3 P(z) */
-    double p = 2.8114572543455206e-15;   /*  1/17! */
-    p = fma(p, z, -7.6471637318198164e-13); /* -1/15! */
-    p = fma(p, z, 1.6059043836821613e-10);  /*  1/13! */
-    p = fma(p, z, -2.5052108385441720e-08); /* -1/11! */
-    p = fma(p, z, 2.7557319223985893e-06);  /*  1/9!  */
-    p = fma(p, z, -1.9841269841269841e-04); /* -1/7!  */
-    p = fma(p, z, 8.3333333333333332e-03);  /*  1/5!  */
-    p = fma(p, z, -1.6666666666666666e-01); /* -1/3!  */
+    double p = MRT_DC(2.8114572543455206e-15);   /*  1/17! */
+    p = fma(p, z, MRT_DC(-7.6471637318198164e-13)); /* -1/15! */
+    p = fma(p, z, MRT_DC(1.6059043836821613e-10));  /*  1/13! */
+    p = fma(p, z, MRT_DC(-2.5052108385441720e-08)); /* -1/11! */
+    p = fma(p, z, MRT_DC(2.7557319223985893e-06));  /*  1/9!  */
+    p = fma(p, z, MRT_DC(-1.9841269841269841e-04)); /* -1/7!  */
+    p = fma(p, z, MRT_DC(8.3333333333333332e-03));  /*  1/5!  */
+    p = fma(p, z, MRT_DC(-1.6666666666666666e-01)); /* -1/3!  */
     double sr = fma(p * z, r, r);
     /* cos r = (1 - z/2) + z^2 Q(z) */
-    double q = -1.5619206968586225e-16;  /* -1/18! */
-    q = fma(q, z, 4.7794773323873853e-14);  /*  1/16! */
-    q = fma(q, z, -1.1470745597729725e-11); /* -1/14! */
-    q = fma(q, z, 2.0876756987868099e-09);  /*  1/12! */
-    q = fma(q, z, -2.7557319223985888e-07); /* -1/10! */
-    q = fma(q, z, 2.4801587301587302e-05);  /*  1/8!  */
-    q = fma(q, z, -1.3888888888888889e-03); /* -1/6!  */
-    q = fma(q, z, 4.1666666666666664e-02);  /*  1/4!  */
+    double q = MRT_DC(-1.5619206968586225e-16);  /* -1/18! */
+    q = fma(q, z, MRT_DC(4.7794773323873853e-14));  /*  1/16! */
+    q = fma(q, z, MRT_DC(-1.1470745597729725e-11)); /* -1/14! */
+    q = fma(q, z, MRT_DC(2.0876756987868099e-09));  /*  1/12! */
+    q = fma(q, z, MRT_DC(-2.7557319223985888e-07)); /* -1/10! */
+    q = fma(q, z, MRT_DC(2.4801587301587302e-05));  /*  1/8!  */
+    q = fma(q, z, MRT_DC(-1.3888888888888889e-03)); /* -1/6!  */
+    q = fma(q, z, MRT_DC(4.1666666666666664e-02));  /*  1/4!  */
     double cr = fma(q * z, z, fma(-0.5, z, 1.0));
     long long n = (long long)k & 3;
     double ss = (n & 1) ? cr : sr;
@@ -95,21 +111,21 @@ MRT_HD double mrt_log_d(double x) {
     }
     double s = (m - 1.0) / (m + 1.0);
     double z = s * s;
-    double p = 2.0 / 23.0;
-    p = fma(p, z, 2.0 / 21.0);
-    p = fma(p, z, 2.0 / 19.0);
-    p = fma(p, z, 2.0 / 17.0);
-    p = fma(p, z, 2.0 / 15.0);
-    p = fma(p, z, 2.0 / 13.0);
-    p = fma(p, z, 2.0 / 11.0);
-    p = fma(p, z, 2.0 / 9.0);
-    p = fma(p, z, 2.0 / 7.0);
-    p = fma(p, z, 2.0 / 5.0);
-    p = fma(p, z, 2.0 / 3.0);
+    double p = MRT_DC(2.0 / 23.0);
+    p = fma(p, z, MRT_DC(2.0 / 21.0));
+    p = fma(p, z, MRT_DC(2.0 / 19.0));
+    p = fma(p, z, MRT_DC(2.0 / 17.0));
+    p = fma(p, z, MRT_DC(2.0 / 15.0));
+    p = fma(p, z, MRT_DC(2.0 / 13.0));
+    p = fma(p, z, MRT_DC(2.0 / 11.0));
+    p = fma(p, z, MRT_DC(2.0 / 9.0));
+    p = fma(p, z, MRT_DC(2.0 / 7.0));
+    p = fma(p, z, MRT_DC(2.0 / 5.0));
+    p = fma(p, z, MRT_DC(2.0 / 3.0));
     double lm = fma(s * z, p, 2.0 * s);
     const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
     double de = (double)e;
-    return fma(de, ln2_hi, fma(de, ln2_lo, lm));
+    return fma(de, MRT_DC(ln2_hi), fma(de, MRT_DC(ln2_lo), lm));
 }
 MRT_HD float mrt_logf(float x) { return (float)mrt_log_d((double)x); }
 
@@ -126,19 +142,19 @@ MRT_HD double mrt_atan_d(double x) { /* |x| <= 1 */
     double t = x / (1.0 + sqrt(fma(x, x, 1.0)));
     t = t / (1.0 + sqrt(fma(t, t, 1.0)));
     double z = t * t;
-    double p = -1.0 / 27.0;
-    p = fma(p, z, 1.0 / 25.0);
-    p = fma(p, z, -1.0 / 23.0);
-    p = fma(p, z, 1.0 / 21.0);
-    p = fma(p, z, -1.0 / 19.0);
-    p = fma(p, z, 1.0 / 17.0);
-    p = fma(p, z, -1.0 / 15.0);
-    p = fma(p, z, 1.0 / 13.0);
-    p = fma(p, z, -1.0 / 11.0);
-    p = fma(p, z, 1.0 / 9.0);
-    p = fma(p, z, -1.0 / 7.0);
-    p = fma(p, z, 1.0 / 5.0);
-    p = fma(p, z, -1.0 / 3.0);
+    double p = MRT_DC(-1.0 / 27.0);
+    p = fma(p, z, MRT_DC(1.0 / 25.0));
+    p = fma(p, z, MRT_DC(-1.0 / 23.0));
+    p = fma(p, z, MRT_DC(1.0 / 21.0));
+    p = fma(p, z, MRT_DC(-1.0 / 19.0));
+    p = fma(p, z, MRT_DC(1.0 / 17.0));
+    p = fma(p, z, MRT_DC(-1.0 / 15.0));
+    p = fma(p, z, MRT_DC(1.0 / 13.0));
+    p = fma(p, z, MRT_DC(-1.0 / 11.0));
+    p = fma(p, z, MRT_DC(1.0 / 9.0));
+    p = fma(p, z, MRT_DC(-1.0 / 7.0));
+    p = fma(p, z, MRT_DC(1.0 / 5.0));
+    p = fma(p, z, MRT_DC(-1.0 / 3.0));
     return 4.0 * fma(t * z, p, t);
 }
 MRT_HD double mrt_atan2_d(double y, double x) {

@@ -54,13 +54,17 @@ struct PathParams {
 // wave's pool at once (ballot + mbcnt compaction), and a wave refills its pool 64 paths at a time
 // with one atomic (work_queue::getWork, work_queue.cpp:158-166).  Lanes stay busy until the pool
 // runs dry instead of idling until the longest path of a 64-path batch finishes.
-#ifdef MRT_WPE  // experiment hook: minimum waves per SIMD (caps VGPRs)
-#define MRT_PATH_ATTR __attribute__((amdgpu_waves_per_eu(MRT_WPE)))
+// Waves per SIMD the register allocator must reach (caps VGPRs at 512/W): the path loop is
+// latency-bound, so a few spilled registers cost less than the lost occupancy.  Tuned per
+// variant on MI355X (DESIGN.md "Occupancy").
+template <uint32_t F> struct PathOcc { static constexpr int W = (F & FT_LIN) ? 6 : 3; };
+#ifdef MRT_WPE  // experiment hook: override for every variant
+#define MRT_OCC(F) MRT_WPE
 #else
-#define MRT_PATH_ATTR
+#define MRT_OCC(F) PathOcc<F>::W
 #endif
 template <uint32_t F>
-__global__ void __launch_bounds__(256) MRT_PATH_ATTR mrt_path_kernel(PathParams P) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OCC(F)))) mrt_path_kernel(PathParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
@@ -229,6 +233,7 @@ struct mrt_scene {
     size_t rad_cap = 0, acc_cap = 0, lev_cap = 0, px_cap = 0, pr_cap = 0, sd_cap = 0;
     uint64_t last_paths = 0;
     uint32_t prog_ops = 0;  // linear hit program length (0: generic machine)
+    uint32_t vgprs = 0;
 };
 
 static mrt_status dev_alloc(mrt_scene* s, void** p, size_t bytes) {
@@ -484,9 +489,18 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
     if (s->lds_bytes > (size_t)prop.sharedMemPerBlock) { mrt_scene_free(s); return mrt_internal_fail(MRT_ERR_INVALID, "scene graph too deep for the LDS stacks"); }
-    int nb = 0;
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kernel_for(s->variant)), 256, s->lds_bytes));
+    // resident workgroups per CU: one 256-thread group = one wave per SIMD; VGPRs (512 per SIMD
+    // lane, granule 8) and LDS (160 KiB per CU) bound it.  (The runtime occupancy query
+    // under-counts gfx950 register budgets, so it is computed from the kernel's attributes.)
+    hipFuncAttributes fa{};
+    HIPCHK(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(kernel_for(s->variant))));
+    const int vg = std::max(8, (fa.numRegs + 7) & ~7);
+    int nb = std::min(8, 512 / vg);
+    if (s->lds_bytes) nb = std::min<int>(nb, (int)((160u * 1024u) / s->lds_bytes));
     if (nb < 1) nb = 1;
+    s->vgprs = (uint32_t)fa.numRegs;
+    if (const char* e = getenv("MRT_BLOCKS_PER_CU"))  // experiment hook
+        if (*e) nb = std::max(1, atoi(e));
     s->grid = prop.multiProcessorCount * nb;
     *out = s;
     return MRT_OK;
@@ -675,6 +689,7 @@ extern "C" mrt_status mrt_scene_kernel_info(const mrt_scene* s, mrt_kernel_info*
     out->lds_bytes = (uint32_t)s->lds_bytes;
     out->grid = (uint32_t)s->grid;
     out->prog_ops = s->prog_ops;
+    out->vgprs = s->vgprs;
     return MRT_OK;
 }
 
