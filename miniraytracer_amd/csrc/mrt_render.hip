@@ -57,7 +57,7 @@ struct PathParams {
 // Waves per SIMD the register allocator must reach (caps VGPRs at 512/W): the path loop is
 // latency-bound, so a few spilled registers cost less than the lost occupancy.  Tuned per
 // variant on MI355X (DESIGN.md "Occupancy").
-template <uint32_t F> struct PathOcc { static constexpr int W = (F & FT_LIN) ? 6 : 3; };
+template <uint32_t F> struct PathOcc { static constexpr int W = (F & FT_LIN) ? 6 : 4; };
 #ifdef MRT_WPE  // experiment hook: override for every variant
 #define MRT_OCC(F) MRT_WPE
 #else
