@@ -80,52 +80,100 @@ __device__ __forceinline__ bool lin_prim_t(const OP& o, const Ray& r, float tmin
     }
 }
 
-// the record the primitive's hit() writes for a hit at t (per-lane node: loaded from the table)
+// the record the primitive's hit() writes for a hit at t.  The node is per lane: each field is
+// loaded where it is used so few registers are live at once.
 template <uint32_t F>
 __device__ __forceinline__ void lin_prim_rec(const DScene& S, uint32_t node, const Ray& r, float t, HitRec& rec) {
-    const mrt_node& n = S.nodes[node];
-    const uint32_t kind = MRT_NODE_KIND(n);
+    const mrt_node* n = S.nodes + node;
+    const uint32_t code = n->kind;
+    const uint32_t kind = code & 0xFFu;
+    const bool needuv = (F & FT_UV) && ((code >> 16) & MRT_F_NEEDUV);
     rec.t = t;
-    rec.mat = n.mat;
+    rec.mat = n->mat;
     rec.p = eval(r, t);
     if (kind == MRT_K_SPHERE) {
-        const f3 cen = sphere_center<F>(n, r.time);
-        rec.n = divf(sub(rec.p, cen), n.f[8]);
-        if ((F & FT_UV) && (MRT_NODE_FLAGS(n) & MRT_F_NEEDUV)) sphere_uv(rec.n, &rec.u, &rec.v);
+        f3 cen = f3{n->f[0], n->f[1], n->f[2]};
+        if ((F & FT_MOVING) && ((code >> 16) & MRT_F_MOVING))
+            cen = add(cen, fmul((r.time - n->f[6]) / (n->f[7] - n->f[6]), sub(f3{n->f[3], n->f[4], n->f[5]}, cen)));
+        rec.n = divf(sub(rec.p, cen), n->f[8]);
+        if (needuv) sphere_uv(rec.n, &rec.u, &rec.v);
         return;
     }
-    const float ns = n.f[5];
+    const float ns = n->f[5];
+    float pb, pc;
     if (kind == MRT_K_XY) {
         rec.n = f3{0, 0, ns};
-        if ((F & FT_UV) && (MRT_NODE_FLAGS(n) & MRT_F_NEEDUV)) {
-            rec.u = ((r.o.x + t * r.d.x) - n.f[0]) / (n.f[1] - n.f[0]);
-            rec.v = ((r.o.y + t * r.d.y) - n.f[2]) / (n.f[3] - n.f[2]);
-        }
+        if (needuv) { pb = r.o.x + t * r.d.x; pc = r.o.y + t * r.d.y; }
     } else if (kind == MRT_K_XZ) {
         rec.n = f3{0, ns, 0};
-        if ((F & FT_UV) && (MRT_NODE_FLAGS(n) & MRT_F_NEEDUV)) {
-            rec.u = ((r.o.x + t * r.d.x) - n.f[0]) / (n.f[1] - n.f[0]);
-            rec.v = ((r.o.z + t * r.d.z) - n.f[2]) / (n.f[3] - n.f[2]);
-        }
+        if (needuv) { pb = r.o.x + t * r.d.x; pc = r.o.z + t * r.d.z; }
     } else {
         rec.n = f3{ns, 0, 0};
-        if ((F & FT_UV) && (MRT_NODE_FLAGS(n) & MRT_F_NEEDUV)) {
-            rec.u = ((r.o.y + t * r.d.y) - n.f[0]) / (n.f[1] - n.f[0]);
-            rec.v = ((r.o.z + t * r.d.z) - n.f[2]) / (n.f[3] - n.f[2]);
-        }
+        if (needuv) { pb = r.o.y + t * r.d.y; pc = r.o.z + t * r.d.z; }
+    }
+    if (needuv) {
+        rec.u = (pb - n->f[0]) / (n->f[1] - n->f[0]);
+        rec.v = (pc - n->f[2]) / (n->f[3] - n->f[2]);
     }
 }
 
+// the query ray parked in LDS while an instance ray occupies the registers ([word][lane])
+__device__ __forceinline__ void lin_save_ray(const LStack& L, const Ray& r) {
+    float* b = L.save + L.lane;
+    b[0] = r.o.x; b[64] = r.o.y; b[128] = r.o.z;
+    b[192] = r.d.x; b[256] = r.d.y; b[320] = r.d.z;
+    b[384] = r.time;
+    b[448] = __int_as_float(r.inside);
+    b[512] = __uint_as_float(r.mask);
+}
+__device__ __forceinline__ Ray lin_load_ray(const LStack& L) {
+    const float* b = L.save + L.lane;
+    Ray r;
+    r.o = f3{b[0], b[64], b[128]};
+    r.d = f3{b[192], b[256], b[320]};
+    r.time = b[384];
+    r.inside = __float_as_int(b[448]);
+    r.mask = __float_as_uint(b[512]);
+    r.inv = f3{0, 0, 0};  // never read on this path: box tests take 1/d on demand
+    return r;
+}
+// aabb::hit with invDir = 1/dir evaluated here, as the reference does per call (aabb.h:49)
+__device__ __forceinline__ bool lin_box(const MRT_CONST_AS LinOp& o, const Ray& r, float tmin, float tmax) {
+    Ray q = r;
+    q.inv = f3{1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z};
+    const float b[6] = {o.f[0], o.f[1], o.f[2], o.f[3], o.f[4], o.f[5]};
+    return aabb_hit(b, b + 3, q, tmin, tmax);
+}
+
+// record frames of instance hits, back to the world (scene_object.cpp:13-16, 85-93)
+template <typename OP>
+__device__ __forceinline__ void lin_untransform(const OP& io, HitRec& rec) {
+    const uint32_t kind = LOP_KIND(io);
+    if (kind == MRT_K_TRROTY) {
+        unrotate_rec(rec, io.f[6], io.f[7]);
+        rec.p = add(rec.p, f3{io.f[8], io.f[9], io.f[10]});
+    } else if (kind == MRT_K_ROTY) {
+        unrotate_rec(rec, io.f[6], io.f[7]);
+    } else {
+        rec.p = add(rec.p, f3{io.f[0], io.f[1], io.f[2]});
+    }
+}
+
+// r: the query ray; on return it holds the same values (reloaded from LDS when instances exist).
+// LDS per lane (L.save): [0..8] the query ray, [9..14] origin/direction of the instance ray of
+// the closest hit (written at the instance's END op when that hit lies inside it).
 template <uint32_t F>
-__device__ __forceinline__ bool scene_hit_lin(const DScene& S, const Ray& ray0, float tmin, HitRec& rec, const LStack& L) {
-    Ray cur = ray0;
+__device__ __forceinline__ bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, const LStack& L) {
+    constexpr bool INST = (F & FT_INST) != 0;
+    if (INST) lin_save_ray(L, r);
+    Ray cur = r;
     float closest = FLT_MAX_;
     uint32_t act = 1u;            // bit l: this lane takes part at nesting level l
     uint32_t lvl = 0;             // wave-uniform
     uint32_t inst = MRT_NONE;     // wave-uniform: op index of the enclosing instance
     uint32_t hnode = MRT_NONE;    // node of the closest hit so far (MRT_NONE: none)
-    uint32_t hinst = MRT_NONE;    // instance op it was found under
-    bool hdone = false;           // rec already holds the closest hit (mesh, or materialised)
+    uint32_t hinst = MRT_NONE;    // op index of the instance it lies in (MRT_NONE: world frame)
+    bool hdone = false;           // rec already holds the closest hit (mesh_hit writes it)
     const MRT_CONST_AS LinOp* prog = const_ptr(S.prog);
     for (uint32_t pc = 0;; pc++) {
         const MRT_CONST_AS LinOp& o = prog[pc];
@@ -158,21 +206,20 @@ __device__ __forceinline__ bool scene_hit_lin(const DScene& S, const Ray& ray0, 
             }
         } else if (op == LOP_LIST) {  // object_list::hit box reject (scene_object.h:83)
             bool in = on;
-            if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = aabb_hit(f3{o.f[0], o.f[1], o.f[2]}, f3{o.f[3], o.f[4], o.f[5]}, cur, tmin, closest);
+            if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, cur, tmin, closest);
             lvl++;
             act = (act & ~(1u << lvl)) | ((uint32_t)in << lvl);
             if (!__any(in)) pc = o.skip - 1;
-        } else if (op == LOP_LIST_END) {
-            lvl--;
-        } else if ((F & FT_INST) && op == LOP_INST) {
+        } else if (INST && op == LOP_INST) {
             const uint32_t kind = LOP_KIND(o);
             bool in = on;
-            Ray moved;
+            const Ray r0 = lin_load_ray(L);
             if (kind == MRT_K_TRROTY) {  // translate::hit then rotate_y::hit (scene_object.cpp:9-18, 70-98)
-                moved = make_ray(sub(ray0.o, f3{o.f[8], o.f[9], o.f[10]}), ray0.d, ray0.time, 0);
-                if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = aabb_hit(f3{o.f[0], o.f[1], o.f[2]}, f3{o.f[3], o.f[4], o.f[5]}, moved, tmin, closest);
+                cur = make_ray(sub(r0.o, f3{o.f[8], o.f[9], o.f[10]}), r0.d, r0.time, 0);
+                if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, cur, tmin, closest);
             } else if (kind == MRT_K_ROTY) {
-                if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = aabb_hit(f3{o.f[0], o.f[1], o.f[2]}, f3{o.f[3], o.f[4], o.f[5]}, ray0, tmin, closest);
+                cur = r0;
+                if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, cur, tmin, closest);
             }
             lvl++;
             act = (act & ~(1u << lvl)) | ((uint32_t)in << lvl);
@@ -181,32 +228,35 @@ __device__ __forceinline__ bool scene_hit_lin(const DScene& S, const Ray& ray0, 
                 pc = o.skip - 1;
                 continue;
             }
-            if (kind == MRT_K_TRROTY) cur = rotate_ray(moved, o.f[6], o.f[7]);
-            else if (kind == MRT_K_ROTY) cur = rotate_ray(ray0, o.f[6], o.f[7]);
-            else cur = make_ray(sub(ray0.o, f3{o.f[0], o.f[1], o.f[2]}), ray0.d, ray0.time, 0);
-        } else if ((F & FT_INST) && op == LOP_INST_END) {
-            // hits inside the instance: record in the instance frame, then back to the world
-            const MRT_CONST_AS LinOp& io = prog[inst];
-            if (hinst == inst) {
-                if (!hdone) lin_prim_rec<F>(S, hnode, cur, closest, rec);
-                const uint32_t kind = LOP_KIND(io);
-                if (kind == MRT_K_TRROTY) {
-                    unrotate_rec(rec, io.f[6], io.f[7]);
-                    rec.p = add(rec.p, f3{io.f[8], io.f[9], io.f[10]});
-                } else if (kind == MRT_K_ROTY) {
-                    unrotate_rec(rec, io.f[6], io.f[7]);
-                } else {
-                    rec.p = add(rec.p, f3{io.f[0], io.f[1], io.f[2]});
-                }
-                hdone = true;
+            if (kind == MRT_K_TRROTY || kind == MRT_K_ROTY) cur = rotate_ray(cur, o.f[6], o.f[7]);
+            else cur = make_ray(sub(r0.o, f3{o.f[0], o.f[1], o.f[2]}), r0.d, r0.time, 0);
+        } else if (INST && op == LOP_INST_END) {
+            if (hinst == inst) {  // keep the instance-frame ray of the hit for the record
+                float* b = L.save + L.lane + 9 * 64;
+                b[0] = cur.o.x; b[64] = cur.o.y; b[128] = cur.o.z;
+                b[192] = cur.d.x; b[256] = cur.d.y; b[320] = cur.d.z;
             }
-            cur = ray0;
+            cur = lin_load_ray(L);
             inst = MRT_NONE;
+            lvl--;
+        } else if (op == LOP_LIST_END) {
             lvl--;
         }
     }
+    if (INST) r = lin_load_ray(L);
     if (hnode == MRT_NONE) return false;
-    if (!hdone) lin_prim_rec<F>(S, hnode, ray0, closest, rec);
+    if (INST && hinst != MRT_NONE) {
+        if (!hdone) {
+            const float* b = L.save + L.lane + 9 * 64;
+            Ray ir = r;
+            ir.o = f3{b[0], b[64], b[128]};
+            ir.d = f3{b[192], b[256], b[320]};
+            lin_prim_rec<F>(S, hnode, ir, closest, rec);
+        }
+        lin_untransform(S.prog[hinst], rec);  // per-lane instance: vector loads
+    } else if (!hdone) {
+        lin_prim_rec<F>(S, hnode, r, closest, rec);
+    }
     return true;
 }
 

@@ -46,7 +46,7 @@ struct PathParams {
     unsigned long long* __restrict__ rays;
     float4* __restrict__ lev;             // fold levels: max_bounces rows x lev_stride
     size_t lev_stride;                    // = total threads of the grid
-    uint32_t lds_frames, lds_rays, lds_mesh;  // LDS stack slots per lane
+    uint32_t lds_frames, lds_rays, lds_mesh, lds_save;  // LDS stack slots / words per lane
 };
 
 // Persistent waves with per-lane path regeneration: every loop iteration advances each busy lane
@@ -68,9 +68,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t words = (P.lds_frames * 2 + P.lds_rays * 11 + P.lds_mesh) * 64;
+    const uint32_t words = (P.lds_frames * 2 + P.lds_rays * 11 + P.lds_mesh + P.lds_save) * 64;
     uint32_t* wb = lds + wave * words;
-    const LStack Ls{wb, (float*)(wb + P.lds_frames * 128), wb + P.lds_frames * 128 + P.lds_rays * 704, lane};
+    uint32_t* const wmesh = wb + P.lds_frames * 128 + P.lds_rays * 704;
+    const LStack Ls{wb, (float*)(wb + P.lds_frames * 128), wmesh, (float*)(wmesh + P.lds_mesh * 64), lane};
     const DScene& S = P.sc;
     const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     float4* __restrict__ lev = P.lev + slot;
@@ -150,7 +151,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
 
 // kernel variants by scene features (the first instantiated superset is launched); FT_LIN
 // variants need the scene's linear hit program (mrt_lin.h), FT_ALL runs any graph
-static constexpr uint32_t kVariants[] = {FT_LIN | FT_INST, FT_LIN | FT_INST | FT_MESH | FT_METAL, FT_LIN | FT_ALL, FT_ALL};
+static constexpr uint32_t kVariants[] = {FT_LIN | FT_INST, FT_LIN | FT_MESH | FT_METAL, FT_LIN | FT_ALL, FT_ALL};
 static constexpr uint32_t kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 typedef void (*path_kernel_t)(PathParams);
 static path_kernel_t kernel_for(uint32_t v) {
@@ -226,7 +227,7 @@ struct mrt_scene {
     unsigned long long* d_rays = nullptr;
     int grid = 0;
     uint32_t features = 0, variant = 0;
-    uint32_t lds_frames = 0, lds_rays = 0, lds_mesh = 0;
+    uint32_t lds_frames = 0, lds_rays = 0, lds_mesh = 0, lds_save = 0;
     size_t lds_bytes = 0;
     std::vector<hipEvent_t> ev;  // [2*k]: start/stop of path-kernel launch k of the last render
     uint32_t n_launch = 0;
@@ -485,7 +486,8 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     s->lds_frames = lin_kernel ? 0 : (uint32_t)std::max(gc.max_frames - 1, 0);
     s->lds_rays = lin_kernel ? 0 : (uint32_t)gc.max_rays;
     s->lds_mesh = (uint32_t)gc.max_mesh;
-    s->lds_bytes = (size_t)4 * 64 * 4 * (s->lds_frames * 2 + s->lds_rays * 11 + s->lds_mesh);
+    s->lds_save = (lin_kernel && (kVariants[s->variant] & FT_INST)) ? 15u : 0u;
+    s->lds_bytes = (size_t)4 * 64 * 4 * (s->lds_frames * 2 + s->lds_rays * 11 + s->lds_mesh + s->lds_save);
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
     if (s->lds_bytes > (size_t)prop.sharedMemPerBlock) { mrt_scene_free(s); return mrt_internal_fail(MRT_ERR_INVALID, "scene graph too deep for the LDS stacks"); }
@@ -602,6 +604,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.lds_frames = s->lds_frames;
         P.lds_rays = s->lds_rays;
         P.lds_mesh = s->lds_mesh;
+        P.lds_save = s->lds_save;
         P.pixels = s->d_pixels;
         P.sdist = s->d_sdist;
         P.npix = s->npix;

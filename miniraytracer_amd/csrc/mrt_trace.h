@@ -53,6 +53,7 @@ struct LStack {
     uint32_t* frames;  // 2 words per slot: node, state
     float* rays;       // 11 words per slot: o.xyz, d.xyz, inv.xyz, inside, mask
     uint32_t* mesh;    // 1 word per slot
+    float* save;       // 9 words: query ray parked by the linear program (mrt_lin.h)
     uint32_t lane;
 };
 
