@@ -171,6 +171,24 @@ __device__ __forceinline__ const MRT_CONST_AS T* const_ptr(const T* p) {
     return (const MRT_CONST_AS T*)p;
 }
 
+// Phase clock (experiment builds with -DMRT_PHASES): wave-uniform s_memtime deltas per phase.
+#ifdef MRT_PHASES
+struct PhaseClock {
+    uint64_t t, a[4];
+};
+#define PH_MARK(pc, i)                                      \
+    do {                                                    \
+        const uint64_t n_ = __builtin_amdgcn_s_memtime();   \
+        (pc).a[i] += n_ - (pc).t;                           \
+        (pc).t = n_;                                        \
+    } while (0)
+#else
+struct PhaseClock {};
+#define PH_MARK(pc, i) \
+    do {               \
+    } while (0)
+#endif
+
 struct HitRec {
     float t;
     f3 p, n;

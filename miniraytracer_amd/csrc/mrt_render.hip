@@ -44,8 +44,8 @@ struct PathParams {
     uint32_t* __restrict__ path_rays;     // optional (debug): n_paths
     uint32_t* __restrict__ counter;       // work counter (paths handed out)
     unsigned long long* __restrict__ rays;
-    float4* __restrict__ lev;             // fold levels: max_bounces rows x lev_stride
-    size_t lev_stride;                    // = total threads of the grid
+    float4* __restrict__ lev;             // fold levels, lane-major: [slot][lev_rows]
+    uint32_t lev_rows;                    // levels per lane (max_bounces, at least 1)
     uint32_t lds_frames, lds_rays, lds_mesh, lds_save;  // LDS stack slots / words per lane
 };
 
@@ -58,6 +58,17 @@ struct PathParams {
 // latency-bound, so a few spilled registers cost less than the lost occupancy.  Tuned per
 // variant on MI355X (DESIGN.md "Occupancy").
 template <uint32_t F> struct PathOcc { static constexpr int W = (F & FT_LIN) ? 6 : 4; };
+#ifdef MRT_PHASES
+__device__ unsigned long long g_phases[4];
+extern "C" int mrt_debug_phases(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phases), sizeof(g_phases)) != hipSuccess) return 1;
+    if (reset) {
+        unsigned long long z[4] = {0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_phases), z, sizeof(z)) != hipSuccess) return 1;
+    }
+    return 0;
+}
+#endif
 #ifdef MRT_WPE  // experiment hook: override for every variant
 #define MRT_OCC(F) MRT_WPE
 #else
@@ -74,7 +85,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
     const LStack Ls{wb, (float*)(wb + P.lds_frames * 128), wmesh, (float*)(wmesh + P.lds_mesh * 64), lane};
     const DScene& S = P.sc;
     const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    float4* __restrict__ lev = P.lev + slot;
+    float4* __restrict__ lev = P.lev + slot * P.lev_rows;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
 
     bool active = false;
@@ -83,6 +94,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
     uint32_t pool_next = 0, pool_end = 0;  // wave-uniform
     bool exhausted = false;
     uint32_t done_rays = 0;
+    PhaseClock ph{};
+#ifdef MRT_PHASES
+    ph.t = __builtin_amdgcn_s_memtime();
+#endif
     for (;;) {
         const uint64_t need = __ballot(!active);
         if (need && !exhausted) {
@@ -129,10 +144,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
             if (pool_next >= P.n_paths) exhausted = true;
         }
         if (!__any(active)) break;
+        PH_MARK(ph, 0);
         if (active) {
             f3 L;
-            if (trace_segment<F>(S, ps, P.max_bounces, lev, P.lev_stride, Ls, &L)) {
-                L = fold_levels(lev, P.lev_stride, ps.nlev, L);
+            const bool ended = trace_segment<F>(S, ps, P.max_bounces, lev, Ls, &L, ph);
+            PH_MARK(ph, 2);
+            if (ended) {
+                L = fold_levels(lev, ps.nlev, L);
                 float* dst = P.rad + (size_t)idx * 3;
                 dst[0] = L.x;
                 dst[1] = L.y;
@@ -142,7 +160,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
                 active = false;
             }
         }
+        PH_MARK(ph, 3);
     }
+#ifdef MRT_PHASES
+    if (lane == 0)
+        for (int i = 0; i < 4; i++) atomicAdd(&g_phases[i], (unsigned long long)ph.a[i]);
+#endif
     // one 64-bit add per wave
     uint64_t my = done_rays;
     for (int off = 32; off > 0; off >>= 1) my += __shfl_xor(my, off);
@@ -222,7 +245,7 @@ struct mrt_scene {
     uint32_t* d_path_rays = nullptr;
     float4* d_acc = nullptr;
     float4* d_lev = nullptr;
-    size_t lev_stride = 0;
+    uint32_t lev_rows = 0;
     uint64_t* d_counter = nullptr;
     unsigned long long* d_rays = nullptr;
     int grid = 0;
@@ -576,9 +599,8 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
     if ((st = grow((void**)&s->d_acc, &s->acc_cap, (size_t)s->npix * 16))) return st;
     if (d->flags & MRT_RF_PATH_DEBUG)
         if ((st = grow((void**)&s->d_path_rays, &s->pr_cap, paths * 4))) return st;
-    s->lev_stride = (size_t)s->grid * 256;
-    size_t levrows = std::max<uint32_t>(d->max_bounces, 1);
-    if ((st = grow((void**)&s->d_lev, &s->lev_cap, levrows * s->lev_stride * 16))) return st;
+    s->lev_rows = std::max<uint32_t>(d->max_bounces, 1);
+    if ((st = grow((void**)&s->d_lev, &s->lev_cap, (size_t)s->lev_rows * s->grid * 256 * 16))) return st;
     uint32_t launches = (ns + s->chunk - 1) / s->chunk;
     while (s->ev.size() < 2 * (size_t)launches) {
         hipEvent_t e;
@@ -622,7 +644,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.counter = (uint32_t*)s->d_counter;
         P.rays = d_rays ? (unsigned long long*)d_rays : s->d_rays;
         P.lev = s->d_lev;
-        P.lev_stride = s->lev_stride;
+        P.lev_rows = s->lev_rows;
         HIPCHK(hipMemsetAsync(s->d_counter, 0, 8, q));
         HIPCHK(hipEventRecord(s->ev[2 * s->n_launch], q));
         hipLaunchKernelGGL(kernel_for(s->variant), dim3(s->grid), dim3(256), s->lds_bytes, q, P);
