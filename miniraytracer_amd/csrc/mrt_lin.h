@@ -37,6 +37,8 @@ static_assert(sizeof(LinOp) == 64, "LinOp is one 64 B scalar load");
 #define LOP_FLAGS(o) (((o).code >> 16) & 0xFFu)
 
 // t of the primitive's hit() or a miss; no record written.  KIND is wave-uniform at the call.
+// Branch-free: every lane evaluates the whole test and the outcome is a predicate (the early
+// returns of the reference only skip work whose result is unused, so the outcome is the same).
 template <uint32_t F, uint32_t KIND, typename OP>
 __device__ __forceinline__ bool lin_prim_t(const OP& o, const Ray& r, float tmin, float tmax, float* tout) {
     if constexpr (KIND == MRT_K_SPHERE) {  // sphere::hit (sphere.cpp:13-46)
@@ -48,16 +50,12 @@ __device__ __forceinline__ bool lin_prim_t(const OP& o, const Ray& r, float tmin
         const float b = dot(oc, r.d);
         const float c = sdot(oc) - radius * radius;
         const float disc = b * b - c;
-        if (!(disc > 0)) return false;
         const float sq = __builtin_sqrtf(disc);
-        float t = (-b - sq);
-        bool ok = t < tmax && t > tmin;
-        if (!ok && r.inside) {
-            t = (-b + sq);
-            ok = t < tmax && t > tmin;
-        }
-        *tout = t;
-        return ok;
+        const float t1 = (-b - sq), t2 = (-b + sq);
+        const bool ok1 = (t1 < tmax) & (t1 > tmin);
+        const bool ok2 = (r.inside != 0) & (t2 < tmax) & (t2 > tmin);
+        *tout = ok1 ? t1 : t2;
+        return (disc > 0) & (ok1 | ok2);
     } else {
         // xy/xz/yz_rect::hit (rect.cpp:24-45, 69-90, 130-151)
         constexpr int AX = KIND == MRT_K_XY ? 2 : KIND == MRT_K_XZ ? 1 : 0;
@@ -65,18 +63,15 @@ __device__ __forceinline__ bool lin_prim_t(const OP& o, const Ray& r, float tmin
         const float dn = AX == 2 ? (r.d.x * 0.0f + r.d.y * 0.0f) + r.d.z * ns
                        : AX == 1 ? (r.d.x * 0.0f + r.d.y * ns) + r.d.z * 0.0f
                                  : (r.d.x * ns + r.d.y * 0.0f) + r.d.z * 0.0f;
-        if (dn > 0.0f) return false;
         const float oa = AX == 2 ? r.o.z : AX == 1 ? r.o.y : r.o.x;
         const float da = AX == 2 ? r.d.z : AX == 1 ? r.d.y : r.d.x;
         const float t = (o.f[4] - oa) / da;
-        if (t < tmin || t > tmax) return false;
         const float ob = AX == 0 ? r.o.y : r.o.x, db = AX == 0 ? r.d.y : r.d.x;
         const float oc = AX == 2 ? r.o.y : r.o.z, dc = AX == 2 ? r.d.y : r.d.z;
         const float pb = ob + t * db;
         const float pc = oc + t * dc;
-        if (pb < o.f[0] || pb > o.f[1] || pc < o.f[2] || pc > o.f[3]) return false;
         *tout = t;
-        return true;
+        return !(dn > 0.0f) & !((t < tmin) | (t > tmax)) & !((pb < o.f[0]) | (pb > o.f[1]) | (pc < o.f[2]) | (pc > o.f[3]));
     }
 }
 
@@ -181,22 +176,19 @@ __device__ __forceinline__ bool scene_hit_lin(const DScene& S, Ray& r, float tmi
         if (op == LOP_END) break;
         const bool on = (act >> lvl) & 1u;
         if (op == LOP_PRIM) {
-            if (on) {
-                float t;
-                bool h;
-                switch (LOP_KIND(o)) {  // uniform: a scalar branch
-                case MRT_K_SPHERE: h = lin_prim_t<F, MRT_K_SPHERE>(o, cur, tmin, closest, &t); break;
-                case MRT_K_XY: h = lin_prim_t<F, MRT_K_XY>(o, cur, tmin, closest, &t); break;
-                case MRT_K_XZ: h = lin_prim_t<F, MRT_K_XZ>(o, cur, tmin, closest, &t); break;
-                default: h = lin_prim_t<F, MRT_K_YZ>(o, cur, tmin, closest, &t); break;
-                }
-                if (h) {
-                    closest = t;
-                    hnode = o.node;
-                    hinst = inst;
-                    hdone = false;
-                }
+            float t;
+            bool h;
+            switch (LOP_KIND(o)) {  // uniform: a scalar branch
+            case MRT_K_SPHERE: h = lin_prim_t<F, MRT_K_SPHERE>(o, cur, tmin, closest, &t); break;
+            case MRT_K_XY: h = lin_prim_t<F, MRT_K_XY>(o, cur, tmin, closest, &t); break;
+            case MRT_K_XZ: h = lin_prim_t<F, MRT_K_XZ>(o, cur, tmin, closest, &t); break;
+            default: h = lin_prim_t<F, MRT_K_YZ>(o, cur, tmin, closest, &t); break;
             }
+            h = h & on;
+            closest = h ? t : closest;
+            hnode = h ? o.node : hnode;
+            hinst = h ? inst : hinst;
+            hdone = h ? false : hdone;
         } else if ((F & FT_MESH) && op == LOP_MESH) {
             if (on && mesh_hit(S, S.nodes[o.node], cur, tmin, closest, rec, true, L)) {
                 closest = rec.t;
