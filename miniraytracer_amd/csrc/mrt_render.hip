@@ -42,7 +42,7 @@ struct PathParams {
     uint32_t max_bounces;
     float* __restrict__ rad;              // n_paths * 3 floats, [s - s0][lp]
     uint32_t* __restrict__ path_rays;     // optional (debug): n_paths
-    uint32_t* __restrict__ counter;       // work counter (paths handed out)
+    unsigned long long* __restrict__ counter;  // work counter (paths handed out)
     unsigned long long* __restrict__ rays;
     float4* __restrict__ lev;             // fold levels, lane-major: [slot][lev_rows]
     uint32_t lev_rows;                    // levels per lane (max_bounces, at least 1)
@@ -58,6 +58,9 @@ struct PathParams {
 // latency-bound, so a few spilled registers cost less than the lost occupancy.  Tuned per
 // variant on MI355X (DESIGN.md "Occupancy").
 template <uint32_t F> struct PathOcc { static constexpr int W = (F & FT_LIN) ? 6 : 4; };
+#ifndef MRT_BATCH
+#define MRT_BATCH 256u  // paths a wave claims per atomic on the work counter (one hot address)
+#endif
 #ifdef MRT_PHASES
 __device__ unsigned long long g_phases[4];
 extern "C" int mrt_debug_phases(unsigned long long* out, int reset) {
@@ -91,7 +94,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
     bool active = false;
     uint32_t idx = 0;
     PathState ps;
-    uint32_t pool_next = 0, pool_end = 0;  // wave-uniform
+    uint64_t pool_next = 0, pool_end = 0;  // wave-uniform
     bool exhausted = false;
     uint32_t done_rays = 0;
     PhaseClock ph{};
@@ -102,15 +105,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
         const uint64_t need = __ballot(!active);
         if (need && !exhausted) {
             const uint32_t c = (uint32_t)__popcll(need);
-            const uint32_t have = pool_end - pool_next;
-            uint32_t nb = 0;
+            const uint32_t have = (uint32_t)(pool_end - pool_next);
+            uint64_t nb = 0;
             if (have < c) {
-                if (lane == 0) nb = atomicAdd(P.counter, 64u);
+                if (lane == 0) nb = atomicAdd(P.counter, (unsigned long long)MRT_BATCH);
                 nb = __shfl(nb, 0);
             }
             if (!active) {
                 const uint32_t rank = (uint32_t)__popcll(need & lt_mask);
-                const uint64_t i = rank < have ? (uint64_t)pool_next + rank : (uint64_t)nb + (rank - have);
+                const uint64_t i = rank < have ? pool_next + rank : nb + (rank - have);
                 if (i < P.n_paths) {
                     idx = (uint32_t)i;
                     // idx = sl * npix + lp; the double estimate is off by at most one either way
@@ -136,7 +139,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
             }
             if (have < c) {
                 pool_next = nb + (c - have);
-                pool_end = nb + 64u;
+                pool_end = nb + MRT_BATCH;
                 if (nb >= P.n_paths) exhausted = true;
             } else {
                 pool_next += c;
@@ -641,7 +644,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.max_bounces = d->max_bounces;
         P.rad = s->d_rad;
         P.path_rays = (d->flags & MRT_RF_PATH_DEBUG) ? s->d_path_rays : nullptr;
-        P.counter = (uint32_t*)s->d_counter;
+        P.counter = (unsigned long long*)s->d_counter;
         P.rays = d_rays ? (unsigned long long*)d_rays : s->d_rays;
         P.lev = s->d_lev;
         P.lev_rows = s->lev_rows;
