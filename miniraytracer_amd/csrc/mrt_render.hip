@@ -77,18 +77,23 @@ extern "C" int mrt_debug_phases(unsigned long long* out, int reset) {
 #else
 #define MRT_OCC(F) PathOcc<F>::W
 #endif
+// fold levels kept in LDS per lane (the rest in HBM): where the LDS budget at the target
+// occupancy allows it
+template <uint32_t F> struct PathLevLds { static constexpr uint32_t K = ((F & 0xFFFFu) == (FT_LIN | FT_INST)) ? 2u : 0u; };
 template <uint32_t F>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OCC(F)))) mrt_path_kernel(PathParams P) {
+    constexpr uint32_t LK = PathLevLds<F>::K;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t words = (P.lds_frames * 2 + P.lds_rays * 11 + P.lds_mesh + P.lds_save) * 64;
+    const uint32_t words = (P.lds_frames * 2 + P.lds_rays * 11 + P.lds_mesh + P.lds_save + LK * 4) * 64;
     uint32_t* wb = lds + wave * words;
     uint32_t* const wmesh = wb + P.lds_frames * 128 + P.lds_rays * 704;
     const LStack Ls{wb, (float*)(wb + P.lds_frames * 128), wmesh, (float*)(wmesh + P.lds_mesh * 64), lane};
     const DScene& S = P.sc;
     const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    float4* __restrict__ lev = P.lev + slot * P.lev_rows;
+    const LevStore<LK> lev{P.lev + slot * P.lev_rows,
+                           (float4*)(wmesh + (P.lds_mesh + P.lds_save) * 64) + lane};
     const uint64_t lt_mask = (1ull << lane) - 1ull;
 
     bool active = false;
@@ -150,7 +155,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
         PH_MARK(ph, 0);
         if (active) {
             f3 L;
-            const bool ended = trace_segment<F>(S, ps, P.max_bounces, lev, Ls, &L, ph);
+            const bool ended = trace_segment<F, LK>(S, ps, P.max_bounces, lev, Ls, &L, ph);
             PH_MARK(ph, 2);
             if (ended) {
                 L = fold_levels(lev, ps.nlev, L);
@@ -177,7 +182,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
 
 // kernel variants by scene features (the first instantiated superset is launched); FT_LIN
 // variants need the scene's linear hit program (mrt_lin.h), FT_ALL runs any graph
-static constexpr uint32_t kVariants[] = {FT_LIN | FT_INST, FT_LIN | FT_MESH | FT_METAL, FT_LIN | FT_ALL, FT_ALL};
+static constexpr uint32_t kVariants[] = {FT_LIN | FT_INST | MRT_SIG_BITS(SIG_CORNELL),
+                                         FT_LIN | FT_MESH | FT_METAL | MRT_SIG_BITS(SIG_ROOM_MESH),
+                                         FT_LIN | FT_INST,
+                                         FT_LIN | FT_MESH | FT_METAL,
+                                         FT_LIN | FT_ALL,
+                                         FT_ALL};
 static constexpr uint32_t kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 typedef void (*path_kernel_t)(PathParams);
 static path_kernel_t kernel_for(uint32_t v) {
@@ -185,8 +195,23 @@ static path_kernel_t kernel_for(uint32_t v) {
     case 0: return mrt_path_kernel<kVariants[0]>;
     case 1: return mrt_path_kernel<kVariants[1]>;
     case 2: return mrt_path_kernel<kVariants[2]>;
-    default: return mrt_path_kernel<kVariants[3]>;
+    case 3: return mrt_path_kernel<kVariants[3]>;
+    case 4: return mrt_path_kernel<kVariants[4]>;
+    default: return mrt_path_kernel<kVariants[5]>;
     }
+}
+static constexpr uint32_t kLevK[] = {PathLevLds<kVariants[0]>::K, PathLevLds<kVariants[1]>::K, PathLevLds<kVariants[2]>::K,
+                                     PathLevLds<kVariants[3]>::K, PathLevLds<kVariants[4]>::K, PathLevLds<kVariants[5]>::K};
+// first variant covering the scene's features: its own program shape first, then the interpreter
+static uint32_t pick_variant(uint32_t features) {
+    const uint32_t feat = features & 0xFFFFu, sig = MRT_SIG_OF(features);
+    for (int pass = 0; pass < 2; pass++)
+        for (uint32_t i = 0; i < kNumVariants; i++) {
+            const uint32_t vf = kVariants[i] & 0xFFFFu, vs = MRT_SIG_OF(kVariants[i]);
+            if ((feat & ~vf) != 0 || (vf & FT_LIN) != (feat & FT_LIN)) continue;
+            if (pass == 0 ? (vs == sig && sig != SIG_NONE) : vs == SIG_NONE) return i;
+        }
+    return kNumVariants - 1;
 }
 
 __device__ __forceinline__ float lum3(f3 c) { return (c.x * 0.212655f + c.y * 0.715158f) + c.z * 0.072187f; }
@@ -504,16 +529,16 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     s->d_rays = (unsigned long long*)((char*)p + 16);
     // kernel variant + LDS stacks sized from the scene graph (top frame lives in registers)
     s->features = scene_features(v, nodes);
+    const char* no_sig = getenv("MRT_NO_SIG");  // test hook: run the interpreter on known shapes too
     if (lin) s->features |= FT_LIN;
-    s->variant = kNumVariants - 1;
-    for (uint32_t i = 0; i < kNumVariants; i++)
-        if ((s->features & ~kVariants[i]) == 0 && (kVariants[i] & FT_LIN) == (s->features & FT_LIN)) { s->variant = i; break; }
+    if (lin && !(no_sig && *no_sig && *no_sig != '0')) s->features |= MRT_SIG_BITS(lin_sig_of(lc.prog.data(), (uint32_t)lc.prog.size()));
+    s->variant = pick_variant(s->features);
     const bool lin_kernel = (kVariants[s->variant] & FT_LIN) != 0;
     s->lds_frames = lin_kernel ? 0 : (uint32_t)std::max(gc.max_frames - 1, 0);
     s->lds_rays = lin_kernel ? 0 : (uint32_t)gc.max_rays;
     s->lds_mesh = (uint32_t)gc.max_mesh;
     s->lds_save = (lin_kernel && (kVariants[s->variant] & FT_INST)) ? 15u : 0u;
-    s->lds_bytes = (size_t)4 * 64 * 4 * (s->lds_frames * 2 + s->lds_rays * 11 + s->lds_mesh + s->lds_save);
+    s->lds_bytes = (size_t)4 * 64 * 4 * (s->lds_frames * 2 + s->lds_rays * 11 + s->lds_mesh + s->lds_save + kLevK[s->variant] * 4);
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
     if (s->lds_bytes > (size_t)prop.sharedMemPerBlock) { mrt_scene_free(s); return mrt_internal_fail(MRT_ERR_INVALID, "scene graph too deep for the LDS stacks"); }

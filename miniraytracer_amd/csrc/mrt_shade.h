@@ -1,6 +1,6 @@
 // mrt_shade.h -- textures, materials, pdfs and one trace() segment (main.cpp:66-118)
 #pragma once
-#include "mrt_lin.h"
+#include "mrt_sig.h"
 
 namespace mrtd {
 
@@ -152,9 +152,29 @@ struct PathState {
     Ray r;
     Pcg rng;
     uint32_t depth;  // bounces so far (trace depth)
-    uint32_t nlev;   // stored fold levels
+    uint32_t nlev;   // stored fold levels | LEV_LOUD once a level could turn a black result non-zero
     uint32_t rays;   // trace() calls of this path
 };
+static constexpr uint32_t LEV_LOUD = 0x80000000u;
+
+// Fold levels of one lane: the first LK in LDS ([level][lane] float4), deeper ones in HBM.
+template <uint32_t LK>
+struct LevStore {
+    float4* g;    // this lane's HBM rows
+    float4* lds;  // this lane's first LDS slot (stride 64 float4 per level)
+    __device__ __forceinline__ void put(uint32_t d, float4 v) const {
+        if (LK > 0 && d < LK) lds[d * 64] = v;
+        else g[d] = v;
+    }
+    __device__ __forceinline__ float4 get(uint32_t d) const { return (LK > 0 && d < LK) ? lds[d * 64] : g[d]; }
+};
+// A level is quiet when folding +0 through it gives +0 exactly: finite factors, for diffuse a
+// pdf > 0 (0 + (a * 0) / pdf == +0), for metal non-negative factors (att * +0 == +0).
+__device__ __forceinline__ bool quiet_level(float4 v) {
+    const bool fin = isfinite(v.x) && isfinite(v.y) && isfinite(v.z);
+    if (v.w < 0.0f) return fin & (((__float_as_uint(v.x) | __float_as_uint(v.y) | __float_as_uint(v.z)) >> 31) == 0);
+    return fin & (v.w > 0.0f) & isfinite(v.w);
+}
 
 // camera::get_ray (camera.h:38-44)
 __device__ __forceinline__ Ray camera_ray(const DScene& S, Pcg& rng, float s, float t) {
@@ -168,14 +188,15 @@ __device__ __forceinline__ Ray camera_ray(const DScene& S, Pcg& rng, float s, fl
 }
 
 // One segment.  Returns true when the path has ended; its radiance is then in *L.
-template <uint32_t F>
-__device__ __forceinline__ bool trace_segment(const DScene& S, PathState& ps, uint32_t max_bounces, float4* __restrict__ lev,
+template <uint32_t F, uint32_t LK>
+__device__ __forceinline__ bool trace_segment(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev,
                                               const LStack& Ls, f3* L, PhaseClock& ph) {
     ps.rays++;
     HitRec rec;
     Ray& r = ps.r;
     bool hit;
-    if constexpr ((F & FT_LIN) != 0) hit = scene_hit_lin<F>(S, r, 0.001f, rec, Ls);
+    if constexpr (MRT_SIG_OF(F) != SIG_NONE) hit = scene_hit_sig<F>(S, r, 0.001f, rec, Ls);
+    else if constexpr ((F & FT_LIN) != 0) hit = scene_hit_lin<F>(S, r, 0.001f, rec, Ls);
     else hit = scene_hit<F>(S, r, 0.001f, rec, ps.rng, Ls);
     PH_MARK(ph, 1);
     if (!hit) {
@@ -203,7 +224,9 @@ __device__ __forceinline__ bool trace_segment(const DScene& S, PathState& ps, ui
         f3 rs = random_in_sphere(ps.rng);
         f3 nd = add(reflected, fmul(1 - M.p, rs));
         f3 att = tex_sample<F>(S, M.tex, rec.u, rec.v, rec.p);
-        lev[ps.nlev++] = make_float4(att.x, att.y, att.z, -1.0f);
+        const float4 lv = make_float4(att.x, att.y, att.z, -1.0f);
+        lev.put(ps.nlev & ~LEV_LOUD, lv);
+        ps.nlev = (ps.nlev + 1) | (quiet_level(lv) ? 0u : LEV_LOUD);
         r = make_ray(rec.p, nd, r.time, 0);
         return false;
     }
@@ -264,7 +287,9 @@ __device__ __forceinline__ bool trace_segment(const DScene& S, PathState& ps, ui
         spdf = 1.0f / (2.0f * PI_F);
     }
     const float pdf_v = S.biased != MRT_NONE ? 0.5f * (biased_pdf_value<F>(S, S.biased, rec.p, sc.d, r.time) + sval) : sval;
-    lev[ps.nlev++] = make_float4(att.x * spdf, att.y * spdf, att.z * spdf, pdf_v);
+    const float4 lv = make_float4(att.x * spdf, att.y * spdf, att.z * spdf, pdf_v);
+    lev.put(ps.nlev & ~LEV_LOUD, lv);
+    ps.nlev = (ps.nlev + 1) | (quiet_level(lv) ? 0u : LEV_LOUD);
     r = sc;
     return false;
 }
@@ -275,13 +300,11 @@ __device__ __forceinline__ f3 fold_level(float4 a, f3 L) {
     if (a.w < 0.0f) return f3{a.x * L.x, a.y * L.y, a.z * L.z};
     return f3{0.0f + ((a.x * L.x) / a.w), 0.0f + ((a.y * L.y) / a.w), 0.0f + ((a.z * L.z) / a.w)};
 }
-__device__ __forceinline__ f3 fold_levels(const float4* __restrict__ lev, uint32_t nlev, f3 L) {
-    for (int d = (int)nlev - 1; d >= 0; d -= 2) {
-        const float4 a0 = lev[d];
-        const float4 a1 = lev[d > 0 ? d - 1 : 0];
-        L = fold_level(a0, L);
-        if (d >= 1) L = fold_level(a1, L);
-    }
+template <uint32_t LK>
+__device__ __forceinline__ f3 fold_levels(const LevStore<LK>& lev, uint32_t nlev, f3 L) {
+    // a black end through quiet levels stays +0 (the common escaped path): nothing to fold
+    if (!(nlev & LEV_LOUD) && ((__float_as_uint(L.x) | __float_as_uint(L.y) | __float_as_uint(L.z)) == 0)) return L;
+    for (int d = (int)(nlev & ~LEV_LOUD) - 1; d >= 0; d--) L = fold_level(lev.get((uint32_t)d), L);
     return L;
 }
 

@@ -1,0 +1,172 @@
+// mrt_sig.h -- linear hit programs of known shape, walked by code generated at compile time.
+//
+// The reference builds a fixed set of scenes (select_scene, scene.cpp:25-49).  Their linear
+// programs (mrt_lin.h) have a handful of distinct SHAPES -- the sequence of (op, kind, skip)
+// with the data left out.  For a shape listed here the kernel is instantiated with the walk
+// unrolled by template recursion: no op fetch/dispatch loop, every op kind and jump target a
+// compile-time constant, only the primitive data read (scalar loads at constant offsets).  The
+// semantics are exactly scene_hit_lin's: same tests, same order, same record.  Programs of any
+// other shape run the scene_hit_lin interpreter.
+#pragma once
+#include "mrt_lin.h"
+
+namespace mrtd {
+
+struct LinSig {
+    uint32_t n;         // ops, including the final LOP_END
+    uint8_t op[32];     // LOP_*
+    uint8_t kind[32];   // node kind (MRT_K_*)
+    uint8_t skip[32];   // matching END op of a LIST / INST
+};
+
+// shape ids (bits 16.. of a kernel's feature word; 0 = interpreter)
+enum : uint32_t { SIG_NONE = 0, SIG_CORNELL = 1, SIG_ROOM_MESH = 2, SIG_COUNT = 3 };
+#define MRT_SIG_OF(F) (((F) >> 16) & 0xFFu)
+#define MRT_SIG_BITS(id) ((uint32_t)(id) << 16)
+
+// clang-format off
+static constexpr LinSig kSigs[SIG_COUNT] = {
+    {0, {}, {}, {}},
+    // scene 5 (cornell_box, scene.cpp:286-330): walls + light, translate(rotate_y(box)), glass sphere
+    {20,
+     {LOP_LIST, LOP_PRIM, LOP_PRIM, LOP_PRIM, LOP_PRIM, LOP_PRIM, LOP_PRIM, LOP_INST, LOP_LIST, LOP_PRIM, LOP_PRIM, LOP_PRIM, LOP_PRIM,
+      LOP_PRIM, LOP_PRIM, LOP_LIST_END, LOP_INST_END, LOP_PRIM, LOP_LIST_END, LOP_END},
+     {MRT_K_LIST, MRT_K_YZ, MRT_K_YZ, MRT_K_XZ, MRT_K_XZ, MRT_K_XZ, MRT_K_XY, MRT_K_TRROTY, MRT_K_LIST, MRT_K_XY, MRT_K_XY, MRT_K_XZ,
+      MRT_K_XZ, MRT_K_YZ, MRT_K_YZ, MRT_K_LIST, MRT_K_TRROTY, MRT_K_SPHERE, MRT_K_LIST, 0},
+     {18, 0, 0, 0, 0, 0, 0, 16, 15, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}},
+    // scenes 8 / 9 (bunny / teapot in the Cornell room): walls + light + one pod_bvh mesh
+    {10,
+     {LOP_LIST, LOP_PRIM, LOP_PRIM, LOP_PRIM, LOP_PRIM, LOP_PRIM, LOP_PRIM, LOP_MESH, LOP_LIST_END, LOP_END},
+     {MRT_K_LIST, MRT_K_YZ, MRT_K_YZ, MRT_K_XZ, MRT_K_XZ, MRT_K_XZ, MRT_K_XY, MRT_K_MESH, MRT_K_LIST, 0},
+     {8, 0, 0, 0, 0, 0, 0, 0, 0, 0}},
+};
+// clang-format on
+
+// host: the shape id of a compiled program (SIG_NONE if it matches no entry)
+inline uint32_t lin_sig_of(const LinOp* prog, uint32_t n) {
+    for (uint32_t id = 1; id < SIG_COUNT; id++) {
+        const LinSig& g = kSigs[id];
+        if (g.n != n) continue;
+        bool ok = true;
+        for (uint32_t i = 0; i < n && ok; i++) {
+            const uint32_t op = prog[i].code & 0xFFu, kind = (prog[i].code >> 8) & 0xFFu;
+            ok = op == g.op[i] && (op == LOP_END || kind == g.kind[i]) &&
+                 ((op != LOP_LIST && op != LOP_INST) || prog[i].skip == g.skip[i]);
+        }
+        if (ok) return id;
+    }
+    return SIG_NONE;
+}
+
+struct SigState {
+    Ray cur;
+    float closest;
+    uint32_t hnode, hinst;
+    bool hdone;
+};
+
+template <uint32_t F, uint32_t SIG>
+struct SigWalk {
+    static constexpr const LinSig& G = kSigs[SIG];
+
+    // ops [PC, END) of the program, lanes `on` taking part
+    template <uint32_t PC, uint32_t END>
+    __device__ static __forceinline__ void run(const DScene& S, const MRT_CONST_AS LinOp* prog, float tmin, SigState& w, bool on,
+                                               HitRec& rec, const LStack& L) {
+        if constexpr (PC < END) {
+            constexpr uint32_t op = G.op[PC];
+            constexpr uint32_t kind = G.kind[PC];
+            const MRT_CONST_AS LinOp& o = prog[PC];
+            if constexpr (op == LOP_PRIM) {
+                float t;
+                const bool h = lin_prim_t<F, kind>(o, w.cur, tmin, w.closest, &t) & on;
+                w.closest = h ? t : w.closest;
+                w.hnode = h ? PC : w.hnode;  // op index; mapped to the node at the end
+                w.hinst = h ? cur_inst<PC>() : w.hinst;
+                w.hdone = h ? false : w.hdone;
+                run<PC + 1, END>(S, prog, tmin, w, on, rec, L);
+            } else if constexpr (op == LOP_MESH) {
+                if (on && mesh_hit(S, S.nodes[o.node], w.cur, tmin, w.closest, rec, true, L)) {
+                    w.closest = rec.t;
+                    w.hnode = PC;
+                    w.hinst = cur_inst<PC>();
+                    w.hdone = true;
+                }
+                run<PC + 1, END>(S, prog, tmin, w, on, rec, L);
+            } else if constexpr (op == LOP_LIST) {  // object_list::hit box reject (scene_object.h:83)
+                constexpr uint32_t skip = G.skip[PC];
+                const bool in = on && (!(LOP_FLAGS(o) & MRT_F_HASBOX) || lin_box(o, w.cur, tmin, w.closest));
+                if (__any(in)) run<PC + 1, skip>(S, prog, tmin, w, in, rec, L);
+                run<skip + 1, END>(S, prog, tmin, w, on, rec, L);
+            } else if constexpr (op == LOP_INST) {  // scene_object.cpp:9-18, 70-98
+                constexpr uint32_t skip = G.skip[PC];
+                const Ray r0 = lin_load_ray(L);
+                bool in = on;
+                if constexpr (kind == MRT_K_TRROTY) {
+                    w.cur = make_ray(sub(r0.o, f3{o.f[8], o.f[9], o.f[10]}), r0.d, r0.time, 0);
+                    if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, w.cur, tmin, w.closest);
+                } else if constexpr (kind == MRT_K_ROTY) {
+                    w.cur = r0;
+                    if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, w.cur, tmin, w.closest);
+                }
+                if (__any(in)) {
+                    if constexpr (kind == MRT_K_TRROTY || kind == MRT_K_ROTY) w.cur = rotate_ray(w.cur, o.f[6], o.f[7]);
+                    else w.cur = make_ray(sub(r0.o, f3{o.f[0], o.f[1], o.f[2]}), r0.d, r0.time, 0);
+                    run<PC + 1, skip>(S, prog, tmin, w, in, rec, L);
+                    if (w.hinst == PC) {  // keep the instance-frame ray of the hit for the record
+                        float* b = L.save + L.lane + 9 * 64;
+                        b[0] = w.cur.o.x; b[64] = w.cur.o.y; b[128] = w.cur.o.z;
+                        b[192] = w.cur.d.x; b[256] = w.cur.d.y; b[320] = w.cur.d.z;
+                    }
+                }
+                w.cur = lin_load_ray(L);
+                run<skip + 1, END>(S, prog, tmin, w, on, rec, L);
+            } else {
+                run<PC + 1, END>(S, prog, tmin, w, on, rec, L);
+            }
+        }
+    }
+
+    // op index of the instance enclosing op PC (MRT_NONE: world frame)
+    template <uint32_t PC>
+    __device__ static constexpr uint32_t cur_inst() {
+        uint32_t found = MRT_NONE;
+        for (uint32_t i = 0; i < PC; i++)
+            if (G.op[i] == LOP_INST && G.skip[i] > PC) found = i;
+        return found;
+    }
+};
+
+// scene_object::hit for a program of shape SIG (same contract as scene_hit_lin)
+template <uint32_t F>
+__device__ __forceinline__ bool scene_hit_sig(const DScene& S, Ray& r, float tmin, HitRec& rec, const LStack& L) {
+    constexpr uint32_t SIG = MRT_SIG_OF(F);
+    constexpr bool INST = (F & FT_INST) != 0;
+    if (INST) lin_save_ray(L, r);
+    const MRT_CONST_AS LinOp* prog = const_ptr(S.prog);
+    SigState w;
+    w.cur = r;
+    w.closest = FLT_MAX_;
+    w.hnode = MRT_NONE;
+    w.hinst = MRT_NONE;
+    w.hdone = false;
+    SigWalk<F, SIG>::template run<0, kSigs[SIG].n - 1>(S, prog, tmin, w, true, rec, L);
+    if (INST) r = lin_load_ray(L);
+    if (w.hnode == MRT_NONE) return false;
+    const uint32_t node = S.prog[w.hnode].node;  // per-lane op index: vector load
+    if (INST && w.hinst != MRT_NONE) {
+        if (!w.hdone) {
+            const float* b = L.save + L.lane + 9 * 64;
+            Ray ir = r;
+            ir.o = f3{b[0], b[64], b[128]};
+            ir.d = f3{b[192], b[256], b[320]};
+            lin_prim_rec<F>(S, node, ir, w.closest, rec);
+        }
+        lin_untransform(S.prog[w.hinst], rec);
+    } else if (!w.hdone) {
+        lin_prim_rec<F>(S, node, r, w.closest, rec);
+    }
+    return true;
+}
+
+}  // namespace mrtd

@@ -153,3 +153,26 @@ def test_kernel_selection(gpu):
         sc = gpu.select_scene(sid, 1.0)
         info = gpu.Renderer(sc, 0).kernel_info()
         assert bool(info["kernel_features"] & gpu._lib.FT_LIN) == want_lin, (sid, info)
+
+
+@pytest.mark.parametrize("sid,w,h,spp", [(5, 64, 64, 16), (9, 40, 40, 9), (8, 40, 40, 9)])
+def test_shape_specialised_walk_equals_interpreter(gpu, sid, w, h, spp, monkeypatch):
+    """Reference scenes whose linear program has a known shape (mrt_sig.h) run a walk unrolled at
+    compile time; it must give the same bits as the interpreter (MRT_NO_SIG=1 at upload)."""
+    sc = gpu.select_scene(sid, w / h)
+    fast = gpu.Renderer(sc, 0)
+    assert (fast.kernel_info()["kernel_features"] >> 16) & 0xFF != 0
+    monkeypatch.setenv("MRT_NO_SIG", "1")
+    interp = gpu.Renderer(sc, 0)
+    assert (interp.kernel_info()["kernel_features"] >> 16) & 0xFF == 0
+    assert interp.kernel_info()["kernel_features"] & gpu._lib.FT_LIN
+    d = gpu.render_desc(w, h, spp, flags=gpu._lib.RF_PATH_DEBUG)
+    n = w * h * (int(spp ** 0.5) ** 2)
+    a, ra = fast.render(d)
+    pa = fast.paths(n)
+    b, rb = interp.render(d)
+    pb = interp.paths(n)
+    assert ra == rb
+    assert np.array_equal(pa[1], pb[1])
+    assert np.array_equal(pa[0].view(np.uint32), pb[0].view(np.uint32))
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
