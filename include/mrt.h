@@ -13,6 +13,7 @@
  *   rays_out                              G_rayCounter                      main.cpp:55, 68, 403-405
  *   cancel                                G_isRunning                       main.cpp:54, 180, 235
  *   mrt_tonemap_argb                      Drago tone map + ARGB32            main.cpp:416-444, vec3.h:327-333
+ *   mrt_lum_max_device/mrt_tonemap_device the same, on the device              main.cpp:421-442
  *
  * Threading: one host thread per device; calls on distinct scenes are thread-safe, calls on the
  * same scene handle are not reentrant.
@@ -123,6 +124,13 @@ mrt_status mrt_scene_kernel_info(const mrt_scene* s, mrt_kernel_info* out);
 
 /* Drago adaptive-log tone map of a linear W*H*4 buffer to ARGB32 (main.cpp:416-444, no gamma). */
 mrt_status mrt_tonemap_argb(const float* rgb, uint32_t width, uint32_t height, uint32_t* argb_out);
+/* The same on the device, in two steps so ranks can combine L_wmax (all_reduce max) in between:
+ *   mrt_lum_max_device  *d_lwmax = max(*d_lwmax, max luminance of the n float4 pixels) -- the
+ *                       caller zeroes *d_lwmax first (main.cpp:424-429)
+ *   mrt_tonemap_device  d_argb[i] = ARGB32(Drago(d_rgb[i]; *d_lwmax)) (main.cpp:430-442)
+ * Pixel order is free (e.g. the local-pixel order of mrt_render_device); enqueued on `stream`. */
+mrt_status mrt_lum_max_device(const float* d_rgb, uint32_t n, float* d_lwmax, void* stream);
+mrt_status mrt_tonemap_device(const float* d_rgb, uint32_t n, const float* d_lwmax, uint32_t* d_argb, void* stream);
 
 const char* mrt_strerror(mrt_status s);
 const char* mrt_last_error(void);

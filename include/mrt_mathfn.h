@@ -184,4 +184,53 @@ MRT_HD float mrt_asinf(float x) {
     return (float)mrt_atan2_d(d, sqrt((1.0 - d) * (1.0 + d)));
 }
 
+/* ---- log10 / exp / pow: the Drago tone map of the image output (main.cpp:421-439) ---- */
+MRT_HD float mrt_log10f(float x) {
+    const double inv_ln10 = 4.34294481903251816668e-01; /* 1 / ln 10 */
+    return (float)(mrt_log_d((double)x) * MRT_DC(inv_ln10));
+}
+/* e^x: x = k ln2 + r, |r| <= ln2/2, Taylor to r^14, scaled by 2^k through the exponent field */
+MRT_HD double mrt_exp_d(double x) {
+    if (x != x) return x;
+    if (x > 709.0) return 1.0 / 0.0;
+    if (x < -745.0) return 0.0;
+    const double inv_ln2 = 1.44269504088896338700e+00;
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    double k = rint(x * MRT_DC(inv_ln2));
+    double r = fma(-k, MRT_DC(ln2_hi), x);
+    r = fma(-k, MRT_DC(ln2_lo), r);
+    double p = MRT_DC(1.0 / 87178291200.0);       /* 1/14! */
+    p = fma(p, r, MRT_DC(1.0 / 6227020800.0));    /* 1/13! */
+    p = fma(p, r, MRT_DC(1.0 / 479001600.0));     /* 1/12! */
+    p = fma(p, r, MRT_DC(1.0 / 39916800.0));      /* 1/11! */
+    p = fma(p, r, MRT_DC(1.0 / 3628800.0));       /* 1/10! */
+    p = fma(p, r, MRT_DC(1.0 / 362880.0));        /* 1/9!  */
+    p = fma(p, r, MRT_DC(1.0 / 40320.0));         /* 1/8!  */
+    p = fma(p, r, MRT_DC(1.0 / 5040.0));          /* 1/7!  */
+    p = fma(p, r, MRT_DC(1.0 / 720.0));           /* 1/6!  */
+    p = fma(p, r, MRT_DC(1.0 / 120.0));           /* 1/5!  */
+    p = fma(p, r, MRT_DC(1.0 / 24.0));            /* 1/4!  */
+    p = fma(p, r, MRT_DC(1.0 / 6.0));             /* 1/3!  */
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    double e = fma(p, r, 1.0);
+    /* e * 2^k in two exact steps (k in [-1075, 1024]) */
+    int ki = (int)k;
+    int k1 = ki / 2, k2 = ki - k1;
+    uint64_t b1 = (uint64_t)(k1 + 1023) << 52, b2 = (uint64_t)(k2 + 1023) << 52;
+    double s1, s2;
+    memcpy(&s1, &b1, 8);
+    memcpy(&s2, &b2, 8);
+    return (e * s1) * s2;
+}
+MRT_HD float mrt_expf(float x) { return (float)mrt_exp_d((double)x); }
+/* x^y for the tone map's x in [0, 1], y > 0 (and the general finite case x > 0) */
+MRT_HD float mrt_powf(float x, float y) {
+    if (y == 5.0f) return mrt_pow5f(x);
+    if (x == 1.0f || y == 0.0f) return 1.0f;
+    if (x == 0.0f) return y > 0.0f ? 0.0f : 1.0f / 0.0f;
+    if (!(x > 0.0f)) return (x - x) / (x - x); /* negative base with non-integer y, or NaN */
+    return (float)mrt_exp_d((double)y * mrt_log_d((double)x));
+}
+
 #endif

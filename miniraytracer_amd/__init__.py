@@ -157,6 +157,16 @@ class Renderer:
             pass
 
 
+def tonemap_device(d_rgb_ptr, n, d_lwmax_ptr, d_argb_ptr, stream_ptr=0, reduce=True):
+    """Device tone map of n float4 pixels (torch data_ptr()s).  reduce=True first max-reduces the
+    luminance into *d_lwmax (which the caller zeroed); pass reduce=False after combining L_wmax
+    across ranks yourself."""
+    if reduce:
+        check(lib().mrt_lum_max_device(C.c_void_p(d_rgb_ptr), n, C.c_void_p(d_lwmax_ptr), C.c_void_p(stream_ptr)), "mrt_lum_max_device")
+    check(lib().mrt_tonemap_device(C.c_void_p(d_rgb_ptr), n, C.c_void_p(d_lwmax_ptr), C.c_void_p(d_argb_ptr), C.c_void_p(stream_ptr)),
+          "mrt_tonemap_device")
+
+
 def tonemap_argb(img):
     img = np.ascontiguousarray(img, dtype=np.float32)
     h, w = img.shape[:2]

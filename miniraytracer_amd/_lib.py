@@ -102,6 +102,10 @@ def lib():
     L.mrt_render_debug.restype = st
     L.mrt_progress.argtypes = [C.c_void_p, C.POINTER(C.c_float)]
     L.mrt_progress.restype = st
+    L.mrt_lum_max_device.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
+    L.mrt_lum_max_device.restype = st
+    L.mrt_tonemap_device.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.mrt_tonemap_device.restype = st
     L.mrt_scene_kernel_info.argtypes = [C.c_void_p, C.POINTER(KernelInfo)]
     L.mrt_scene_kernel_info.restype = st
     L.mrt_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_uint32)]
@@ -130,5 +134,5 @@ EXPORTS = [
     "mrt_scene_upload", "mrt_scene_free", "mrt_default_render_desc", "mrt_local_pixels",
     "mrt_render", "mrt_render_device", "mrt_prepare", "mrt_render_debug", "mrt_progress",
     "mrt_tonemap_argb", "mrt_strerror", "mrt_last_error", "mrt_kernel_ms", "mrt_pack_obj",
-    "mrt_scene_kernel_info",
+    "mrt_scene_kernel_info", "mrt_lum_max_device", "mrt_tonemap_device",
 ]

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "mrt_internal.h"
+#include "../../include/mrt_tonemap.h"
 
 static thread_local std::string g_last_error;
 
@@ -239,33 +240,18 @@ extern "C" mrt_status mrt_local_pixels(const mrt_render_desc* d, uint32_t* n_out
 }
 
 // ---- Drago adaptive logarithmic tone map + ARGB32 (main.cpp:416-444, vec3.h:275-279, 327-333) ----
-static inline float lumf(const float* c) { return (c[0] * 0.212655f + c[1] * 0.715158f) + c[2] * 0.072187f; }
-static inline float logf_(float x) { return (float)std::log((double)x); }
 
+// Drago adaptive logarithmic mapping (main.cpp:416-444) on the host; include/mrt_tonemap.h
 extern "C" mrt_status mrt_tonemap_argb(const float* rgb, uint32_t W, uint32_t H, uint32_t* argb) {
     if (!rgb || !argb) return mrt_internal_fail(MRT_ERR_INVALID, "tonemap: null");
-    const float L_dmax = 230.0f;
-    const float bias = logf_(0.7f) / logf_(0.5f);
-    float L_wmax = 0;
     size_t n = (size_t)W * H;
+    float L_wmax = 0;
     for (size_t i = 0; i < n; i++) {
-        float l = lumf(rgb + i * 4);
+        float l = mrt_luminance(rgb + i * 4);
         L_wmax = (L_wmax < l) ? l : L_wmax;  // std::max
     }
-    float invlogmax = 1.0f / (float)std::log10((double)(L_wmax + 1.0f));
-    float invmax = 1.0f / L_wmax;
-    for (size_t i = 0; i < n; i++) {
-        const float* c = rgb + i * 4;
-        float lum = lumf(c);
-        float loglw = logf_(lum + 1.0f);
-        float lum_new = (L_dmax * 0.01f * invlogmax) * (loglw / logf_(2 + (float)std::pow((double)(lum * invmax), (double)bias) * 8));
-        uint32_t ch[3];
-        for (int k = 0; k < 3; k++) {
-            float v = (lum_new * c[k]) / (lum + 0.00001f);
-            v = (v < 1.0f ? v : 1.0f) * 255.99f;
-            ch[k] = (uint32_t)v;
-        }
-        argb[i] = (ch[0] << 16) | (ch[1] << 8) | ch[2];
-    }
+    mrt_tonemap_params tp;
+    mrt_tonemap_setup(L_wmax, &tp);
+    for (size_t i = 0; i < n; i++) argb[i] = mrt_tonemap_pixel(&tp, rgb + i * 4);
     return MRT_OK;
 }

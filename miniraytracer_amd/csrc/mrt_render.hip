@@ -20,6 +20,7 @@
 
 #include "mrt_internal.h"
 #include "mrt_shade.h"
+#include "../../include/mrt_tonemap.h"
 
 using namespace mrtd;
 
@@ -251,6 +252,49 @@ __global__ void __launch_bounds__(256) mrt_final_kernel(const float4* __restrict
         if (l > max_lum) c = mulf(c, max_lum / l);
     }
     out[lp] = make_float4(c.x, c.y, c.z, 0.0f);
+}
+
+// Image output on the device (main.cpp:416-444): global max luminance, then per-pixel Drago +
+// ARGB32 -- the functions of include/mrt_tonemap.h, the same bits as the host mrt_tonemap_argb.
+__global__ void __launch_bounds__(256) mrt_lum_max_kernel(const float4* __restrict__ rgb, uint32_t n, unsigned int* __restrict__ lwmax_bits) {
+    float m = 0.0f;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const float4 c = rgb[i];
+        const float cc[3] = {c.x, c.y, c.z};
+        const float l = mrt_luminance(cc);
+        m = (m < l) ? l : m;  // std::max(L_wmax, lum): NaN and negative luminance never win
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const float o = __shfl_xor(m, off);
+        m = (m < o) ? o : m;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMax(lwmax_bits, __float_as_uint(m));  // m >= +0: bit order == value order
+}
+__global__ void __launch_bounds__(256) mrt_tonemap_kernel(const float4* __restrict__ rgb, uint32_t n, const float* __restrict__ lwmax,
+                                                         uint32_t* __restrict__ argb) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    mrt_tonemap_params tp;
+    mrt_tonemap_setup(*lwmax, &tp);
+    const float4 c = rgb[i];
+    const float cc[3] = {c.x, c.y, c.z};
+    argb[i] = mrt_tonemap_pixel(&tp, cc);
+}
+
+extern "C" mrt_status mrt_lum_max_device(const float* d_rgb, uint32_t n, float* d_lwmax, void* stream) {
+    if (!d_rgb || !d_lwmax) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_lum_max_device: null");
+    if (n == 0) return MRT_OK;
+    const uint32_t blocks = std::min<uint32_t>((n + 255) / 256, 2048);
+    hipLaunchKernelGGL(mrt_lum_max_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const float4*)d_rgb, n, (unsigned int*)d_lwmax);
+    HIPCHK(hipGetLastError());
+    return MRT_OK;
+}
+extern "C" mrt_status mrt_tonemap_device(const float* d_rgb, uint32_t n, const float* d_lwmax, uint32_t* d_argb, void* stream) {
+    if (!d_rgb || !d_lwmax || !d_argb) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_tonemap_device: null");
+    if (n == 0) return MRT_OK;
+    hipLaunchKernelGGL(mrt_tonemap_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, (const float4*)d_rgb, n, d_lwmax, d_argb);
+    HIPCHK(hipGetLastError());
+    return MRT_OK;
 }
 
 // --------------------------------------------------------------------------------------------

@@ -5,7 +5,8 @@
 //
 //   --h-mode shipped   run the reference main() as shipped (threads, work_queue, tone map loop),
 //                      headless; print rays / trace seconds / Mrays/s from the reference's own
-//                      title string (main.cpp:399-406) and dump G_linearBackBuffer as PFM.
+//                      title string (main.cpp:399-406) and dump G_linearBackBuffer as PFM
+//                      (--h-out) and the Drago tone-mapped G_backBuffer as raw ARGB32 (--h-argb).
 //   --h-mode stream    "stream-matched" render: for every (pixel, sample) path re-seed the
 //                      reference PCG with the path key (see path_key below), call the reference
 //                      camera::get_ray + trace() unchanged, accumulate with draw() (mode 0,
@@ -50,9 +51,9 @@ float cosf(float x) { return mrt_cosf(x); }
 void sincosf(float x, float* s, float* c) { *s = mrt_sinf(x); *c = mrt_cosf(x); }
 float tanf(float x) { return mrt_tanf(x); }
 float logf(float x) { return mrt_logf(x); }
-float log10f(float x) { return (float)log10((double)x); }
-float expf(float x) { return (float)exp((double)x); }
-float powf(float x, float y) { return y == 5.0f ? mrt_pow5f(x) : (float)pow((double)x, (double)y); }
+float log10f(float x) { return mrt_log10f(x); }
+float expf(float x) { return mrt_expf(x); }
+float powf(float x, float y) { return mrt_powf(x, y); }
 float atan2f(float y, float x) { return mrt_atan2f(y, x); }
 float asinf(float x) { return mrt_asinf(x); }
 }
@@ -569,6 +570,13 @@ static int mode_shipped(int argc, char** argv) {
     double wall = MRT_TimeDelta(t0, MRT_GetTime());
     MRT_Params* p = getParams();
     if (out) write_pfm(out, G_linearBackBuffer, p->bufferWidth, p->bufferHeight);
+    if (const char* argb = harg(argc, argv, "--h-argb", nullptr)) {  // the tone-mapped display buffer
+        FILE* f = fopen(argb, "wb");
+        if (f) {
+            fwrite(G_backBuffer, 4, (size_t)p->bufferWidth * p->bufferHeight, f);
+            fclose(f);
+        }
+    }
     float secs = 0, mrays = 0;
     const char* tr = strstr(H_title.c_str(), "Trace: ");
     if (tr) sscanf(tr, "Trace: %fs - %f Mrays/s", &secs, &mrays);

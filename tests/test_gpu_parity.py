@@ -176,3 +176,47 @@ def test_shape_specialised_walk_equals_interpreter(gpu, sid, w, h, spp, monkeypa
     assert np.array_equal(pa[1], pb[1])
     assert np.array_equal(pa[0].view(np.uint32), pb[0].view(np.uint32))
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.mark.parametrize("sid", [5, 2])
+def test_device_tonemap_matches_reference_display_loop(gpu, sid):
+    """mrt_lum_max_device + mrt_tonemap_device on the reference display loop's own input give its
+    G_backBuffer bit for bit (tests/golden/tonemap_<id>.npz, main.cpp:416-444)."""
+    import os
+    import torch
+    from conftest import GOLDEN
+    g = np.load(os.path.join(GOLDEN, f"tonemap_{sid}.npz"))
+    h, w = g["argb"].shape
+    rgb = torch.zeros((h * w, 4), dtype=torch.float32)
+    rgb[:, :3] = torch.from_numpy(g["linear"].reshape(-1, 3).copy())
+    rgb = rgb.cuda()
+    lwmax = torch.zeros(1, dtype=torch.float32, device="cuda")
+    argb = torch.zeros(h * w, dtype=torch.int32, device="cuda")
+    gpu.tonemap_device(rgb.data_ptr(), h * w, lwmax.data_ptr(), argb.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(argb.cpu().numpy().view(np.uint32).reshape(h, w), g["argb"])
+
+
+def test_device_tonemap_of_rendered_image(gpu):
+    """Render into device memory (local tile order), tone-map on the device, compare with the host
+    tone map of the assembled image."""
+    import torch
+    w, h, spp = 64, 48, 16
+    sc, r = renderer(gpu, 5, w, h)
+    d = gpu.render_desc(w, h, spp)
+    r.prepare(d)
+    px = gpu.local_pixels(d)
+    out = torch.zeros((len(px), 4), dtype=torch.float32, device="cuda")
+    rays = torch.zeros(1, dtype=torch.int64, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    r.render_device(d, out.data_ptr(), rays.data_ptr(), s)
+    lwmax = torch.zeros(1, dtype=torch.float32, device="cuda")
+    argb = torch.zeros(len(px), dtype=torch.int32, device="cuda")
+    gpu.tonemap_device(out.data_ptr(), len(px), lwmax.data_ptr(), argb.data_ptr(), s)
+    torch.cuda.synchronize()
+    img = np.zeros((h * w, 4), dtype=np.float32)
+    img[px] = out.cpu().numpy()
+    want = gpu.tonemap_argb(img.reshape(h, w, 4)).reshape(-1)
+    got = np.zeros(h * w, dtype=np.uint32)
+    got[px] = argb.cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, want)

@@ -5,6 +5,8 @@ import os
 import re
 
 import numpy as np
+
+from conftest import GOLDEN
 import pytest
 
 from conftest import ROOT
@@ -103,8 +105,22 @@ def test_local_pixels_follow_work_queue_tiles(mrt, W, H, ts, world):
     assert np.all(seen == 1)
 
 
-def test_tonemap_matches_reference_formula(mrt):
-    """Drago mapping (main.cpp:416-444) + ARGB32 (vec3.h:327-333) on a synthetic HDR buffer."""
+@pytest.mark.parametrize("sid", [5, 2])
+def test_tonemap_matches_reference_display_loop(mrt, sid):
+    """Drago mapping (main.cpp:416-444) + ARGB32 (vec3.h:327-333): the host tone map equals, bit for
+    bit, the G_backBuffer the reference's own display loop produced from the same linear buffer
+    (tests/golden/tonemap_<id>.npz, exact reference build)."""
+    g = np.load(os.path.join(GOLDEN, f"tonemap_{sid}.npz"))
+    h, w = g["argb"].shape
+    img = np.zeros((h, w, 4), dtype=np.float32)
+    img[..., :3] = g["linear"]
+    argb = mrt.tonemap_argb(img)
+    assert np.array_equal(argb, g["argb"]), np.argwhere(argb != g["argb"])[:5]
+
+
+def test_tonemap_formula_with_libm(mrt):
+    """The same mapping restated with numpy's libm logs/pow: equal up to one level per channel
+    (the numerics contract's log/pow may differ from libm in the last float bit)."""
     rng = np.random.default_rng(0)
     img = np.zeros((7, 9, 4), dtype=np.float32)
     img[..., :3] = rng.exponential(0.5, size=(7, 9, 3)).astype(np.float32)
@@ -123,7 +139,8 @@ def test_tonemap_matches_reference_formula(mrt):
             ln = (f(230.0) * f(0.01) * invlogmax) * (loglw / f(np.log(np.float64(f(2) + pw * f(8)))))
             c = [(ln * img[y, x, k]) / (l + f(0.00001)) for k in range(3)]
             c = [int(f(min(v, f(1))) * f(255.99)) for v in c]
-            assert argb[y, x] == (c[0] << 16) | (c[1] << 8) | c[2]
+            got = [(int(argb[y, x]) >> s) & 255 for s in (16, 8, 0)]
+            assert all(abs(a - b) <= 1 for a, b in zip(got, c))
 
 
 def test_select_scene_errors_are_loud(mrt, tmp_path):

@@ -10,6 +10,7 @@ Fixtures (all small; data only -- inputs and expected outputs):
   stream_<id>.npz         stream-matched render: per-path radiance + ray counts + draw() image
   stream_5_mode1.npz      same for draw2() (mode 1) accumulation
   shipped_5.npz           as-shipped multithreaded reference render (statistical parity)
+  tonemap_<id>.npz        the reference display loop's input (linear buffer) and Drago/ARGB32 output
 """
 import gzip
 import json
@@ -102,6 +103,18 @@ def main():
             m = stream(sid, w, h, spp, depth, 0, f"stream_{sid}.npz")
             print("stream", sid, m)
         print("mode1", stream(5, 24, 24, 16, 32, 1, "stream_5_mode1.npz"))
+
+        # 6. Drago tone map + ARGB32 of the reference's own display loop (main.cpp:416-444), exact
+        #    build: the linear buffer it mapped and the ARGB it produced
+        for sid, w, h, spp in [(5, 48, 40, 16), (2, 40, 24, 4)]:
+            img, argb = os.path.join(tmp, "t.pfm"), os.path.join(tmp, "t.argb")
+            run(EXACT, ["-scene", sid, "-width", w, "-height", h, "-samples", spp, "-threads", 2, "-mode", 0,
+                        "--h-out", img, "--h-argb", argb])
+            raw = open(img, "rb").read().split(b"\n", 3)
+            lin = np.frombuffer(raw[3], dtype="<f4").reshape(h, w, 3)
+            out = np.fromfile(argb, dtype="<u4").reshape(h, w)
+            np.savez_compressed(os.path.join(OUT, f"tonemap_{sid}.npz"), linear=lin, argb=out)
+            print("tonemap", sid, int(out.min()), int(out.max()))
 
         # 5. shipped reference (multithreaded, its own worker seeds): statistical parity fixture
         if os.path.exists(os.path.join(OUT, "shipped_5.npz")) and "--force" not in sys.argv:
