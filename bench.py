@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--height", type=int, default=500)
     ap.add_argument("--samples", type=int, default=1024)
     ap.add_argument("--depth", type=int, default=32)
+    ap.add_argument("--tile-size", type=int, default=8,
+                    help="work_queue tile edge; also the multi-GPU partition grain (tile k -> rank k %% N)")
     ap.add_argument("--cpu-spp", type=int, default=256, help="spp of the bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_cornell_c2.json"))
@@ -89,7 +91,7 @@ def main():
     # scene build + upload + workspace: outside the timed region (main.cpp:309 precedes 375)
     scene = m.select_scene(args.scene, args.width / args.height)
     rnd = m.Renderer(scene, device=local)
-    desc = m.render_desc(args.width, args.height, args.samples, depth=args.depth, rank=rank, world=world)
+    desc = m.render_desc(args.width, args.height, args.samples, depth=args.depth, tile_size=args.tile_size, rank=rank, world=world)
     rnd.prepare(desc)
     px = m.local_pixels(desc)
     n_local = len(px)
@@ -99,7 +101,7 @@ def main():
 
     if world > 1:
         from miniraytracer_amd.dist import TileGather
-        tg = TileGather(args.width, args.height, args.samples, args.depth, world, rank, dev)
+        tg = TileGather(args.width, args.height, args.samples, args.depth, world, rank, dev, tile_size=args.tile_size)
         assert tg.n_local == n_local
 
     def step():
@@ -171,6 +173,7 @@ def main():
                                    f"{desc.sqrt_samples ** 2} spp, depth {args.depth}, draw() accumulation",
                        "scene": args.scene, "width": args.width, "height": args.height,
                        "spp": desc.sqrt_samples ** 2, "depth": args.depth, "parallelism": f"tiles{world}",
+                       "tile_size": args.tile_size,
                        "rays_per_step": nrays // args.steps},
             "roofline": roofline,
             "cpu_baseline": None,
