@@ -129,7 +129,7 @@ __device__ __forceinline__ Ray lin_load_ray(const LStack& L) {
     r.time = b[384];
     r.inside = __float_as_int(b[448]);
     r.mask = __float_as_uint(b[512]);
-    r.inv = f3{0, 0, 0};  // never read on this path: box tests take 1/d on demand
+    r.inv = f3{0, 0, 0};  // box tests take 1/d on demand; mesh_hit callers recompute it
     return r;
 }
 // aabb::hit with invDir = 1/dir evaluated here, as the reference does per call (aabb.h:49)
@@ -229,6 +229,7 @@ __device__ __forceinline__ bool scene_hit_lin(const DScene& S, Ray& r, float tmi
                 b[192] = cur.d.x; b[256] = cur.d.y; b[320] = cur.d.z;
             }
             cur = lin_load_ray(L);
+            if constexpr ((F & FT_MESH) != 0) cur.inv = f3{1.0f / cur.d.x, 1.0f / cur.d.y, 1.0f / cur.d.z};  // mesh_hit reads inv
             inst = MRT_NONE;
             lvl--;
         } else if (op == LOP_LIST_END) {
