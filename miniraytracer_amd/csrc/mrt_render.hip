@@ -524,6 +524,43 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
         f.f[8] = n.f[0]; f.f[9] = n.f[1]; f.f[10] = n.f[2];
         n = f;
     }
+    // pod_bvh -> wide nodes (both child boxes inline); MESH nodes get b = root ref
+    std::vector<MeshWide> wide;
+    {
+        std::vector<uint32_t> wide_of(v->n_mesh_nodes, MRT_NONE);
+        for (uint32_t i = 0; i < v->n_mesh_nodes; i++)
+            if ((v->mesh_nodes[i].count_order & 0xFFFFFFu) == 0) {
+                wide_of[i] = (uint32_t)wide.size();
+                wide.push_back(MeshWide{});
+            }
+        bool ok = wide.size() < MESH_LEAF;
+        auto ref_of = [&](uint32_t i) -> uint32_t {
+            if (i >= v->n_mesh_nodes) { ok = false; return 0; }
+            const mrt_mesh_node& m = v->mesh_nodes[i];
+            const uint32_t cnt = m.count_order & 0xFFFFFFu;
+            if (cnt == 0) return wide_of[i];
+            if (cnt > 0x7Fu || m.left_or_first > 0xFFFFFFu) ok = false;
+            return MESH_LEAF | (cnt << 24) | m.left_or_first;
+        };
+        for (uint32_t i = 0; i < v->n_mesh_nodes && ok; i++) {
+            if (wide_of[i] == MRT_NONE) continue;
+            const mrt_mesh_node& m = v->mesh_nodes[i];
+            const uint32_t l = m.left_or_first;
+            if (l + 1 >= v->n_mesh_nodes) { ok = false; break; }
+            MeshWide& W = wide[wide_of[i]];
+            const mrt_mesh_node &L = v->mesh_nodes[l], &R = v->mesh_nodes[l + 1];
+            for (int k = 0; k < 3; k++) {
+                W.lmin[k] = L.bmin[k]; W.lmax[k] = L.bmax[k];
+                W.rmin[k] = R.bmin[k]; W.rmax[k] = R.bmax[k];
+            }
+            W.lref = ref_of(l);
+            W.rref = ref_of(l + 1);
+            W.order = m.count_order >> 24;
+        }
+        for (mrt_node& n : nodes)
+            if ((n.kind & 0xFF) == MRT_K_MESH) n.b = ref_of(n.a);
+        if (!ok) return mrt_internal_fail(MRT_ERR_INVALID, "mesh BVH outside the device encoding (leaf > 127 triangles or > 2^24 triangles)");
+    }
     GraphCheck gc{nodes, v};
     gc.walk(v->root, 0, 0, false, 0);
     if (!gc.ok) return mrt_internal_fail(MRT_ERR_INVALID, gc.why.c_str());
@@ -544,6 +581,7 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     UP(nodes.data(), nodes.size(), &S.nodes);
     UP(v->children, v->n_children, &S.children);
     UP(v->mesh_nodes, v->n_mesh_nodes, &S.mnodes);
+    UP(wide.data(), wide.size(), &S.mwide);
     UP((const float4*)v->tri_geo, (size_t)v->n_tris * 3, &S.tri_geo);
     UP((const float4*)v->tri_nrm, (size_t)v->n_tris * 3, &S.tri_nrm);
     UP(v->materials, v->n_materials, &S.mats);

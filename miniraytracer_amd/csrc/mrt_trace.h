@@ -7,11 +7,27 @@ namespace mrtd {
 
 struct LinOp;  // mrt_lin.h
 
+// pod_bvh inner node with both children's boxes inline (built on upload from mrt_mesh_node[]):
+// one 64 B load tests both children.  Child ref: inner -> index into the wide array; leaf ->
+// MESH_LEAF | count << 24 | first triangle.
+struct MeshWide {
+    float lmin[3];
+    uint32_t lref;
+    float lmax[3];
+    uint32_t rref;
+    float rmin[3];
+    uint32_t order;  // the node's node_order byte (triangle.h:282-322)
+    float rmax[3];
+    uint32_t pad;
+};
+#define MESH_LEAF 0x80000000u
+
 // Device-side scene: the mrt_scene_view arrays resident in HBM.
 struct DScene {
     const mrt_node* __restrict__ nodes;
     const uint32_t* __restrict__ children;
     const mrt_mesh_node* __restrict__ mnodes;
+    const MeshWide* __restrict__ mwide;
     const float4* __restrict__ tri_geo;
     const float4* __restrict__ tri_nrm;
     const mrt_material* __restrict__ mats;
@@ -168,54 +184,66 @@ __device__ __forceinline__ bool tri_hit(const DScene& S, uint32_t i, const Ray& 
 
 // pod_bvh::hit (triangle.h:171-221): depth-first, closer child first (node_order & dirMask); the
 // first leaf that reports a hit ends the walk (every ancestor returns on hit_closer/hit_farther).
-// Short stack in LDS: only the farther child of each visited inner node is pushed.
+// Both children's boxes are tested when their parent is reached -- with the same (tmin, tmax) the
+// reference uses when it visits them, since nothing narrows tmax before the walk ends -- and only
+// a farther child whose box was hit is pushed (short stack in LDS).  n.a = root node, n.b = root ref.
+__device__ __forceinline__ bool mesh_leaf(const DScene& S, uint32_t ref, const mrt_node& n, const Ray& r, float tmin, float tmax, HitRec& rec,
+                                          bool full) {
+    const uint32_t first = ref & 0xFFFFFFu, cnt = (ref >> 24) & 0x7Fu;
+    bool has = false;
+    uint32_t best = 0;
+    float bu = 0, bv = 0, tt = tmax;
+    for (uint32_t k = 0; k < cnt; k++) {
+        float t, uu, vv;
+        if (tri_hit(S, first + k, r, tmin, tt, &t, &uu, &vv)) {
+            has = true;
+            tt = t;
+            best = first + k;
+            bu = uu;
+            bv = vv;
+        }
+    }
+    if (has) {
+        rec.t = tt;
+        if (full) {
+            const float4* q = S.tri_nrm + (size_t)best * 3;
+            f3 nm = ld3(q[0]), nu = ld3(q[1]), nv = ld3(q[2]);
+            rec.p = eval(r, tt);
+            rec.n = normalize(add(add(mulf(nm, (1 - bu) - bv), mulf(nu, bu)), mulf(nv, bv)));
+            rec.u = bu;
+            rec.v = bv;
+            rec.mat = n.mat;
+        }
+    }
+    return has;
+}
 __device__ __forceinline__ bool mesh_hit(const DScene& S, const mrt_node& n, const Ray& r, float tmin, float tmax, HitRec& rec, bool full,
                                          const LStack& L) {
-    uint32_t ni = n.a, msp = 0;
+    const mrt_mesh_node& root = S.mnodes[n.a];
+    if (!aabb_hit(root.bmin, root.bmax, r, tmin, tmax)) return false;
+    uint32_t ref = n.b, msp = 0;
     for (;;) {
-        const mrt_mesh_node& mn = S.mnodes[ni];
-        bool go = aabb_hit(mn.bmin, mn.bmax, r, tmin, tmax);
-        if (go) {
-            uint32_t cnt = mn.count_order & 0xFFFFFFu;
-            if (cnt) {
-                bool has = false;
-                uint32_t best = 0;
-                float bu = 0, bv = 0, tt = tmax;
-                for (uint32_t k = 0; k < cnt; k++) {
-                    float t, uu, vv;
-                    if (tri_hit(S, mn.left_or_first + k, r, tmin, tt, &t, &uu, &vv)) {
-                        has = true;
-                        tt = t;
-                        best = mn.left_or_first + k;
-                        bu = uu;
-                        bv = vv;
-                    }
-                }
-                if (has) {
-                    rec.t = tt;
-                    if (full) {
-                        const float4* q = S.tri_nrm + (size_t)best * 3;
-                        f3 nm = ld3(q[0]), nu = ld3(q[1]), nv = ld3(q[2]);
-                        rec.p = eval(r, tt);
-                        rec.n = normalize(add(add(mulf(nm, (1 - bu) - bv), mulf(nu, bu)), mulf(nv, bv)));
-                        rec.u = bu;
-                        rec.v = bv;
-                        rec.mat = n.mat;
-                    }
-                    return true;
-                }
-            } else {
-                uint32_t l = mn.left_or_first;
-                bool left_first = ((mn.count_order >> 24) & r.mask) != 0;
-                L.mesh[msp * 64 + L.lane] = left_first ? l + 1 : l;  // farther
-                msp++;
-                ni = left_first ? l : l + 1;  // closer
+        if (ref & MESH_LEAF) {
+            if (mesh_leaf(S, ref, n, r, tmin, tmax, rec, full)) return true;
+        } else {
+            const MeshWide& W = S.mwide[ref];
+            const bool hl = aabb_hit(W.lmin, W.lmax, r, tmin, tmax);
+            const bool hr = aabb_hit(W.rmin, W.rmax, r, tmin, tmax);
+            const bool left_first = (W.order & r.mask) != 0;
+            const uint32_t cref = left_first ? W.lref : W.rref, fref = left_first ? W.rref : W.lref;
+            const bool hc = left_first ? hl : hr, hf = left_first ? hr : hl;
+            if (hc) {
+                if (hf) L.mesh[(msp++) * 64 + L.lane] = fref;
+                ref = cref;
+                continue;
+            }
+            if (hf) {
+                ref = fref;
                 continue;
             }
         }
         if (msp == 0) return false;
-        msp--;
-        ni = L.mesh[msp * 64 + L.lane];
+        ref = L.mesh[(--msp) * 64 + L.lane];
     }
 }
 
