@@ -104,13 +104,25 @@ def main():
         tg = TileGather(args.width, args.height, args.samples, args.depth, world, rank, dev, tile_size=args.tile_size)
         assert tg.n_local == n_local
 
+    pending = [None]
+
     def step():
         rnd.render_device(desc, out.data_ptr(), rays.data_ptr(), stream.cuda_stream)
         if world > 1:
-            tg.gather(out)  # the one RCCL collective of the data path (tile shards -> rank 0)
+            # the one RCCL collective of the data path (tile shards -> rank 0), overlapped with the
+            # next render: finish the previous step's gather, then start this one's
+            if pending[0] is not None:
+                tg.finish(pending[0])
+            pending[0] = tg.start(out)
+
+    def drain():
+        if pending[0] is not None:
+            tg.finish(pending[0])
+            pending[0] = None
 
     for _ in range(args.warmup):
         step()
+    drain()
     torch.cuda.synchronize(dev)
     rays.zero_()
     if world > 1:
@@ -119,6 +131,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()

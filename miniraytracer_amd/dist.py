@@ -32,8 +32,17 @@ class TileGather:
 
     def gather(self, local):
         """local: [n_local, 4] float32 on `device`.  Returns the [H, W, 4] framebuffer on rank 0."""
+        return self.finish(self.start(local))
+
+    def start(self, local):
+        """Enqueue the gather of `local` (its contents are copied before this returns on the
+        device stream, so the caller may render into it again).  Returns a handle for finish()."""
         self.pad[: self.n_local].copy_(local)
-        dist.gather(self.pad, self.bufs if self.rank == 0 else None, dst=0)
+        return dist.gather(self.pad, self.bufs if self.rank == 0 else None, dst=0, async_op=True)
+
+    def finish(self, handle):
+        """Wait for a start()ed gather and, on rank 0, scatter the shards into the framebuffer."""
+        handle.wait()
         if self.rank != 0:
             return None
         for r in range(self.world):

@@ -37,6 +37,12 @@ def _worker(rank, world, port, q):
     tg = TileGather(W, H, SPP, 32, world, rank, torch.device("cpu"), tile_size=16)
     local = torch.from_numpy(img.reshape(-1, 4)[tg.px[rank]].copy())
     full = tg.gather(local)
+    full = full.clone() if full is not None else None
+    # overlapped form used by bench.py: start() copies the shard, finish() scatters on rank 0
+    h = tg.start(local * 0 + local)
+    full2 = tg.finish(h)
+    if rank == 0:
+        assert torch.equal(full, full2)
     total = torch.tensor([len(tg.px[rank])], dtype=torch.int64)
     dist.all_reduce(total)
     if rank == 0:
