@@ -126,6 +126,12 @@ class Renderer:
         check(lib().mrt_render_device(self._h, C.byref(desc), C.c_void_p(d_out_ptr), C.c_void_p(d_rays_ptr),
                                       C.c_void_p(stream_ptr)), "mrt_render_device")
 
+    def progress(self):
+        """Percent of the current / last render's paths handed out (work_queue::getPercentDone)."""
+        pct = C.c_float()
+        check(lib().mrt_progress(self._h, C.byref(pct)), "mrt_progress")
+        return pct.value
+
     def kernel_info(self):
         """dict(features, kernel_features, lds_bytes, grid, prog_ops) of the path kernel this scene runs."""
         ki = _lib.KernelInfo()

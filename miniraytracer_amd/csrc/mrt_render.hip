@@ -318,7 +318,13 @@ struct mrt_scene {
     float4* d_acc = nullptr;
     float4* d_lev = nullptr;
     uint32_t lev_rows = 0;
-    uint64_t* d_counter = nullptr;
+    uint64_t* d_counter = nullptr;   // 64 B scratch: [0] unused, [2] ray total of mrt_render
+    uint64_t* d_counters = nullptr;  // one work counter per chunk launch (progress reads them)
+    size_t cnt_cap = 0;
+    std::vector<uint64_t> chunk_paths;
+    hipStream_t pstream = nullptr;   // non-blocking stream for progress reads
+    hipEvent_t ev_reset = nullptr;   // recorded once this render's counters are zeroed
+    uint32_t n_chunks = 0;           // launches of the current render
     unsigned long long* d_rays = nullptr;
     int grid = 0;
     uint32_t features = 0, variant = 0;
@@ -646,7 +652,9 @@ extern "C" void mrt_scene_free(mrt_scene* s) {
     (void)hipSetDevice(s->device);
     for (void* p : s->allocs) (void)hipFree(p);
     for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
-    for (void* p : {(void*)s->d_pixels, (void*)s->d_sdist, (void*)s->d_rad, (void*)s->d_path_rays, (void*)s->d_acc, (void*)s->d_lev})
+    if (s->pstream) (void)hipStreamDestroy(s->pstream);
+    if (s->ev_reset) (void)hipEventDestroy(s->ev_reset);
+    for (void* p : {(void*)s->d_counters, (void*)s->d_pixels, (void*)s->d_sdist, (void*)s->d_rad, (void*)s->d_path_rays, (void*)s->d_acc, (void*)s->d_lev})
         if (p) (void)hipFree(p);
     delete s;
 }
@@ -712,6 +720,10 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
     s->lev_rows = std::max<uint32_t>(d->max_bounces, 1);
     if ((st = grow((void**)&s->d_lev, &s->lev_cap, (size_t)s->lev_rows * s->grid * 256 * 16))) return st;
     uint32_t launches = (ns + s->chunk - 1) / s->chunk;
+    if ((st = grow((void**)&s->d_counters, &s->cnt_cap, (size_t)launches * 8))) return st;
+    if (!s->pstream) HIPCHK(hipStreamCreateWithFlags(&s->pstream, hipStreamNonBlocking));
+    if (!s->ev_reset) HIPCHK(hipEventCreateWithFlags(&s->ev_reset, hipEventDisableTiming));
+    if (s->chunk_paths.size() < launches) s->chunk_paths.resize(launches, 0);
     while (s->ev.size() < 2 * (size_t)launches) {
         hipEvent_t e;
         HIPCHK(hipEventCreate(&e));
@@ -728,6 +740,12 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
     hipStream_t q = (hipStream_t)stream;
     uint32_t ns = d->sqrt_samples * d->sqrt_samples;
     HIPCHK(hipMemsetAsync(s->d_acc, 0, (size_t)s->npix * 16, q));
+    const uint32_t launches = (ns + s->chunk - 1) / s->chunk;
+    s->n_chunks = 0;
+    HIPCHK(hipMemsetAsync(s->d_counters, 0, (size_t)launches * 8, q));
+    HIPCHK(hipEventRecord(s->ev_reset, q));
+    for (uint32_t k = 0; k < launches; k++) s->chunk_paths[k] = (uint64_t)s->npix * (std::min(ns, (k + 1) * s->chunk) - k * s->chunk);
+    s->n_chunks = launches;
     s->n_launch = 0;
     for (uint32_t s0 = 0; s0 < ns; s0 += s->chunk) {
         uint32_t s1 = std::min(ns, s0 + s->chunk);
@@ -751,11 +769,10 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.max_bounces = d->max_bounces;
         P.rad = s->d_rad;
         P.path_rays = (d->flags & MRT_RF_PATH_DEBUG) ? s->d_path_rays : nullptr;
-        P.counter = (unsigned long long*)s->d_counter;
+        P.counter = (unsigned long long*)(s->d_counters + s->n_launch);
         P.rays = d_rays ? (unsigned long long*)d_rays : s->d_rays;
         P.lev = s->d_lev;
         P.lev_rows = s->lev_rows;
-        HIPCHK(hipMemsetAsync(s->d_counter, 0, 8, q));
         HIPCHK(hipEventRecord(s->ev[2 * s->n_launch], q));
         hipLaunchKernelGGL(kernel_for(s->variant), dim3(s->grid), dim3(256), s->lds_bytes, q, P);
         HIPCHK(hipGetLastError());
@@ -809,11 +826,23 @@ extern "C" mrt_status mrt_render_debug(mrt_scene* s, float* path_rgb, uint32_t* 
     return MRT_OK;
 }
 
+// work_queue::getPercentDone (work_queue.cpp:142-175): paths handed out over all paths of the
+// render.  Reads the per-launch counters on a non-blocking stream, so it can be called from
+// another host thread while the render runs.
 extern "C" mrt_status mrt_progress(mrt_scene* s, float* pct) {
     if (!s || !pct) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_progress: null");
-    uint64_t c = 0;
-    HIPCHK(hipMemcpy(&c, s->d_counter, 8, hipMemcpyDeviceToHost));
-    *pct = s->last_paths ? std::min(100.0f, (float)(c * 100.0 / (double)s->last_paths)) : 0.0f;
+    *pct = 0.0f;
+    const size_t n = s->n_chunks;
+    if (n == 0 || !s->pstream || hipEventQuery(s->ev_reset) != hipSuccess) return MRT_OK;  // not started
+    std::vector<uint64_t> c(n);
+    HIPCHK(hipMemcpyAsync(c.data(), s->d_counters, n * 8, hipMemcpyDeviceToHost, s->pstream));
+    HIPCHK(hipStreamSynchronize(s->pstream));
+    double done = 0, total = 0;
+    for (size_t k = 0; k < n; k++) {
+        done += (double)std::min<uint64_t>(c[k], s->chunk_paths[k]);
+        total += (double)s->chunk_paths[k];
+    }
+    *pct = total > 0 ? (float)std::min(100.0, done * 100.0 / total) : 0.0f;
     return MRT_OK;
 }
 

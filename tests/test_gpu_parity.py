@@ -220,3 +220,27 @@ def test_device_tonemap_of_rendered_image(gpu):
     got = np.zeros(h * w, dtype=np.uint32)
     got[px] = argb.cpu().numpy().view(np.uint32)
     assert np.array_equal(got, want)
+
+
+def test_progress_while_rendering(gpu):
+    """mrt_progress (work_queue::getPercentDone) is readable from another host thread during a
+    render: once the render has started it never decreases, passes through intermediate values
+    and ends at 100 (until the new render resets it, it reports the previous one)."""
+    import threading
+    w, h, spp = 500, 500, 1024
+    sc, r = renderer(gpu, 5, w, h)
+    d = gpu.render_desc(w, h, spp, chunk_samples=256)
+    r.prepare(d)
+    seen = []
+    t = threading.Thread(target=lambda: r.render(d))
+    t.start()
+    while t.is_alive():
+        seen.append(r.progress())
+    t.join()
+    seen.append(r.progress())
+    started = max(i for i, v in enumerate(seen) if v == 0.0)  # the new render resets progress to 0
+    run = seen[started:]
+    drops = [(i, a, b) for i, (a, b) in enumerate(zip(run, run[1:])) if b < a]
+    assert not drops, (drops[:5], len(run), sorted(set(round(v, 1) for v in run))[:20])
+    assert any(0.0 < v < 100.0 for v in run)
+    assert run[-1] == 100.0
