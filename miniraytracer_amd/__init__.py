@@ -111,11 +111,14 @@ class Renderer:
         check(lib().mrt_scene_upload(device, C.byref(scene.view), C.byref(self._h)), "mrt_scene_upload")
         self.scene = scene
 
-    def render(self, desc):
-        """Blocking render into a host float32 (H, W, 4) image (row 0 = bottom); returns (img, rays)."""
+    def render(self, desc, cancel=None):
+        """Blocking render into a host float32 (H, W, 4) image (row 0 = bottom); returns (img, rays).
+        cancel: optional ctypes.c_int; setting it non-zero from another thread stops the render
+        (G_isRunning, main.cpp:180/235) and raises MrtError (MRT_ERR_CANCELLED)."""
         img = np.zeros((desc.height, desc.width, 4), dtype=np.float32)
         rays = C.c_uint64()
-        check(lib().mrt_render(self._h, C.byref(desc), img.ctypes.data, C.byref(rays), None), "mrt_render")
+        check(lib().mrt_render(self._h, C.byref(desc), img.ctypes.data, C.byref(rays), C.byref(cancel) if cancel is not None else None),
+              "mrt_render")
         return img, rays.value
 
     def prepare(self, desc):

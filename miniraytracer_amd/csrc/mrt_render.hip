@@ -17,6 +17,7 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <unistd.h>
 
 #include "mrt_internal.h"
 #include "mrt_shade.h"
@@ -44,6 +45,7 @@ struct PathParams {
     float* __restrict__ rad;              // n_paths * 3 floats, [s - s0][lp]
     uint32_t* __restrict__ path_rays;     // optional (debug): n_paths
     unsigned long long* __restrict__ counter;  // work counter (paths handed out)
+    const int* cancel;                    // device flag: non-zero makes the launch exit (G_isRunning)
     unsigned long long* __restrict__ rays;
     float4* __restrict__ lev;             // fold levels, lane-major: [slot][lev_rows]
     uint32_t lev_rows;                    // levels per lane (max_bounces, at least 1)
@@ -97,6 +99,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
                            (float4*)(wmesh + (P.lds_mesh + P.lds_save) * 64) + lane};
     const uint64_t lt_mask = (1ull << lane) - 1ull;
 
+    // main.cpp:180/235 stop on !G_isRunning: a launch of a cancelled render does no work (mrt_render
+    // splits a cancellable render into several launches)
+    if (__hip_atomic_load(P.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return;
     bool active = false;
     uint32_t idx = 0;
     PathState ps;
@@ -743,6 +748,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
     const uint32_t launches = (ns + s->chunk - 1) / s->chunk;
     s->n_chunks = 0;
     HIPCHK(hipMemsetAsync(s->d_counters, 0, (size_t)launches * 8, q));
+    HIPCHK(hipMemsetAsync(s->d_counter + 4, 0, 8, q));  // cancel flag
     HIPCHK(hipEventRecord(s->ev_reset, q));
     for (uint32_t k = 0; k < launches; k++) s->chunk_paths[k] = (uint64_t)s->npix * (std::min(ns, (k + 1) * s->chunk) - k * s->chunk);
     s->n_chunks = launches;
@@ -770,6 +776,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.rad = s->d_rad;
         P.path_rays = (d->flags & MRT_RF_PATH_DEBUG) ? s->d_path_rays : nullptr;
         P.counter = (unsigned long long*)(s->d_counters + s->n_launch);
+        P.cancel = (const int*)(s->d_counter + 4);
         P.rays = d_rays ? (unsigned long long*)d_rays : s->d_rays;
         P.lev = s->d_lev;
         P.lev_rows = s->lev_rows;
@@ -793,17 +800,36 @@ extern "C" mrt_status mrt_render(mrt_scene* s, const mrt_render_desc* d, float* 
     if (!s || !d || !rgb_out) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_render: null");
     mrt_status st = mrt_prepare(s, d);
     if (st) return st;
+    if (cancel && *cancel) return mrt_internal_fail(MRT_ERR_CANCELLED, "cancelled");
+    mrt_render_desc dc = *d;  // a cancellable render runs as >= 16 launches; cancel lands between them
+    const uint32_t ns = d->sqrt_samples * d->sqrt_samples;
+    if (cancel && dc.chunk_samples == 0 && !(dc.flags & MRT_RF_PATH_DEBUG)) dc.chunk_samples = std::max(1u, ns / 16);
+    d = &dc;
+    if ((st = mrt_prepare(s, d))) return st;
     float* d_out = nullptr;
     HIPCHK(hipMalloc(&d_out, (size_t)s->npix * 16 + 16));
     HIPCHK(hipMemset(s->d_rays, 0, 8));
-    if (cancel && *cancel) {
-        (void)hipFree(d_out);
-        return mrt_internal_fail(MRT_ERR_CANCELLED, "cancelled");
-    }
     st = mrt_render_device(s, d, d_out, (uint64_t*)s->d_rays, nullptr);
     if (st) {
         (void)hipFree(d_out);
         return st;
+    }
+    // wait, forwarding the caller's cancel flag to the device flag the path kernel polls
+    bool cancelled = false;
+    for (;;) {
+        const hipError_t q = hipStreamQuery(nullptr);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) {
+            (void)hipFree(d_out);
+            return mrt_internal_fail(MRT_ERR_HIP, hipGetErrorString(q));
+        }
+        if (cancel && *cancel && !cancelled) {
+            static const int one = 1;
+            HIPCHK(hipMemcpyAsync(s->d_counter + 4, &one, sizeof(int), hipMemcpyHostToDevice, s->pstream));
+            HIPCHK(hipStreamSynchronize(s->pstream));
+            cancelled = true;
+        }
+        usleep(200);
     }
     std::vector<float> local((size_t)s->npix * 4);
     std::vector<uint32_t> px = mrt_internal_local_pixels(d);
@@ -814,6 +840,7 @@ extern "C" mrt_status mrt_render(mrt_scene* s, const mrt_render_desc* d, float* 
     uint64_t rays = 0;
     HIPCHK(hipMemcpy(&rays, s->d_rays, 8, hipMemcpyDeviceToHost));
     if (rays_out) *rays_out = rays;
+    if (cancelled) return mrt_internal_fail(MRT_ERR_CANCELLED, "cancelled (partial image)");
     return MRT_OK;
 }
 
