@@ -595,7 +595,36 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     UP(wide.data(), wide.size(), &S.mwide);
     UP((const float4*)v->tri_geo, (size_t)v->n_tris * 3, &S.tri_geo);
     UP((const float4*)v->tri_nrm, (size_t)v->n_tris * 3, &S.tri_nrm);
-    UP(v->materials, v->n_materials, &S.mats);
+    std::vector<DMat> dmats(v->n_materials);
+    for (uint32_t i = 0; i < v->n_materials; i++) {
+        const mrt_material& m = v->materials[i];
+        DMat& d = dmats[i];
+        d.kind = m.kind;
+        d.tex = m.tex;
+        d.p = m.p;
+        d.flags = 0;
+        if (m.tex < v->n_textures && v->textures[m.tex].kind == MRT_T_COLOR) {
+            d.flags = DMAT_COLOR;
+            for (int k = 0; k < 4; k++) d.col[k] = v->textures[m.tex].f[k];
+        }
+    }
+    UP(dmats.data(), dmats.size(), &S.mats);
+    // scene.biased_objects flattened: an object_list's children, or the object itself
+    std::vector<mrt_node> bleaf;
+    uint32_t blist = 0;
+    if (v->biased != MRT_NONE) {
+        const mrt_node& b = nodes[v->biased];
+        if ((b.kind & 0xFF) == MRT_K_LIST) {
+            blist = 1;
+            for (uint32_t i = 0; i < b.b; i++) bleaf.push_back(nodes[v->children[b.a + i]]);
+        } else {
+            bleaf.push_back(b);
+        }
+    }
+    if (bleaf.empty()) bleaf.push_back(mrt_node{});
+    UP(bleaf.data(), bleaf.size(), &S.bleaf);
+    S.nbleaf = blist ? nodes[v->biased].b : 1u;
+    S.blist = blist;
     UP(v->textures, v->n_textures, &S.texs);
     UP((const float4*)v->perlin_ranvec, 256, &S.ranvec);
     UP(v->perlin_perm, 768, &S.perm);

@@ -70,6 +70,13 @@ __device__ __forceinline__ f3 tex_sample(const DScene& S, uint32_t t, float u, f
     }
 }
 
+// the material's texture at the hit (constant colours come inline with the material)
+template <uint32_t F>
+__device__ __forceinline__ f3 mat_color(const DScene& S, const DMat& M, const HitRec& rec) {
+    if (!(F & FT_TEX) || (M.flags & DMAT_COLOR)) return f3{M.col[0], M.col[1], M.col[2]};
+    return tex_sample<F>(S, M.tex, rec.u, rec.v, rec.p);
+}
+
 // onb(n) * vec (onb.h:19-27)
 __device__ __forceinline__ f3 onb_apply(f3 w, f3 vec) {
     f3 a = fabsf(w.x) > 0.9f ? f3{0, 1, 0} : f3{1, 0, 0};
@@ -106,13 +113,32 @@ __device__ __forceinline__ float leaf_pdf_value(const DScene& S, const mrt_node&
     }
     return 0;
 }
+// a node record read through the constant address space (scalar loads at a uniform address)
+__device__ __forceinline__ mrt_node ld_node(const MRT_CONST_AS mrt_node* p) {
+    mrt_node n;
+    n.kind = p->kind;
+    n.a = p->a;
+    n.b = p->b;
+    n.mat = p->mat;
+    for (int k = 0; k < 12; k++) n.f[k] = p->f[k];
+    return n;
+}
+
+// object_list::pdf_value over the biased list (scene_object.h:64-70): the leaves are read through
+// the constant address space (uniform index: scalar loads, no node -> children -> node chain)
 template <uint32_t F>
-__device__ __forceinline__ float biased_pdf_value(const DScene& S, uint32_t node, f3 origin, f3 dir, float time) {
-    const mrt_node& n = S.nodes[node];
-    if (MRT_NODE_KIND(n) != MRT_K_LIST) return leaf_pdf_value<F>(S, n, origin, dir, time);
+__device__ __forceinline__ float biased_pdf_value(const DScene& S, f3 origin, f3 dir, float time) {
+    const MRT_CONST_AS mrt_node* bl = const_ptr(S.bleaf);
+    if (!S.blist) {
+        const mrt_node n = ld_node(bl);
+        return leaf_pdf_value<F>(S, n, origin, dir, time);
+    }
     float sum = 0;
-    for (uint32_t i = 0; i < n.b; i++) sum += leaf_pdf_value<F>(S, S.nodes[S.children[n.a + i]], origin, dir, time);
-    return sum / (float)n.b;
+    for (uint32_t i = 0; i < S.nbleaf; i++) {
+        const mrt_node n = ld_node(bl + i);
+        sum += leaf_pdf_value<F>(S, n, origin, dir, time);
+    }
+    return sum / (float)S.nbleaf;
 }
 template <uint32_t F>
 __device__ __forceinline__ f3 leaf_pdf_generate(const DScene& S, const mrt_node& n, f3 origin, float time, Pcg& rng) {
@@ -133,11 +159,17 @@ __device__ __forceinline__ f3 leaf_pdf_generate(const DScene& S, const mrt_node&
     return f3{1, 0, 0};
 }
 template <uint32_t F>
-__device__ __forceinline__ f3 biased_pdf_generate(const DScene& S, uint32_t node, f3 origin, float time, Pcg& rng) {
-    const mrt_node& n = S.nodes[node];
-    if (MRT_NODE_KIND(n) != MRT_K_LIST) return leaf_pdf_generate<F>(S, n, origin, time, rng);
-    int i = int(randf(rng) * (float)n.b);
-    return leaf_pdf_generate<F>(S, S.nodes[S.children[n.a + i]], origin, time, rng);
+__device__ __forceinline__ f3 biased_pdf_generate(const DScene& S, f3 origin, float time, Pcg& rng) {
+    if (!S.blist) {
+        const mrt_node n = ld_node(const_ptr(S.bleaf));
+        return leaf_pdf_generate<F>(S, n, origin, time, rng);
+    }
+    const int i = int(randf(rng) * (float)S.nbleaf);  // object_list::pdf_generate (scene_object.h:72-77)
+    if (S.nbleaf == 1) {
+        const mrt_node n = ld_node(const_ptr(S.bleaf));
+        return leaf_pdf_generate<F>(S, n, origin, time, rng);
+    }
+    return leaf_pdf_generate<F>(S, S.bleaf[i], origin, time, rng);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -209,9 +241,9 @@ __device__ __forceinline__ bool trace_segment(const DScene& S, PathState& ps, ui
         }
         return true;
     }
-    const mrt_material M = S.mats[rec.mat];
+    const DMat M = S.mats[rec.mat];
     if (M.kind == MRT_M_LIGHT) {  // diffuse_light: sampleEmissive, never scatters (material.h:190-199)
-        *L = dot(rec.n, r.d) < 0.0f ? fmul(M.p, tex_sample<F>(S, M.tex, rec.u, rec.v, rec.p)) : f3{0, 0, 0};
+        *L = dot(rec.n, r.d) < 0.0f ? fmul(M.p, mat_color<F>(S, M, rec)) : f3{0, 0, 0};
         return true;
     }
     if (ps.depth >= max_bounces) {  // the emitted term of a non-emissive material
@@ -223,7 +255,7 @@ __device__ __forceinline__ bool trace_segment(const DScene& S, PathState& ps, ui
         f3 reflected = sub(r.d, fmul(2.0f * dot(r.d, rec.n), rec.n));
         f3 rs = random_in_sphere(ps.rng);
         f3 nd = add(reflected, fmul(1 - M.p, rs));
-        f3 att = tex_sample<F>(S, M.tex, rec.u, rec.v, rec.p);
+        f3 att = mat_color<F>(S, M, rec);
         const float4 lv = make_float4(att.x, att.y, att.z, -1.0f);
         lev.put(ps.nlev & ~LEV_LOUD, lv);
         ps.nlev = (ps.nlev + 1) | (quiet_level(lv) ? 0u : LEV_LOUD);
@@ -268,11 +300,11 @@ __device__ __forceinline__ bool trace_segment(const DScene& S, PathState& ps, ui
     }
     // lambertian / isotropic (material.h:48-74) with mix_pdf against the biased list (main.cpp:84-102)
     const bool lamb = !(F & FT_ISO) || M.kind == MRT_M_LAMBERTIAN;
-    const f3 att = tex_sample<F>(S, M.tex, rec.u, rec.v, rec.p);
+    const f3 att = mat_color<F>(S, M, rec);
     f3 gen;
     bool surface = true;
     if (S.biased != MRT_NONE && randf(ps.rng) < 0.5f) {
-        gen = biased_pdf_generate<F>(S, S.biased, rec.p, r.time, ps.rng);
+        gen = biased_pdf_generate<F>(S, rec.p, r.time, ps.rng);
         surface = false;
     }
     if (surface) gen = lamb ? onb_apply(rec.n, random_cosine_direction(ps.rng)) : random_in_sphere(ps.rng);
@@ -286,7 +318,7 @@ __device__ __forceinline__ bool trace_segment(const DScene& S, PathState& ps, ui
         sval = 1 / (2 * PI_F);
         spdf = 1.0f / (2.0f * PI_F);
     }
-    const float pdf_v = S.biased != MRT_NONE ? 0.5f * (biased_pdf_value<F>(S, S.biased, rec.p, sc.d, r.time) + sval) : sval;
+    const float pdf_v = S.biased != MRT_NONE ? 0.5f * (biased_pdf_value<F>(S, rec.p, sc.d, r.time) + sval) : sval;
     const float4 lv = make_float4(att.x * spdf, att.y * spdf, att.z * spdf, pdf_v);
     lev.put(ps.nlev & ~LEV_LOUD, lv);
     ps.nlev = (ps.nlev + 1) | (quiet_level(lv) ? 0u : LEV_LOUD);

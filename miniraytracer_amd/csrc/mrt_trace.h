@@ -22,6 +22,16 @@ struct MeshWide {
 };
 #define MESH_LEAF 0x80000000u
 
+// device material: mrt_material plus, when its texture is a constant colour, that colour inline
+// (one load per shading instead of material -> texture)
+struct DMat {
+    uint32_t kind, tex;
+    float p;
+    uint32_t flags;  // DMAT_COLOR: col holds the texture's colour
+    float col[4];
+};
+#define DMAT_COLOR 0x1u
+
 // Device-side scene: the mrt_scene_view arrays resident in HBM.
 struct DScene {
     const mrt_node* __restrict__ nodes;
@@ -30,12 +40,14 @@ struct DScene {
     const MeshWide* __restrict__ mwide;
     const float4* __restrict__ tri_geo;
     const float4* __restrict__ tri_nrm;
-    const mrt_material* __restrict__ mats;
+    const DMat* __restrict__ mats;
     const mrt_texture* __restrict__ texs;
     const float4* __restrict__ ranvec;
     const int32_t* __restrict__ perm;
     const uint8_t* __restrict__ texels;
     const LinOp* __restrict__ prog;  // linear hit program (FT_LIN kernels), mrt_lin.h
+    const mrt_node* __restrict__ bleaf;  // leaves of scene.biased_objects (the list's children, or the object)
+    uint32_t nbleaf, blist;              // leaf count; 1 if biased_objects is an object_list
     uint32_t root, biased, sky;
     mrt_camera cam;
 };
