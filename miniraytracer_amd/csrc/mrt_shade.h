@@ -91,15 +91,15 @@ template <uint32_t F>
 __device__ __forceinline__ float leaf_pdf_value(const DScene& S, const mrt_node& n, f3 origin, f3 dir, float time) {
     uint32_t k = MRT_NODE_KIND(n);
     HitRec rec;
-    if (k == MRT_K_XZ) {
-        Ray r = make_ray(origin, dir, 0.0f, 0);
-        if (rect_hit<F, 1>(n, r, 0.001f, FLT_MAX_, rec, true)) {
-            float area = (n.f[1] - n.f[0]) * (n.f[3] - n.f[2]);
-            float dist_sq = rec.t * rec.t;
-            float cosine = fabsf(dot(dir, rec.n));
-            return dist_sq / (cosine * area);
-        }
-        return 0;
+    if (k == MRT_K_XZ) {  // xz_rect::pdf_value (rect.cpp:92-102), the hit test branch-free
+        const Ray r = make_ray(origin, dir, 0.0f, 0);
+        float t;
+        const bool h = lin_prim_t<F, MRT_K_XZ>(n, r, 0.001f, FLT_MAX_, &t);
+        const float area = (n.f[1] - n.f[0]) * (n.f[3] - n.f[2]);
+        const float dist_sq = t * t;
+        const float cosine = fabsf(dot(dir, f3{0, n.f[5], 0}));
+        const float pdf = dist_sq / (cosine * area);
+        return h ? pdf : 0.0f;
     }
     if ((F & FT_BSPHERE) && k == MRT_K_SPHERE) {
         Ray r = make_ray(origin, dir, time, 0);
