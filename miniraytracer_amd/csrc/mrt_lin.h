@@ -23,6 +23,7 @@ enum : uint32_t {
     LOP_LIST_END = 4,
     LOP_INST = 5,      // translate / rotate_y / fused translate(rotate_y) enter, skip = its LOP_INST_END
     LOP_INST_END = 6,
+    LOP_BVHW = 7,      // bvh_node subtree as wide nodes (per-lane traversal, bvhw_hit)
 };
 
 // one op = the node's own record (no second load): code = op | kind << 8 | flags << 16
@@ -191,6 +192,13 @@ __device__ __forceinline__ bool scene_hit_lin(const DScene& S, Ray& r, float tmi
             hdone = h ? false : hdone;
         } else if ((F & FT_MESH) && op == LOP_MESH) {
             if (on && mesh_hit(S, S.nodes[o.node], cur, tmin, closest, rec, true, L)) {
+                closest = rec.t;
+                hnode = o.node;
+                hinst = inst;
+                hdone = true;
+            }
+        } else if ((F & FT_BVHW) && op == LOP_BVHW) {
+            if (on && bvhw_hit<F>(S, S.nodes[o.node], cur, tmin, closest, rec, true, L)) {
                 closest = rec.t;
                 hnode = o.node;
                 hinst = inst;

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <functional>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -389,6 +390,7 @@ struct GraphCheck {
     const std::vector<mrt_node>& nodes;
     const mrt_scene_view* v;
     int max_frames = 0, max_rays = 0, max_mesh = 0;
+    int bvhw_depth = 0;  // deepest wide-node stack of the converted bvh_node subtrees
     bool ok = true;
     std::string why;
     int mesh_depth(uint32_t ni, int guard) {
@@ -405,6 +407,10 @@ struct GraphCheck {
         if (k == MRT_K_SPHERE || k == MRT_K_XY || k == MRT_K_XZ || k == MRT_K_YZ) return;
         if (k == MRT_K_MESH) {
             max_mesh = std::max(max_mesh, mesh_depth(n.a, 0));
+            return;
+        }
+        if (k == MRT_K_BVHW) {
+            max_mesh = std::max(max_mesh, bvhw_depth);
             return;
         }
         frames++;
@@ -459,6 +465,9 @@ struct LinCompiler {
         case MRT_K_MESH:
             prog.push_back(op_of(LOP_MESH, id));
             return true;
+        case MRT_K_BVHW:
+            prog.push_back(op_of(LOP_BVHW, id));
+            return true;
         case MRT_K_LIST: {
             size_t at = prog.size();
             prog.push_back(op_of(LOP_LIST, id));
@@ -488,6 +497,7 @@ static uint32_t scene_features(const mrt_scene_view* v, const std::vector<mrt_no
     for (const mrt_node& n : nodes) {
         switch (n.kind & 0xFF) {
         case MRT_K_BVH: f |= FT_BVH; break;
+        case MRT_K_BVHW: f |= FT_BVHW; break;
         case MRT_K_MESH: f |= FT_MESH; break;
         case MRT_K_VOLUME: f |= FT_VOLUME; break;
         case MRT_K_TRANSLATE: case MRT_K_ROTY: case MRT_K_TRROTY: f |= FT_INST; break;
@@ -572,7 +582,80 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
             if ((n.kind & 0xFF) == MRT_K_MESH) n.b = ref_of(n.a);
         if (!ok) return mrt_internal_fail(MRT_ERR_INVALID, "mesh BVH outside the device encoding (leaf > 127 triangles or > 2^24 triangles)");
     }
+    // bvh_node subtrees whose leaves are primitives / object_lists of primitives (and of boxes of
+    // primitives) -> wide nodes; the subtree root becomes an MRT_K_BVHW node (a = root ref)
+    std::vector<BvhWide> bwide;
+    int bvhw_depth = 0;
+    {
+        const size_t nn = nodes.size();
+        auto kind_of = [&](uint32_t i) { return nodes[i].kind & 0xFFu; };
+        auto is_leaf_prim = [&](uint32_t i) {
+            const uint32_t k = kind_of(i);
+            return k == MRT_K_SPHERE || k == MRT_K_XY || k == MRT_K_XZ || k == MRT_K_YZ;
+        };
+        auto leaf_ok = [&](uint32_t i) {
+            if (is_leaf_prim(i)) return true;
+            if (kind_of(i) != MRT_K_LIST) return false;
+            const mrt_node& l = nodes[i];
+            for (uint32_t c = 0; c < l.b; c++) {
+                const uint32_t ci = v->children[l.a + c];
+                if (ci >= nn) return false;
+                if (is_leaf_prim(ci)) continue;
+                if (kind_of(ci) != MRT_K_LIST) return false;
+                const mrt_node& g = nodes[ci];
+                for (uint32_t j = 0; j < g.b; j++) {
+                    const uint32_t gi = v->children[g.a + j];
+                    if (gi >= nn || !is_leaf_prim(gi)) return false;
+                }
+            }
+            return true;
+        };
+        std::vector<uint8_t> under_bvh(nn, 0);
+        for (size_t i = 0; i < nn; i++)
+            if (kind_of((uint32_t)i) == MRT_K_BVH) {
+                if (nodes[i].a < nn) under_bvh[nodes[i].a] = 1;
+                if (nodes[i].b < nn) under_bvh[nodes[i].b] = 1;
+            }
+        // does the subtree at i qualify (bvh_node inner nodes, qualifying leaves)?
+        std::function<bool(uint32_t, int)> ok = [&](uint32_t i, int guard) -> bool {
+            if (i >= nn || guard > 64) return false;
+            if (kind_of(i) != MRT_K_BVH) return leaf_ok(i);
+            return ok(nodes[i].a, guard + 1) && ok(nodes[i].b, guard + 1);
+        };
+        std::function<uint32_t(uint32_t, int)> build = [&](uint32_t i, int depth) -> uint32_t {
+            bvhw_depth = std::max(bvhw_depth, depth);
+            if (kind_of(i) != MRT_K_BVH) return BVHW_LEAF | i;
+            const uint32_t w = (uint32_t)bwide.size();
+            bwide.push_back(BvhWide{});
+            const mrt_node& b = nodes[i];
+            const uint32_t lc = b.a, rc = b.b;
+            const uint32_t lref = build(lc, depth + 1), rref = build(rc, depth + 1);
+            BvhWide& W = bwide[w];
+            W.lref = lref;
+            W.rref = rref;
+            W.order = (b.kind >> 8) & 0xFFu;
+            W.flags = 0;
+            const mrt_node &L = nodes[lc], &R = nodes[rc];
+            auto has_box = [&](const mrt_node& c) {
+                const uint32_t k = c.kind & 0xFFu;
+                return k == MRT_K_BVH || (k == MRT_K_LIST && ((c.kind >> 16) & MRT_F_HASBOX));
+            };
+            if (has_box(L)) { W.flags |= 1u; for (int k = 0; k < 3; k++) { W.lmin[k] = L.f[k]; W.lmax[k] = L.f[3 + k]; } }
+            if (has_box(R)) { W.flags |= 2u; for (int k = 0; k < 3; k++) { W.rmin[k] = R.f[k]; W.rmax[k] = R.f[3 + k]; } }
+            return w;
+        };
+        const char* no_bvhw = getenv("MRT_NO_BVHW");  // test hook: keep the generic bvh_node walk
+        if (!(no_bvhw && *no_bvhw && *no_bvhw != '0'))
+            for (size_t i = 0; i < nn; i++)
+                if (kind_of((uint32_t)i) == MRT_K_BVH && !under_bvh[i] && ok((uint32_t)i, 0) && bwide.size() < BVHW_LEAF / 2) {
+                    const uint32_t root = build((uint32_t)i, 1);
+                    mrt_node& r = nodes[i];
+                    r.kind = (r.kind & ~0xFFu) | MRT_K_BVHW;
+                    r.a = root;
+                }
+    }
     GraphCheck gc{nodes, v};
+    gc.bvhw_depth = bvhw_depth;
     gc.walk(v->root, 0, 0, false, 0);
     if (!gc.ok) return mrt_internal_fail(MRT_ERR_INVALID, gc.why.c_str());
     if (v->biased != MRT_NONE) {
@@ -593,6 +676,7 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     UP(v->children, v->n_children, &S.children);
     UP(v->mesh_nodes, v->n_mesh_nodes, &S.mnodes);
     UP(wide.data(), wide.size(), &S.mwide);
+    UP(bwide.data(), bwide.size(), &S.bwide);
     UP((const float4*)v->tri_geo, (size_t)v->n_tris * 3, &S.tri_geo);
     UP((const float4*)v->tri_nrm, (size_t)v->n_tris * 3, &S.tri_nrm);
     std::vector<DMat> dmats(v->n_materials);

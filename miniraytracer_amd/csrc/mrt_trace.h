@@ -32,12 +32,29 @@ struct DMat {
 };
 #define DMAT_COLOR 0x1u
 
+// bvh_node (scene_object.h:138-244) subtree as wide nodes: both children's boxes inline.  flags:
+// bit 0 / 1 = the left / right child has a box (bvh_node, object_list with hasBox); primitives
+// are hit() directly.  Child ref: inner -> index into the wide array; leaf -> BVHW_LEAF | node
+// index of the primitive or object_list.
+struct BvhWide {
+    float lmin[3];
+    uint32_t lref;
+    float lmax[3];
+    uint32_t rref;
+    float rmin[3];
+    uint32_t order;
+    float rmax[3];
+    uint32_t flags;
+};
+#define BVHW_LEAF 0x80000000u
+
 // Device-side scene: the mrt_scene_view arrays resident in HBM.
 struct DScene {
     const mrt_node* __restrict__ nodes;
     const uint32_t* __restrict__ children;
     const mrt_mesh_node* __restrict__ mnodes;
     const MeshWide* __restrict__ mwide;
+    const BvhWide* __restrict__ bwide;
     const float4* __restrict__ tri_geo;
     const float4* __restrict__ tri_nrm;
     const DMat* __restrict__ mats;
@@ -57,6 +74,7 @@ struct DScene {
 #define MRT_NODE_FLAGS(n) (((n).kind >> 16) & 0xFFu)
 #define MRT_F_NEEDUV 0x4u   /* set on upload when the node's material samples uv */
 #define MRT_K_TRROTY 11u    /* upload fuses translate(rotate_y(x)) into one instance node */
+#define MRT_K_BVHW 12u      /* upload: a bvh_node subtree over primitives / object_lists as wide nodes */
 
 // Scene features; kernels are instantiated for feature subsets so that Cornell-like scenes run
 // without the code (and registers) of BVH/mesh/volume/texture paths they never take.
@@ -72,8 +90,9 @@ enum : uint32_t {
     FT_SKY = 1u << 8,
     FT_BSPHERE = 1u << 9,  // sphere in the biased (light-sampling) list
     FT_UV = 1u << 10,      // uv sampled on spheres / rects
-    FT_ALL = (1u << 11) - 1,
     FT_LIN = 1u << 11,     // scene graph compiled to a linear hit program (mrt_lin.h)
+    FT_BVHW = 1u << 12,    // bvh_node subtrees as wide nodes (MRT_K_BVHW)
+    FT_ALL = ((1u << 13) - 1) & ~FT_LIN,
 };
 
 // Per-wave LDS stacks, lane-interleaved ([slot][word][lane]) so every access is conflict-free.
@@ -87,7 +106,8 @@ struct LStack {
 
 template <uint32_t F>
 __device__ __forceinline__ bool is_prim(uint32_t kind) {
-    return kind == MRT_K_SPHERE || kind == MRT_K_XY || kind == MRT_K_XZ || kind == MRT_K_YZ || ((F & FT_MESH) && kind == MRT_K_MESH);
+    return kind == MRT_K_SPHERE || kind == MRT_K_XY || kind == MRT_K_XZ || kind == MRT_K_YZ || ((F & FT_MESH) && kind == MRT_K_MESH) ||
+           ((F & FT_BVHW) && kind == MRT_K_BVHW);
 }
 
 // get_sphere_uv (sphere.cpp:6-11)
@@ -260,6 +280,81 @@ __device__ __forceinline__ bool mesh_hit(const DScene& S, const mrt_node& n, con
 }
 
 template <uint32_t F>
+__device__ __forceinline__ bool leaf_prim_hit(const mrt_node& n, uint32_t kind, const Ray& r, float tmin, float tmax, HitRec& rec, bool full) {
+    switch (kind) {
+    case MRT_K_SPHERE: return sphere_hit<F>(n, r, tmin, tmax, rec, full);
+    case MRT_K_XY: return rect_hit<F, 2>(n, r, tmin, tmax, rec, full);
+    case MRT_K_XZ: return rect_hit<F, 1>(n, r, tmin, tmax, rec, full);
+    default: return rect_hit<F, 0>(n, r, tmin, tmax, rec, full);
+    }
+}
+
+// a bvh_node leaf: a primitive, or an object_list (its box already tested by the parent) of
+// primitives and object_lists of primitives (box, box.h:6-30) -- object_list::hit semantics,
+// the running closest narrowing across children (scene_object.h:79-103)
+template <uint32_t F>
+__device__ __forceinline__ bool bvhw_leaf(const DScene& S, uint32_t node, const Ray& r, float tmin, float tmax, HitRec& rec, bool full) {
+    const mrt_node& n = S.nodes[node];
+    const uint32_t k = MRT_NODE_KIND(n);
+    if (k != MRT_K_LIST) return leaf_prim_hit<F>(n, k, r, tmin, tmax, rec, full);
+    float closest = tmax;
+    bool hit = false;
+    for (uint32_t i = 0; i < n.b; i++) {
+        const mrt_node& c = S.nodes[S.children[n.a + i]];
+        const uint32_t ck = MRT_NODE_KIND(c);
+        if (ck == MRT_K_LIST) {
+            if ((MRT_NODE_FLAGS(c) & MRT_F_HASBOX) && !aabb_hit(c.f, c.f + 3, r, tmin, closest)) continue;
+            for (uint32_t j = 0; j < c.b; j++) {
+                const mrt_node& g = S.nodes[S.children[c.a + j]];
+                if (leaf_prim_hit<F>(g, MRT_NODE_KIND(g), r, tmin, closest, rec, full)) {
+                    hit = true;
+                    closest = rec.t;
+                }
+            }
+        } else if (leaf_prim_hit<F>(c, ck, r, tmin, closest, rec, full)) {
+            hit = true;
+            closest = rec.t;
+        }
+    }
+    return hit;
+}
+
+// bvh_node::hit (scene_object.h:208-244) over wide nodes: the root's own box, then depth-first,
+// closer child first (node_order & dirMask), the first child subtree that hits ends the walk.
+// A child's box is tested at its parent with the (tmin, tmax) the reference uses when it visits
+// it; only a farther child whose box was hit is pushed (short stack in LDS, shared with meshes).
+// n.a = root ref, n.f[0..5] = the root bvh_node's box.
+template <uint32_t F>
+__device__ __forceinline__ bool bvhw_hit(const DScene& S, const mrt_node& n, const Ray& r, float tmin, float tmax, HitRec& rec, bool full,
+                                         const LStack& L) {
+    if (!aabb_hit(n.f, n.f + 3, r, tmin, tmax)) return false;
+    uint32_t ref = n.a, sp = 0;
+    for (;;) {
+        if (ref & BVHW_LEAF) {
+            if (bvhw_leaf<F>(S, ref & ~BVHW_LEAF, r, tmin, tmax, rec, full)) return true;
+        } else {
+            const BvhWide& W = S.bwide[ref];
+            const bool hl = !(W.flags & 1u) || aabb_hit(W.lmin, W.lmax, r, tmin, tmax);
+            const bool hr = !(W.flags & 2u) || aabb_hit(W.rmin, W.rmax, r, tmin, tmax);
+            const bool left_first = (W.order & r.mask) != 0;
+            const uint32_t cref = left_first ? W.lref : W.rref, fref = left_first ? W.rref : W.lref;
+            const bool hc = left_first ? hl : hr, hf = left_first ? hr : hl;
+            if (hc) {
+                if (hf && fref != cref) L.mesh[(sp++) * 64 + L.lane] = fref;  // n == 1: left == right, a repeat misses again
+                ref = cref;
+                continue;
+            }
+            if (hf) {
+                ref = fref;
+                continue;
+            }
+        }
+        if (sp == 0) return false;
+        ref = L.mesh[(--sp) * 64 + L.lane];
+    }
+}
+
+template <uint32_t F>
 __device__ __forceinline__ bool prim_hit(const DScene& S, const mrt_node& n, uint32_t kind, const Ray& r, float tmin, float tmax, HitRec& rec,
                                          bool full, const LStack& L) {
     switch (kind) {
@@ -268,6 +363,8 @@ __device__ __forceinline__ bool prim_hit(const DScene& S, const mrt_node& n, uin
     case MRT_K_XZ: return rect_hit<F, 1>(n, r, tmin, tmax, rec, full);
     case MRT_K_YZ: return rect_hit<F, 0>(n, r, tmin, tmax, rec, full);
     default:
+        if constexpr ((F & FT_BVHW) != 0)
+            if (kind == MRT_K_BVHW) return bvhw_hit<F>(S, n, r, tmin, tmax, rec, full, L);
         if constexpr ((F & FT_MESH) != 0) return mesh_hit(S, n, r, tmin, tmax, rec, full, L);
         return false;
     }

@@ -148,8 +148,9 @@ def test_linear_program_equals_generic_machine(gpu, sid, w, h, spp, monkeypatch)
 
 
 def test_kernel_selection(gpu):
-    """BVH / volume scenes fall back to the generic machine; the Cornell box runs a linear program."""
-    for sid, want_lin in [(0, False), (6, False), (7, False), (5, True), (9, True)]:
+    """Volume scenes fall back to the generic machine; the Cornell box, the meshes and the random
+    spheres (bvh_node converted to wide nodes) run a linear program."""
+    for sid, want_lin in [(0, True), (6, False), (7, False), (5, True), (9, True)]:
         sc = gpu.select_scene(sid, 1.0)
         info = gpu.Renderer(sc, 0).kernel_info()
         assert bool(info["kernel_features"] & gpu._lib.FT_LIN) == want_lin, (sid, info)
@@ -277,3 +278,24 @@ def test_cancel_stops_render(gpu):
     assert time.perf_counter() - t0 < 8 * t_full + 0.5
     again, rays_again = r.render(d)
     assert rays_again == rays_full and np.array_equal(again.view(np.uint32), full.view(np.uint32))
+
+
+@pytest.mark.parametrize("sid,w,h,spp", [(0, 60, 30, 9), (1, 60, 30, 9), (7, 40, 40, 4)])
+def test_wide_bvh_equals_generic_bvh_walk(gpu, sid, w, h, spp, monkeypatch):
+    """bvh_node subtrees converted to wide nodes (MRT_K_BVHW) give the same bits per path as the
+    generic machine's bvh_node walk (MRT_NO_BVHW=1 at upload)."""
+    sc = gpu.select_scene(sid, w / h)
+    fast = gpu.Renderer(sc, 0)
+    assert fast.kernel_info()["features"] & (1 << 12)
+    monkeypatch.setenv("MRT_NO_BVHW", "1")
+    slow = gpu.Renderer(sc, 0)
+    assert not slow.kernel_info()["features"] & (1 << 12)
+    d = gpu.render_desc(w, h, spp, depth=16, flags=gpu._lib.RF_PATH_DEBUG)
+    n = w * h * (int(spp ** 0.5) ** 2)
+    a, ra = fast.render(d)
+    pa = fast.paths(n)
+    b, rb = slow.render(d)
+    pb = slow.paths(n)
+    assert ra == rb
+    assert np.array_equal(pa[1], pb[1])
+    assert np.array_equal(pa[0].view(np.uint32), pb[0].view(np.uint32))
