@@ -61,7 +61,12 @@ struct PathParams {
 // Waves per SIMD the register allocator must reach (caps VGPRs at 512/W): the path loop is
 // latency-bound, so a few spilled registers cost less than the lost occupancy.  Tuned per
 // variant on MI355X (DESIGN.md "Occupancy").
-template <uint32_t F> struct PathOcc { static constexpr int W = (F & FT_LIN) ? 6 : 4; };
+// (compact variants -- Cornell, Cornell room + mesh, plain interpreter -- reach 80 VGPRs without
+// spills at 6; the wide-feature variants spill there and run best at 3 waves, 168 VGPRs)
+template <uint32_t F> struct PathOcc {
+    static constexpr bool kWide = (F & (FT_BVHW | FT_TEX | FT_VOLUME)) != 0 || !(F & FT_LIN);
+    static constexpr int W = kWide ? 3 : 6;
+};
 #ifndef MRT_BATCH
 #define MRT_BATCH 256u  // paths a wave claims per atomic on the work counter (one hot address)
 #endif
@@ -193,6 +198,7 @@ static constexpr uint32_t kVariants[] = {FT_LIN | FT_INST | MRT_SIG_BITS(SIG_COR
                                          FT_LIN | FT_MESH | FT_METAL | MRT_SIG_BITS(SIG_ROOM_MESH),
                                          FT_LIN | FT_INST,
                                          FT_LIN | FT_MESH | FT_METAL,
+                                         FT_LIN | FT_BVHW | FT_TEX | FT_METAL | FT_MOVING | FT_SKY | FT_UV,
                                          FT_LIN | FT_ALL,
                                          FT_ALL};
 static constexpr uint32_t kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
@@ -204,11 +210,13 @@ static path_kernel_t kernel_for(uint32_t v) {
     case 2: return mrt_path_kernel<kVariants[2]>;
     case 3: return mrt_path_kernel<kVariants[3]>;
     case 4: return mrt_path_kernel<kVariants[4]>;
-    default: return mrt_path_kernel<kVariants[5]>;
+    case 5: return mrt_path_kernel<kVariants[5]>;
+    default: return mrt_path_kernel<kVariants[6]>;
     }
 }
 static constexpr uint32_t kLevK[] = {PathLevLds<kVariants[0]>::K, PathLevLds<kVariants[1]>::K, PathLevLds<kVariants[2]>::K,
-                                     PathLevLds<kVariants[3]>::K, PathLevLds<kVariants[4]>::K, PathLevLds<kVariants[5]>::K};
+                                     PathLevLds<kVariants[3]>::K, PathLevLds<kVariants[4]>::K, PathLevLds<kVariants[5]>::K,
+                                     PathLevLds<kVariants[6]>::K};
 // first variant covering the scene's features: its own program shape first, then the interpreter
 static uint32_t pick_variant(uint32_t features) {
     const uint32_t feat = features & 0xFFFFu, sig = MRT_SIG_OF(features);
@@ -492,11 +500,12 @@ struct LinCompiler {
     }
 };
 
-static uint32_t scene_features(const mrt_scene_view* v, const std::vector<mrt_node>& nodes) {
+static uint32_t scene_features(const mrt_scene_view* v, const std::vector<mrt_node>& nodes, const std::vector<uint8_t>& absorbed) {
     uint32_t f = 0;
-    for (const mrt_node& n : nodes) {
+    for (size_t i = 0; i < nodes.size(); i++) {
+        const mrt_node& n = nodes[i];
         switch (n.kind & 0xFF) {
-        case MRT_K_BVH: f |= FT_BVH; break;
+        case MRT_K_BVH: if (!absorbed[i]) f |= FT_BVH; break;
         case MRT_K_BVHW: f |= FT_BVHW; break;
         case MRT_K_MESH: f |= FT_MESH; break;
         case MRT_K_VOLUME: f |= FT_VOLUME; break;
@@ -586,6 +595,7 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     // primitives) -> wide nodes; the subtree root becomes an MRT_K_BVHW node (a = root ref)
     std::vector<BvhWide> bwide;
     int bvhw_depth = 0;
+    std::vector<uint8_t> absorbed(nodes.size(), 0);  // bvh_nodes now inside a wide subtree
     {
         const size_t nn = nodes.size();
         auto kind_of = [&](uint32_t i) { return nodes[i].kind & 0xFFu; };
@@ -625,6 +635,7 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
         std::function<uint32_t(uint32_t, int)> build = [&](uint32_t i, int depth) -> uint32_t {
             bvhw_depth = std::max(bvhw_depth, depth);
             if (kind_of(i) != MRT_K_BVH) return BVHW_LEAF | i;
+            absorbed[i] = 1;
             const uint32_t w = (uint32_t)bwide.size();
             bwide.push_back(BvhWide{});
             const mrt_node& b = nodes[i];
@@ -734,7 +745,7 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     s->d_counter = (uint64_t*)p;
     s->d_rays = (unsigned long long*)((char*)p + 16);
     // kernel variant + LDS stacks sized from the scene graph (top frame lives in registers)
-    s->features = scene_features(v, nodes);
+    s->features = scene_features(v, nodes, absorbed);
     const char* no_sig = getenv("MRT_NO_SIG");  // test hook: run the interpreter on known shapes too
     if (lin) s->features |= FT_LIN;
     if (lin && !(no_sig && *no_sig && *no_sig != '0')) s->features |= MRT_SIG_BITS(lin_sig_of(lc.prog.data(), (uint32_t)lc.prog.size()));
