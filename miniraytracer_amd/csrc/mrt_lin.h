@@ -24,6 +24,8 @@ enum : uint32_t {
     LOP_INST = 5,      // translate / rotate_y / fused translate(rotate_y) enter, skip = its LOP_INST_END
     LOP_INST_END = 6,
     LOP_BVHW = 7,      // bvh_node subtree as wide nodes (per-lane traversal, bvhw_hit)
+    LOP_VOLUME = 8,    // constant_volume; the next op (LOP_VBOUND) is its primitive boundary
+    LOP_VBOUND = 9,
 };
 
 // one op = the node's own record (no second load): code = op | kind << 8 | flags << 16
@@ -159,7 +161,7 @@ __device__ __forceinline__ void lin_untransform(const OP& io, HitRec& rec) {
 // LDS per lane (L.save): [0..8] the query ray, [9..14] origin/direction of the instance ray of
 // the closest hit (written at the instance's END op when that hit lies inside it).
 template <uint32_t F>
-__device__ __forceinline__ bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, const LStack& L) {
+__device__ __forceinline__ bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, const LStack& L, Pcg& rng) {
     constexpr bool INST = (F & FT_INST) != 0;
     if (INST) lin_save_ray(L, r);
     Ray cur = r;
@@ -197,6 +199,45 @@ __device__ __forceinline__ bool scene_hit_lin(const DScene& S, Ray& r, float tmi
                 hinst = inst;
                 hdone = true;
             }
+        } else if ((F & FT_VOLUME) && op == LOP_VOLUME) {
+            // constant_volume::hit (volumes.cpp:5-35): two boundary queries, then a free-flight
+            // distance drawn from the path's RNG (inside hit(), in list order)
+            const MRT_CONST_AS LinOp& bo = prog[pc + 1];
+            float t1, t2;
+            bool h1, h2;
+            if (LOP_KIND(bo) == MRT_K_SPHERE) {
+                h1 = lin_prim_t<F, MRT_K_SPHERE>(bo, cur, -FLT_MAX_, FLT_MAX_, &t1);
+                h2 = lin_prim_t<F, MRT_K_SPHERE>(bo, cur, t1 + 0.0001f, FLT_MAX_, &t2);
+            } else if (LOP_KIND(bo) == MRT_K_XY) {
+                h1 = lin_prim_t<F, MRT_K_XY>(bo, cur, -FLT_MAX_, FLT_MAX_, &t1);
+                h2 = lin_prim_t<F, MRT_K_XY>(bo, cur, t1 + 0.0001f, FLT_MAX_, &t2);
+            } else if (LOP_KIND(bo) == MRT_K_XZ) {
+                h1 = lin_prim_t<F, MRT_K_XZ>(bo, cur, -FLT_MAX_, FLT_MAX_, &t1);
+                h2 = lin_prim_t<F, MRT_K_XZ>(bo, cur, t1 + 0.0001f, FLT_MAX_, &t2);
+            } else {
+                h1 = lin_prim_t<F, MRT_K_YZ>(bo, cur, -FLT_MAX_, FLT_MAX_, &t1);
+                h2 = lin_prim_t<F, MRT_K_YZ>(bo, cur, t1 + 0.0001f, FLT_MAX_, &t2);
+            }
+            if (on && h1 && h2) {
+                float a = t1 < tmin ? tmin : t1;
+                const float b = t2 > closest ? closest : t2;
+                if (a < b) {
+                    if (a < 0) a = 0;
+                    const float inside_dist = b - a;
+                    const float hit_dist = -(1 / o.f[0]) * log_(randf(rng));
+                    if (hit_dist < inside_dist) {
+                        closest = a + hit_dist;
+                        rec.t = closest;
+                        rec.p = eval(cur, closest);
+                        rec.n = f3{1, 0, 0};
+                        rec.mat = o.mat;
+                        hnode = o.node;
+                        hinst = inst;
+                        hdone = true;
+                    }
+                }
+            }
+            pc++;  // past the boundary op
         } else if ((F & FT_BVHW) && op == LOP_BVHW) {
             if (on && bvhw_hit<F>(S, S.nodes[o.node], cur, tmin, closest, rec, true, L)) {
                 closest = rec.t;

@@ -476,6 +476,14 @@ struct LinCompiler {
         case MRT_K_BVHW:
             prog.push_back(op_of(LOP_BVHW, id));
             return true;
+        case MRT_K_VOLUME: {  // a primitive boundary only (sphere / rect)
+            if (n.a >= nodes.size()) return false;
+            const uint32_t bk = nodes[n.a].kind & 0xFFu;
+            if (bk != MRT_K_SPHERE && bk != MRT_K_XY && bk != MRT_K_XZ && bk != MRT_K_YZ) return false;
+            prog.push_back(op_of(LOP_VOLUME, id));
+            prog.push_back(op_of(LOP_VBOUND, n.a));
+            return true;
+        }
         case MRT_K_LIST: {
             size_t at = prog.size();
             prog.push_back(op_of(LOP_LIST, id));

@@ -228,7 +228,7 @@ __device__ __forceinline__ bool trace_segment(const DScene& S, PathState& ps, ui
     Ray& r = ps.r;
     bool hit;
     if constexpr (MRT_SIG_OF(F) != SIG_NONE) hit = scene_hit_sig<F>(S, r, 0.001f, rec, Ls);
-    else if constexpr ((F & FT_LIN) != 0) hit = scene_hit_lin<F>(S, r, 0.001f, rec, Ls);
+    else if constexpr ((F & FT_LIN) != 0) hit = scene_hit_lin<F>(S, r, 0.001f, rec, Ls, ps.rng);
     else hit = scene_hit<F>(S, r, 0.001f, rec, ps.rng, Ls);
     PH_MARK(ph, 1);
     if (!hit) {

@@ -125,7 +125,7 @@ def test_full_size_cornell_properties(gpu, orc):
 
 
 @pytest.mark.parametrize("sid,w,h,spp", [(5, 64, 64, 16), (9, 40, 40, 9), (8, 40, 40, 9), (2, 48, 24, 9),
-                                         (3, 48, 24, 9), (4, 48, 24, 9)])
+                                         (3, 48, 24, 9), (4, 48, 24, 9), (0, 48, 24, 9), (7, 40, 40, 4)])
 def test_linear_program_equals_generic_machine(gpu, sid, w, h, spp, monkeypatch):
     """Scenes without bvh_node/constant_volume run the linear hit program (mrt_lin.h); the generic
     explicit-stack machine (MRT_FORCE_GENERIC=1 at upload) must give the same bits per path."""
@@ -148,9 +148,10 @@ def test_linear_program_equals_generic_machine(gpu, sid, w, h, spp, monkeypatch)
 
 
 def test_kernel_selection(gpu):
-    """Volume scenes fall back to the generic machine; the Cornell box, the meshes and the random
-    spheres (bvh_node converted to wide nodes) run a linear program."""
-    for sid, want_lin in [(0, True), (6, False), (7, False), (5, True), (9, True)]:
+    """Volumes bounded by instances (scene 6) fall back to the generic machine; the Cornell box,
+    the meshes, the random spheres and book2 (bvh_nodes as wide nodes, sphere-bounded volumes) run
+    a linear program."""
+    for sid, want_lin in [(0, True), (6, False), (7, True), (5, True), (9, True)]:
         sc = gpu.select_scene(sid, 1.0)
         info = gpu.Renderer(sc, 0).kernel_info()
         assert bool(info["kernel_features"] & gpu._lib.FT_LIN) == want_lin, (sid, info)
