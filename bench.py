@@ -45,6 +45,10 @@ def parse():
                     help="work_queue tile edge; also the multi-GPU partition grain (tile k -> rank k %% N)")
     ap.add_argument("--cpu-spp", type=int, default=256, help="spp of the bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--emulate-world", type=int, default=1,
+                    help="single-GPU rehearsal: render only rank --emulate-rank's share of an N-rank job "
+                         "(no collectives); used to predict per-rank step time at N GPUs")
+    ap.add_argument("--emulate-rank", type=int, default=0)
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_cornell_c2.json"))
     return ap.parse_args()
 
@@ -91,7 +95,10 @@ def main():
     # scene build + upload + workspace: outside the timed region (main.cpp:309 precedes 375)
     scene = m.select_scene(args.scene, args.width / args.height)
     rnd = m.Renderer(scene, device=local)
-    desc = m.render_desc(args.width, args.height, args.samples, depth=args.depth, tile_size=args.tile_size, rank=rank, world=world)
+    d_rank, d_world = rank, world
+    if world == 1 and args.emulate_world > 1:
+        d_rank, d_world = args.emulate_rank, args.emulate_world
+    desc = m.render_desc(args.width, args.height, args.samples, depth=args.depth, tile_size=args.tile_size, rank=d_rank, world=d_world)
     rnd.prepare(desc)
     px = m.local_pixels(desc)
     n_local = len(px)
@@ -187,6 +194,7 @@ def main():
                        "scene": args.scene, "width": args.width, "height": args.height,
                        "spp": desc.sqrt_samples ** 2, "depth": args.depth, "parallelism": f"tiles{world}",
                        "tile_size": args.tile_size,
+                       **({"emulated_share": f"rank {d_rank} of {d_world}"} if d_world != world else {}),
                        "rays_per_step": nrays // args.steps},
             "roofline": roofline,
             "cpu_baseline": None,
