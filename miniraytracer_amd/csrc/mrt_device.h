@@ -28,6 +28,11 @@ struct f3 {
     float x, y, z;
 };
 __device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+// Correctly rounded f32 square root.  (RN32(v_sqrt_f64(x)) is NOT: v_sqrt_f64 is approximate and
+// misrounds 3.9% of f32 inputs, tools/numcheck/divsqrt_check.hip.)
+__device__ __forceinline__ float sqrt_(float x) {
+    return __builtin_sqrtf(x);
+}
 __device__ __forceinline__ f3 add(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
 __device__ __forceinline__ f3 sub(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
 __device__ __forceinline__ f3 mul(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
@@ -36,7 +41,53 @@ __device__ __forceinline__ f3 fmul(float f, f3 a) { return f3{f * a.x, f * a.y, 
 __device__ __forceinline__ f3 divf(f3 a, float f) { return f3{a.x / f, a.y / f, a.z / f}; }
 __device__ __forceinline__ float dot(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 __device__ __forceinline__ float sdot(f3 a) { return (a.x * a.x + a.y * a.y) + a.z * a.z; }
-__device__ __forceinline__ f3 normalize(f3 a) { return divf(a, __builtin_sqrtf(sdot(a))); }
+// ---- exact f32 division on a short path (tools/numcheck/markstein_check.hip) ----------------------
+// IEEE a/b compiles to 11 VALU (div_scale x2, rcp, 6 fma, div_fmas, div_fixup).  With y = RN(1/b)
+// known, Markstein's correction q' = q + (a - b*q)*y (q = RN(a*y), residual exact by fma) IS the
+// correctly rounded quotient unless something over/underflows (div_core, 4 VALU).  y itself is
+// v_rcp_f32 + one Newton step (recip_nr, 3 VALU), equal to IEEE 1/b for every normal b with a
+// normal reciprocal -- all 2^32 patterns checked on MI355X.  div_core == IEEE a/b was checked for
+// every normal divisor x 32 numerators (9.7e10 quotients, 0 mismatches) under: b and y normal, and
+// a == 0 or (q' normal and |a| >= 2^-100).  Call sites establish those conditions from cheap range
+// tests on their operands (a ray's `nice` flag, normalize's own test) and take the IEEE division in
+// a wave-uniform branch otherwise (never taken on real scenes).
+__device__ __forceinline__ float recip_nr(float b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float y0 = __builtin_amdgcn_rcpf(b);
+    return __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0);
+#else
+    return 1.0f / b;
+#endif
+}
+__device__ __forceinline__ float div_core(float a, float b, float y) {
+    const float q = a * y;
+    const float r = __builtin_fmaf(-b, q, a);
+    return __builtin_copysignf(__builtin_fmaf(r, y, q), q);
+}
+__device__ __forceinline__ bool any_lane(bool p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_ballot_w64(p) != 0;
+#else
+    return p;
+#endif
+}
+// |x| as an unsigned key (sign shifted out): 2^e -> (e + 127) << 24, 0 -> 0, inf/NaN above all finite
+__device__ __forceinline__ uint32_t mag2(float x) { return __float_as_uint(x) << 1; }
+#define MRT_MAG2(e) ((uint32_t)((e) + 127) << 24)
+// |x| in [2^lo, 2^hi)
+#define MRT_MAG_IN(x, lo, hi) ((mag2(x) - MRT_MAG2(lo)) < (MRT_MAG2(hi) - MRT_MAG2(lo)))
+// a / |a| (Vec3::normalize, vec3.h:116-122): one reciprocal for the three quotients.  Fast path:
+// |a| in [2^-26, 2^26) and every component 0 or >= 2^-100 in magnitude (then each quotient is 0 or
+// normal, and y is normal).
+__device__ __forceinline__ f3 normalize(f3 a) {
+    const float len = sqrt_(sdot(a));
+    const float y = recip_nr(len);
+    f3 q{div_core(a.x, len, y), div_core(a.y, len, y), div_core(a.z, len, y)};
+    const uint32_t mn = min(min(mag2(a.x) - 1u, mag2(a.y) - 1u), mag2(a.z) - 1u);  // 0 -> UINT_MAX
+    const bool ok = MRT_MAG_IN(len, -26, 26) & (mn >= MRT_MAG2(-100) - 1u);
+    if (__builtin_expect(any_lane(!ok), 0)) q = ok ? q : divf(a, len);
+    return q;
+}
 __device__ __forceinline__ f3 cross(f3 a, f3 b) { return f3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
 __device__ __forceinline__ float maxps(float a, float b) { return a > b ? a : b; }
 __device__ __forceinline__ float minps(float a, float b) { return a < b ? a : b; }
@@ -108,18 +159,18 @@ __device__ __forceinline__ f3 random_in_disk(Pcg& r) {
 // NOTE: x,y scaled by 2*sqrt(r2), as the reference does (pcg.cpp:92-93)
 __device__ __forceinline__ f3 random_cosine_direction(Pcg& r) {
     float r1 = randf(r), r2 = randf(r);
-    float z = __builtin_sqrtf(1 - r2);
+    float z = sqrt_(1 - r2);
     float phi = (2 * PI_F) * r1;
-    float s2 = __builtin_sqrtf(r2);
+    float s2 = sqrt_(r2);
     float sp, cp;
     sincos_(phi, &sp, &cp);
     return f3{(cp * 2) * s2, (sp * 2) * s2, z};
 }
 __device__ __forceinline__ f3 random_towards_sphere(Pcg& r, float radius, float dist_sq) {
     float r1 = randf(r), r2 = randf(r);
-    float z = 1 + r2 * (__builtin_sqrtf(1 - (radius * radius) / dist_sq) - 1);
+    float z = 1 + r2 * (sqrt_(1 - (radius * radius) / dist_sq) - 1);
     float phi = (2 * PI_F) * r1;
-    float q = __builtin_sqrtf(1 - z * z);
+    float q = sqrt_(1 - z * z);
     float sp, cp;
     sincos_(phi, &sp, &cp);
     return f3{cp * q, sp * q, z};
@@ -127,11 +178,28 @@ __device__ __forceinline__ f3 random_towards_sphere(Pcg& r, float radius, float 
 
 // ---------------------------------------------------------------- ray (ray.h:18-56)
 struct Ray {
-    f3 o, d, inv;  // inv = 1/d per lane (aabb.h:49), hoisted out of the slab tests
+    f3 o, d, inv;  // inv = RN(1/d) per lane (aabb.h:49), hoisted out of the slab and rect tests
     float time;
     int inside;
     uint32_t mask;
+    bool nice;     // operand ranges under which inv and rect-test quotients take div_core (ray_nice)
 };
+// A ray is `nice` when every direction component has magnitude in [2^-26, 2) and every origin
+// component is 0 or in [2^-77, 2^60]: then inv = recip_nr(d) is exact, and a rect test's
+// (k - o_a) / d_a may use div_core with inv (the difference of two such coordinates -- rect planes are
+// checked on upload, MRT_F_SLOWDIV -- is 0 or >= 2^-100, and the quotient stays normal).
+__device__ __forceinline__ bool ray_nice(f3 o, f3 d) {
+    const bool dn = MRT_MAG_IN(d.x, -26, 1) & MRT_MAG_IN(d.y, -26, 1) & MRT_MAG_IN(d.z, -26, 1);
+    const uint32_t mn = min(min(mag2(o.x) - 1u, mag2(o.y) - 1u), mag2(o.z) - 1u);  // 0 -> UINT_MAX
+    const float mx = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+    return dn & (mn >= MRT_MAG2(-77) - 1u) & (mx <= 0x1p60f);
+}
+// 1/d per component (aabb.h:49), exact
+__device__ __forceinline__ f3 ray_inv(f3 d, bool nice) {
+    f3 y{recip_nr(d.x), recip_nr(d.y), recip_nr(d.z)};
+    if (__builtin_expect(any_lane(!nice), 0)) y = nice ? y : f3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    return y;
+}
 __device__ __forceinline__ Ray make_ray(f3 o, f3 dir, float time, int inside) {
     Ray r;
     r.o = o;
@@ -141,7 +209,8 @@ __device__ __forceinline__ Ray make_ray(f3 o, f3 dir, float time, int inside) {
     // ComputeDirMask runs on the constructor ARGUMENT (ray.h:51 sees the parameter `dir`)
     uint32_t X = __float_as_uint(dir.x) >> 31, Y = __float_as_uint(dir.y) >> 31, Z = __float_as_uint(dir.z) >> 31;
     r.mask = 1u << (Z | (Y << 1) | (X << 2));
-    r.inv = f3{1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z};
+    r.nice = ray_nice(r.o, r.d);
+    r.inv = ray_inv(r.d, r.nice);
     return r;
 }
 __device__ __forceinline__ f3 eval(const Ray& r, float t) { return add(r.o, fmul(t, r.d)); }
@@ -166,6 +235,15 @@ __device__ __forceinline__ bool aabb_hit(f3 bmin, f3 bmax, const Ray& r, float t
 
 // uniform-address reads of scene tables through the constant address space -> s_load
 #define MRT_CONST_AS __attribute__((address_space(4)))
+#define MRT_F_SLOWDIV 0x8u  /* set on upload on rects whose plane coordinate is outside {0} U [2^-77, 2^60] */
+#if defined(__HIP_DEVICE_COMPILE__)
+#define MRT_GLOBAL_AS __attribute__((address_space(1)))
+#define MRT_LDS_AS __attribute__((address_space(3)))
+#else
+#define MRT_GLOBAL_AS
+#define MRT_LDS_AS
+#endif
+typedef float v4f __attribute__((ext_vector_type(4)));  // native vector: loads/stores in any address space
 template <typename T>
 __device__ __forceinline__ const MRT_CONST_AS T* const_ptr(const T* p) {
     return (const MRT_CONST_AS T*)p;
@@ -174,7 +252,7 @@ __device__ __forceinline__ const MRT_CONST_AS T* const_ptr(const T* p) {
 // Phase clock (experiment builds with -DMRT_PHASES): wave-uniform s_memtime deltas per phase.
 #ifdef MRT_PHASES
 struct PhaseClock {
-    uint64_t t, a[4];
+    uint64_t t, a[8];
 };
 #define PH_MARK(pc, i)                                      \
     do {                                                    \

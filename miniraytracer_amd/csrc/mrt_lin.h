@@ -39,6 +39,10 @@ static_assert(sizeof(LinOp) == 64, "LinOp is one 64 B scalar load");
 #define LOP_KIND(o) (((o).code >> 8) & 0xFFu)
 #define LOP_FLAGS(o) (((o).code >> 16) & 0xFFu)
 
+__device__ __forceinline__ uint32_t op_flags(const LinOp& o) { return LOP_FLAGS(o); }
+__device__ __forceinline__ uint32_t op_flags(const MRT_CONST_AS LinOp& o) { return LOP_FLAGS(o); }
+__device__ __forceinline__ uint32_t op_flags(const mrt_node& n) { return MRT_NODE_FLAGS(n); }
+
 // t of the primitive's hit() or a miss; no record written.  KIND is wave-uniform at the call.
 // Branch-free: every lane evaluates the whole test and the outcome is a predicate (the early
 // returns of the reference only skip work whose result is unused, so the outcome is the same).
@@ -53,7 +57,7 @@ __device__ __forceinline__ bool lin_prim_t(const OP& o, const Ray& r, float tmin
         const float b = dot(oc, r.d);
         const float c = sdot(oc) - radius * radius;
         const float disc = b * b - c;
-        const float sq = __builtin_sqrtf(disc);
+        const float sq = sqrt_(disc);
         const float t1 = (-b - sq), t2 = (-b + sq);
         const bool ok1 = (t1 < tmax) & (t1 > tmin);
         const bool ok2 = (r.inside != 0) & (t2 < tmax) & (t2 > tmin);
@@ -68,7 +72,11 @@ __device__ __forceinline__ bool lin_prim_t(const OP& o, const Ray& r, float tmin
                                  : (r.d.x * ns + r.d.y * 0.0f) + r.d.z * 0.0f;
         const float oa = AX == 2 ? r.o.z : AX == 1 ? r.o.y : r.o.x;
         const float da = AX == 2 ? r.d.z : AX == 1 ? r.d.y : r.d.x;
-        const float t = (o.f[4] - oa) / da;
+        const float ia = AX == 2 ? r.inv.z : AX == 1 ? r.inv.y : r.inv.x;
+        const float num = o.f[4] - oa;
+        float t = div_core(num, da, ia);  // (k - o_a) / d_a, exact for a nice ray (make_ray)
+        const bool slow = (op_flags(o) & MRT_F_SLOWDIV) != 0;  // uniform
+        if (__builtin_expect(slow || any_lane(!r.nice), 0)) t = (r.nice && !slow) ? t : num / da;
         const float ob = AX == 0 ? r.o.y : r.o.x, db = AX == 0 ? r.d.y : r.d.x;
         const float oc = AX == 2 ? r.o.y : r.o.z, dc = AX == 2 ? r.d.y : r.d.z;
         const float pb = ob + t * db;
@@ -132,15 +140,14 @@ __device__ __forceinline__ Ray lin_load_ray(const LStack& L) {
     r.time = b[384];
     r.inside = __float_as_int(b[448]);
     r.mask = __float_as_uint(b[512]);
-    r.inv = f3{0, 0, 0};  // box tests take 1/d on demand; mesh_hit callers recompute it
+    r.nice = ray_nice(r.o, r.d);  // recomputed where used (cheaper than parking them in LDS)
+    r.inv = ray_inv(r.d, r.nice);
     return r;
 }
-// aabb::hit with invDir = 1/dir evaluated here, as the reference does per call (aabb.h:49)
+// aabb::hit (invDir = 1/dir of the ray, aabb.h:49)
 __device__ __forceinline__ bool lin_box(const MRT_CONST_AS LinOp& o, const Ray& r, float tmin, float tmax) {
-    Ray q = r;
-    q.inv = f3{1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z};
     const float b[6] = {o.f[0], o.f[1], o.f[2], o.f[3], o.f[4], o.f[5]};
-    return aabb_hit(b, b + 3, q, tmin, tmax);
+    return aabb_hit(b, b + 3, r, tmin, tmax);
 }
 
 // record frames of instance hits, back to the world (scene_object.cpp:13-16, 85-93)
@@ -278,7 +285,6 @@ __device__ __forceinline__ bool scene_hit_lin(const DScene& S, Ray& r, float tmi
                 b[192] = cur.d.x; b[256] = cur.d.y; b[320] = cur.d.z;
             }
             cur = lin_load_ray(L);
-            if constexpr ((F & FT_MESH) != 0) cur.inv = f3{1.0f / cur.d.x, 1.0f / cur.d.y, 1.0f / cur.d.z};  // mesh_hit reads inv
             inst = MRT_NONE;
             lvl--;
         } else if (op == LOP_LIST_END) {

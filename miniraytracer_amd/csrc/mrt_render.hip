@@ -1,7 +1,7 @@
 // mrt_render.hip -- the MI355X render path behind the C-ABI (include/mrt.h).
 //
 // Kernels (DESIGN.md "Kernels"):
-//   mrt_path_kernel   persistent waves pull 64-path batches from one device counter (one atomic
+//   mrt_path_kernel   persistent waves pull 256-path batches (64 near the end of a launch) from one device counter (one atomic
 //                     per wave per batch, like work_queue::getWork pulls a tile,
 //                     work_queue.cpp:158-166) and run trace() for each lane's path to completion;
 //                     per-path radiance is written sample-major [s][local pixel] (coalesced).
@@ -41,6 +41,7 @@ struct PathParams {
     uint32_t width, height, sq, ns;
     uint32_t s0;                          // first sample of this chunk
     uint32_t n_paths;                     // npix * chunk samples (< 2^32, enforced on the host)
+    uint32_t tail_zone;                   // last paths of the launch handed out MRT_TAIL_BATCH at a time
     uint64_t seed;
     uint32_t max_bounces;
     float* __restrict__ rad;              // n_paths * 3 floats, [s - s0][lp]
@@ -70,12 +71,15 @@ template <uint32_t F> struct PathOcc {
 #ifndef MRT_BATCH
 #define MRT_BATCH 256u  // paths a wave claims per atomic on the work counter (one hot address)
 #endif
+#ifndef MRT_TAIL_BATCH
+#define MRT_TAIL_BATCH 64u  // claim size within the last `tail_zone` paths of a launch
+#endif
 #ifdef MRT_PHASES
-__device__ unsigned long long g_phases[4];
+__device__ unsigned long long g_phases[8];
 extern "C" int mrt_debug_phases(unsigned long long* out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phases), sizeof(g_phases)) != hipSuccess) return 1;
     if (reset) {
-        unsigned long long z[4] = {0, 0, 0, 0};
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_phases), z, sizeof(z)) != hipSuccess) return 1;
     }
     return 0;
@@ -101,8 +105,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
     const LStack Ls{wb, (float*)(wb + P.lds_frames * 128), wmesh, (float*)(wmesh + P.lds_mesh * 64), lane};
     const DScene& S = P.sc;
     const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const LevStore<LK> lev{P.lev + slot * P.lev_rows,
-                           (float4*)(wmesh + (P.lds_mesh + P.lds_save) * 64) + lane};
+    const LevStore<LK> lev{(MRT_GLOBAL_AS v4f*)(P.lev + slot * P.lev_rows),
+                           (MRT_LDS_AS v4f*)((float4*)(wmesh + (P.lds_mesh + P.lds_save) * 64) + lane)};
     const uint64_t lt_mask = (1ull << lane) - 1ull;
 
     // main.cpp:180/235 stop on !G_isRunning: a launch of a cancelled render does no work (mrt_render
@@ -123,11 +127,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
         if (need && !exhausted) {
             const uint32_t c = (uint32_t)__popcll(need);
             const uint32_t have = (uint32_t)(pool_end - pool_next);
+            // near the end of the launch, claims shrink so the last ones finish together
+            const uint32_t batch = pool_end + P.tail_zone >= P.n_paths ? MRT_TAIL_BATCH : MRT_BATCH;
             uint64_t nb = 0;
             if (have < c) {
-                if (lane == 0) nb = atomicAdd(P.counter, (unsigned long long)MRT_BATCH);
+                if (lane == 0) nb = atomicAdd(P.counter, (unsigned long long)batch);
                 nb = __shfl(nb, 0);
             }
+            PH_MARK(ph, 0);
             if (!active) {
                 const uint32_t rank = (uint32_t)__popcll(need & lt_mask);
                 const uint64_t i = rank < have ? pool_next + rank : nb + (rank - have);
@@ -154,9 +161,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
                     active = true;
                 }
             }
+            PH_MARK(ph, 4);
             if (have < c) {
                 pool_next = nb + (c - have);
-                pool_end = nb + MRT_BATCH;
+                pool_end = nb + batch;
                 if (nb >= P.n_paths) exhausted = true;
             } else {
                 pool_next += c;
@@ -171,10 +179,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
             PH_MARK(ph, 2);
             if (ended) {
                 L = fold_levels(lev, ps.nlev, L);
+                PH_MARK(ph, 5);
                 float* dst = P.rad + (size_t)idx * 3;
+#ifdef MRT_EXP_NOSTORE
+                if (L.x == 12345.0f)
+#endif
+                {
                 dst[0] = L.x;
                 dst[1] = L.y;
                 dst[2] = L.z;
+                }
                 if (P.path_rays) P.path_rays[idx] = ps.rays;
                 done_rays += ps.rays;
                 active = false;
@@ -184,7 +198,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
     }
 #ifdef MRT_PHASES
     if (lane == 0)
-        for (int i = 0; i < 4; i++) atomicAdd(&g_phases[i], (unsigned long long)ph.a[i]);
+        for (int i = 0; i < 8; i++) atomicAdd(&g_phases[i], (unsigned long long)ph.a[i]);
 #endif
     // one 64-bit add per wave
     uint64_t my = done_rays;
@@ -231,25 +245,44 @@ static uint32_t pick_variant(uint32_t features) {
 
 __device__ __forceinline__ float lum3(f3 c) { return (c.x * 0.212655f + c.y * 0.715158f) + c.z * 0.072187f; }
 
+// one sample of draw()/draw2()'s per-pixel loop
+__device__ __forceinline__ f3 fold_sample(f3 c, f3 smp, uint32_t s, uint32_t mode, float max_lum) {
+    if (mode == 0) {
+        if (!finite3(smp)) smp = c;
+        return add(c, smp);
+    }
+    if (!finite3(smp)) smp = s > 0 ? c : f3{0, 0, 0};
+    if (s > 0) smp = add(c, mulf(sub(smp, c), 1.0f / ((float)s + 1.0f)));
+    float l = lum3(smp);
+    if (l > max_lum) smp = mulf(smp, max_lum / l);
+    return smp;
+}
+// The sum is sequential per pixel (bit-exact order), so the kernel is load-latency bound when
+// few pixels are local (multi-GPU shards): samples are fetched FOLD_DEPTH at a time (coalesced
+// across the wave's pixels) before the dependent adds.
+#define FOLD_DEPTH 16
 __global__ void __launch_bounds__(256) mrt_fold_kernel(const float* __restrict__ rad, float4* __restrict__ acc, uint32_t npix, uint32_t s0,
                                                       uint32_t s1, uint32_t mode, float max_lum) {
     uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
     if (lp >= npix) return;
     float4 a = acc[lp];
     f3 c{a.x, a.y, a.z};
-    for (uint32_t s = s0; s < s1; s++) {
-        const float* q = rad + ((size_t)(s - s0) * npix + lp) * 3;
-        f3 smp{q[0], q[1], q[2]};
-        if (mode == 0) {
-            if (!finite3(smp)) smp = c;
-            c = add(c, smp);
-        } else {
-            if (!finite3(smp)) smp = s > 0 ? c : f3{0, 0, 0};
-            if (s > 0) smp = add(c, mulf(sub(smp, c), 1.0f / ((float)s + 1.0f)));
-            float l = lum3(smp);
-            if (l > max_lum) smp = mulf(smp, max_lum / l);
-            c = smp;
+    const float* q = rad + (size_t)lp * 3;
+    const size_t stride = (size_t)npix * 3;
+    uint32_t s = s0;
+    for (; s + FOLD_DEPTH <= s1; s += FOLD_DEPTH) {
+        f3 v[FOLD_DEPTH];
+#pragma unroll
+        for (int k = 0; k < FOLD_DEPTH; k++) {
+            const float* e = q + (size_t)(s - s0 + k) * stride;
+            v[k] = f3{__builtin_nontemporal_load(e), __builtin_nontemporal_load(e + 1), __builtin_nontemporal_load(e + 2)};
         }
+#pragma unroll
+        for (int k = 0; k < FOLD_DEPTH; k++) c = fold_sample(c, v[k], s + k, mode, max_lum);
+    }
+    for (; s < s1; s++) {
+        const float* e = q + (size_t)(s - s0) * stride;
+        c = fold_sample(c, f3{e[0], e[1], e[2]}, s, mode, max_lum);
     }
     acc[lp] = make_float4(c.x, c.y, c.z, 0.0f);
 }
@@ -548,6 +581,13 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
         if ((k == MRT_K_SPHERE || k == MRT_K_XY || k == MRT_K_XZ || k == MRT_K_YZ) && n.mat < v->n_materials &&
             needs_uv_tex(v, v->materials[n.mat].tex))
             n.kind |= MRT_F_NEEDUV << 16;
+    }
+    // rect planes outside {0} U [2^-77, 2^60] keep the IEEE division in rect tests (mrt_device.h ray_nice)
+    for (mrt_node& n : nodes) {
+        const uint32_t k = n.kind & 0xFF;
+        if (k != MRT_K_XY && k != MRT_K_XZ && k != MRT_K_YZ) continue;
+        const float c = std::fabs(n.f[4]);
+        if (!(c == 0.0f || (c >= 0x1p-77f && c <= 0x1p60f))) n.kind |= MRT_F_SLOWDIV << 16;
     }
     for (mrt_node& n : nodes) {
         if ((n.kind & 0xFF) != MRT_K_TRANSLATE || n.a >= nodes.size()) continue;
@@ -903,6 +943,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.ns = ns;
         P.s0 = s0;
         P.n_paths = s->npix * (s1 - s0);
+        P.tail_zone = (uint32_t)std::min<uint64_t>((uint64_t)s->grid * 4 * 2 * MRT_BATCH, P.n_paths);  // ~2 big claims per wave
         P.seed = d->seed;
         P.max_bounces = d->max_bounces;
         P.rad = s->d_rad;

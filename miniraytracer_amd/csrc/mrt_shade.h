@@ -105,7 +105,7 @@ __device__ __forceinline__ float leaf_pdf_value(const DScene& S, const mrt_node&
         Ray r = make_ray(origin, dir, time, 0);
         if (sphere_hit<F>(n, r, 0.001f, FLT_MAX_, rec, false)) {
             float radius = n.f[8];
-            float cos_theta_max = __builtin_sqrtf(1 - (radius * radius) / sdot(sub(sphere_center<F>(n, time), origin)));
+            float cos_theta_max = sqrt_(1 - (radius * radius) / sdot(sub(sphere_center<F>(n, time), origin)));
             float solid_angle = (2 * PI_F) * (1 - cos_theta_max);
             return 1 / solid_angle;
         }
@@ -192,13 +192,22 @@ static constexpr uint32_t LEV_LOUD = 0x80000000u;
 // Fold levels of one lane: the first LK in LDS ([level][lane] float4), deeper ones in HBM.
 template <uint32_t LK>
 struct LevStore {
-    float4* g;    // this lane's HBM rows
-    float4* lds;  // this lane's first LDS slot (stride 64 float4 per level)
+    // explicit address spaces: a generic pointer here made the compiler merge the two cases into
+    // one flat access, which counts against vmcnt AND lgkmcnt (every later LDS wait then waited
+    // for the level store to reach memory)
+    MRT_GLOBAL_AS v4f* g;  // this lane's HBM rows
+    MRT_LDS_AS v4f* lds;   // this lane's first LDS slot (stride 64 float4 per level)
     __device__ __forceinline__ void put(uint32_t d, float4 v) const {
-        if (LK > 0 && d < LK) lds[d * 64] = v;
-        else g[d] = v;
+        const v4f w = {v.x, v.y, v.z, v.w};
+        if (LK > 0 && d < LK) lds[d * 64] = w;
+        else g[d] = w;
     }
-    __device__ __forceinline__ float4 get(uint32_t d) const { return (LK > 0 && d < LK) ? lds[d * 64] : g[d]; }
+    __device__ __forceinline__ float4 get(uint32_t d) const {
+        v4f w;
+        if (LK > 0 && d < LK) w = lds[d * 64];
+        else w = g[d];
+        return make_float4(w.x, w.y, w.z, w.w);
+    }
 };
 // A level is quiet when folding +0 through it gives +0 exactly: finite factors, for diffuse a
 // pdf > 0 (0 + (a * 0) / pdf == +0), for metal non-negative factors (att * +0 == +0).
@@ -280,8 +289,8 @@ __device__ __forceinline__ bool trace_segment(const DScene& S, PathState& ps, ui
         const float ncosI = dot(r.d, facing);
         const float sinT2 = (nio * nio) * (1.0f - ncosI * ncosI);
         if (sinT2 <= 1.0f) {
-            const float cosT = __builtin_sqrtf(1.0f - sinT2);
-            const float cs = cosI < 0 ? __builtin_sqrtf(1.0f - (nio * nio) * (1.0f - cosI * cosI)) : cosI;
+            const float cosT = sqrt_(1.0f - sinT2);
+            const float cs = cosI < 0 ? sqrt_(1.0f - (nio * nio) * (1.0f - cosI * cosI)) : cosI;
             float r0 = (1 - ref) / (1 + ref);
             r0 = r0 * r0;
             const float reflect_prob = r0 + (1 - r0) * pow5_((1 - cs));
@@ -308,6 +317,7 @@ __device__ __forceinline__ bool trace_segment(const DScene& S, PathState& ps, ui
         surface = false;
     }
     if (surface) gen = lamb ? onb_apply(rec.n, random_cosine_direction(ps.rng)) : random_in_sphere(ps.rng);
+    PH_MARK(ph, 6);
     const Ray sc = make_ray(rec.p, gen, r.time, 0);
     float sval, spdf;
     if (lamb) {

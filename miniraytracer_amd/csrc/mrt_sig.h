@@ -120,7 +120,6 @@ struct SigWalk {
                     }
                 }
                 w.cur = lin_load_ray(L);
-                if constexpr ((F & FT_MESH) != 0) w.cur.inv = f3{1.0f / w.cur.d.x, 1.0f / w.cur.d.y, 1.0f / w.cur.d.z};
                 run<skip + 1, END>(S, prog, tmin, w, on, rec, L);
             } else {
                 run<PC + 1, END>(S, prog, tmin, w, on, rec, L);

@@ -136,7 +136,7 @@ __device__ __forceinline__ bool sphere_hit(const mrt_node& n, const Ray& r, floa
     float c = sdot(oc) - radius * radius;
     float disc = b * b - c;
     if (disc > 0) {
-        float sq = __builtin_sqrtf(disc);
+        float sq = sqrt_(disc);
         float t = (-b - sq);
         bool ok = t < tmax && t > tmin;
         if (!ok && r.inside) {
@@ -376,7 +376,7 @@ __device__ __forceinline__ void push_ray(const LStack& L, uint32_t slot, const R
     b[192] = r.d.x; b[256] = r.d.y; b[320] = r.d.z;
     b[384] = r.inv.x; b[448] = r.inv.y; b[512] = r.inv.z;
     b[576] = __int_as_float(r.inside);
-    b[640] = __uint_as_float(r.mask);
+    b[640] = __uint_as_float(r.mask | ((uint32_t)r.nice << 31));
 }
 __device__ __forceinline__ void pop_ray(const LStack& L, uint32_t slot, Ray& r) {
     const float* b = L.rays + slot * 11 * 64 + L.lane;
@@ -384,7 +384,9 @@ __device__ __forceinline__ void pop_ray(const LStack& L, uint32_t slot, Ray& r) 
     r.d = f3{b[192], b[256], b[320]};
     r.inv = f3{b[384], b[448], b[512]};
     r.inside = __float_as_int(b[576]);
-    r.mask = __float_as_uint(b[640]);
+    const uint32_t m = __float_as_uint(b[640]);
+    r.mask = m & 0xFFu;
+    r.nice = (m >> 31) != 0;
 }
 
 // rotate_y::hit ray transform (scene_object.cpp:75-82)

@@ -1,4 +1,4 @@
 cd $GRAFT_REPO_ROOT
 cp exp/libmrt_ph.so miniraytracer_amd/libmrt.so
-for a in "5 500 500 256" "0 400 200 64" "7 256 256 64" "9 400 400 64"; do timeout -k 10 120 python tools/_phases.py $a || break; done
+for a in ${PH_CFGS:-"5 500 500 256" "8 512 512 64" "7 256 256 64"}; do NPH=${NPH:-8} timeout -k 10 120 python tools/_phases.py $a || break; done
 cp exp/libmrt_w0.so miniraytracer_amd/libmrt.so

@@ -17,7 +17,7 @@ lib().mrt_debug_phases(out, 1)
 img, rays = r.render(d)
 lib().mrt_debug_phases(out, 1)
 v = np.array(list(out), dtype=np.float64)
-names = ["regen+loop", "scene_hit", "shading", "fold+write", "mat->ld", "mat..lamb", "dirgen", "sc ray..pdf"][:NPH]
+names = ["loop+pool", "scene_hit", "shade:pdf+lev", "write+bottom", "new path", "fold", "shade:mat+dir", "-"][:NPH]
 print(f"scene {scene} {w}x{h}x{spp}: rays {rays}")
 for n, x in zip(names, v):
     print(f"  {n:12s} {100 * x / v.sum():6.2f}%")
