@@ -28,11 +28,6 @@ struct f3 {
     float x, y, z;
 };
 __device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
-// Correctly rounded f32 square root.  (RN32(v_sqrt_f64(x)) is NOT: v_sqrt_f64 is approximate and
-// misrounds 3.9% of f32 inputs, tools/numcheck/divsqrt_check.hip.)
-__device__ __forceinline__ float sqrt_(float x) {
-    return __builtin_sqrtf(x);
-}
 __device__ __forceinline__ f3 add(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
 __device__ __forceinline__ f3 sub(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
 __device__ __forceinline__ f3 mul(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
@@ -76,16 +71,38 @@ __device__ __forceinline__ uint32_t mag2(float x) { return __float_as_uint(x) <<
 #define MRT_MAG2(e) ((uint32_t)((e) + 127) << 24)
 // |x| in [2^lo, 2^hi)
 #define MRT_MAG_IN(x, lo, hi) ((mag2(x) - MRT_MAG2(lo)) < (MRT_MAG2(hi) - MRT_MAG2(lo)))
+// Correctly rounded f32 square root.  hipcc's expansion is v_sqrt_f32, a one-ulp neighbour test
+// by fma residuals, and a 2^32 scaling of inputs below 2^-96 (+ zero/inf fix-up); the core alone
+// equals it for every input with |x| >= 2^-96 or x == +-0 (all 2^32 patterns checked on MI355X,
+// tools/numcheck/sqrt_check.hip).  (RN32(v_sqrt_f64(x)) is NOT exact: v_sqrt_f64 misrounds 3.9% of
+// f32 inputs, tools/numcheck/divsqrt_check.hip.)
+__device__ __forceinline__ float sqrt_core(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sdn = __uint_as_float(__float_as_uint(s) - 1u), sup = __uint_as_float(__float_as_uint(s) + 1u);
+    const float r = __builtin_fmaf(-sdn, s, x) <= 0.0f ? sdn : s;
+    return __builtin_fmaf(-sup, s, x) > 0.0f ? sup : r;
+#else
+    return __builtin_sqrtf(x);
+#endif
+}
+__device__ __forceinline__ float sqrt_(float x) {
+    float r = sqrt_core(x);
+    const bool ok = mag2(x) - 1u >= MRT_MAG2(-96) - 1u;  // |x| >= 2^-96 or x == +-0
+    if (__builtin_expect(any_lane(!ok), 0)) r = ok ? r : __builtin_sqrtf(x);
+    return r;
+}
 // a / |a| (Vec3::normalize, vec3.h:116-122): one reciprocal for the three quotients.  Fast path:
-// |a| in [2^-26, 2^26) and every component 0 or >= 2^-100 in magnitude (then each quotient is 0 or
-// normal, and y is normal).
+// |a|^2 in [2^-52, 2^52) and every component 0 or >= 2^-100 in magnitude (then each quotient is 0
+// or normal, and y is normal).
 __device__ __forceinline__ f3 normalize(f3 a) {
-    const float len = sqrt_(sdot(a));
+    const float dd = sdot(a);
+    const float len = sqrt_core(dd);  // |a|^2 in [2^-52, 2^52): the core is exact, |a| in [2^-26, 2^26)
     const float y = recip_nr(len);
     f3 q{div_core(a.x, len, y), div_core(a.y, len, y), div_core(a.z, len, y)};
     const uint32_t mn = min(min(mag2(a.x) - 1u, mag2(a.y) - 1u), mag2(a.z) - 1u);  // 0 -> UINT_MAX
-    const bool ok = MRT_MAG_IN(len, -26, 26) & (mn >= MRT_MAG2(-100) - 1u);
-    if (__builtin_expect(any_lane(!ok), 0)) q = ok ? q : divf(a, len);
+    const bool ok = MRT_MAG_IN(dd, -52, 52) & (mn >= MRT_MAG2(-100) - 1u);
+    if (__builtin_expect(any_lane(!ok), 0)) q = ok ? q : divf(a, __builtin_sqrtf(dd));
     return q;
 }
 __device__ __forceinline__ f3 cross(f3 a, f3 b) { return f3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
@@ -159,9 +176,10 @@ __device__ __forceinline__ f3 random_in_disk(Pcg& r) {
 // NOTE: x,y scaled by 2*sqrt(r2), as the reference does (pcg.cpp:92-93)
 __device__ __forceinline__ f3 random_cosine_direction(Pcg& r) {
     float r1 = randf(r), r2 = randf(r);
-    float z = sqrt_(1 - r2);
+    // randf() is 0 or >= 2^-23: both radicands are 0 or in [2^-23, 1], where sqrt_core is exact
+    float z = sqrt_core(1 - r2);
     float phi = (2 * PI_F) * r1;
-    float s2 = sqrt_(r2);
+    float s2 = sqrt_core(r2);
     float sp, cp;
     sincos_(phi, &sp, &cp);
     return f3{(cp * 2) * s2, (sp * 2) * s2, z};

@@ -39,6 +39,8 @@ struct PathParams {
     uint32_t npix;                        // local pixel count
     double inv_npix;                      // 1.0 / npix (path index -> sample row without a divide)
     uint32_t width, height, sq, ns;
+    float inv_w, inv_h;                   // RN(1/width), RN(1/height)
+    uint32_t fast_uv;                     // width, height <= 2^24 and sq <= 2^16: u, v through div_core
     uint32_t s0;                          // first sample of this chunk
     uint32_t n_paths;                     // npix * chunk samples (< 2^32, enforced on the host)
     uint32_t tail_zone;                   // last paths of the launch handed out MRT_TAIL_BATCH at a time
@@ -150,8 +152,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
                     const uint32_t x = xy.x, y = xy.y;
                     const uint32_t pix = x + y * P.width;
                     const float2 dd = P.sdist[s];  // ((i + 0.5) / sq, (j + 0.5) / sq), s = i*sq + j
-                    const float u = ((float)x + dd.x) / (float)P.width;
-                    const float v = ((float)y + dd.y) / (float)P.height;
+                    // (x + dx) / W with RN(1/W) from the host: numerator >= 1/(2 sq) >= 2^-17, W <= 2^24
+                    const float nu = (float)x + dd.x, nv = (float)y + dd.y;
+                    float u = div_core(nu, (float)P.width, P.inv_w), v = div_core(nv, (float)P.height, P.inv_h);
+                    if (!P.fast_uv) { u = nu / (float)P.width; v = nv / (float)P.height; }
                     const uint64_t path_id = (uint64_t)pix * P.ns + s;
                     pcg_seed(ps.rng, splitmix64(P.seed ^ path_id), path_id);
                     ps.r = camera_ray(S, ps.rng, u, v);
@@ -750,6 +754,12 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
             d.flags = DMAT_COLOR;
             for (int k = 0; k < 4; k++) d.col[k] = v->textures[m.tex].f[k];
         }
+        if (m.kind == MRT_M_DIELECTRIC) {  // dielectric::scatter's per-material quotients (material.h:121-175)
+            const float ref = m.p;
+            d.col[0] = 1.0f / ref;
+            float r0 = (1 - ref) / (1 + ref);
+            d.col[1] = r0 * r0;
+        }
     }
     UP(dmats.data(), dmats.size(), &S.mats);
     // scene.biased_objects flattened: an object_list's children, or the object itself
@@ -939,6 +949,9 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.inv_npix = 1.0 / (double)std::max<uint32_t>(s->npix, 1);
         P.width = d->width;
         P.height = d->height;
+        P.inv_w = 1.0f / (float)d->width;
+        P.inv_h = 1.0f / (float)d->height;
+        P.fast_uv = d->width <= (1u << 24) && d->height <= (1u << 24) && d->sqrt_samples <= (1u << 16);
         P.sq = d->sqrt_samples;
         P.ns = ns;
         P.s0 = s0;

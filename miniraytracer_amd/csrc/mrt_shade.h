@@ -281,7 +281,7 @@ __device__ __forceinline__ bool trace_segment(const DScene& S, PathState& ps, ui
             nio = ref;
         } else {
             facing = rec.n;
-            nio = 1.0f / ref;
+            nio = M.col[0];  // 1.0f / ref, computed on upload (the same IEEE quotient)
         }
         f3 nd = sub(r.d, fmul(2.0f * dot(r.d, rec.n), rec.n));  // reflect (vec3.h:178-181)
         int inside = r.inside;
@@ -291,8 +291,7 @@ __device__ __forceinline__ bool trace_segment(const DScene& S, PathState& ps, ui
         if (sinT2 <= 1.0f) {
             const float cosT = sqrt_(1.0f - sinT2);
             const float cs = cosI < 0 ? sqrt_(1.0f - (nio * nio) * (1.0f - cosI * cosI)) : cosI;
-            float r0 = (1 - ref) / (1 + ref);
-            r0 = r0 * r0;
+            const float r0 = M.col[1];  // ((1 - ref) / (1 + ref))^2, computed on upload
             const float reflect_prob = r0 + (1 - r0) * pow5_((1 - cs));
             if (!(randf(ps.rng) < reflect_prob)) {
                 nd = add(fmul(nio, r.d), fmul(nio * -ncosI - cosT, facing));
@@ -322,7 +321,11 @@ __device__ __forceinline__ bool trace_segment(const DScene& S, PathState& ps, ui
     float sval, spdf;
     if (lamb) {
         const float cosine = dot(sc.d, rec.n);
-        sval = cosine > 0 ? cosine / PI_F : 0;
+        // cosine / PI_F through div_core: PI_F and RN(1/PI_F) are normal, cosine <= 1
+        constexpr float INV_PI = 1.0f / PI_F;
+        float sv = div_core(cosine, PI_F, INV_PI);
+        if (__builtin_expect(any_lane((cosine > 0) & (cosine < 0x1p-100f)), 0)) sv = cosine < 0x1p-100f ? cosine / PI_F : sv;
+        sval = cosine > 0 ? sv : 0;
         spdf = cosine < 0 ? 0 : cosine * (1.0f / PI_F);  // dot(rec.n, dir) == dot(dir, rec.n)
     } else {
         sval = 1 / (2 * PI_F);
