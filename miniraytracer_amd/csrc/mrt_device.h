@@ -237,13 +237,23 @@ __device__ __forceinline__ f3 eval(const Ray& r, float t) { return add(r.o, fmul
 __device__ __forceinline__ bool aabb_hit(const float* bmin, const float* bmax, const Ray& r, float tmin, float tmax) {
     float t0x = (bmin[0] - r.o.x) * r.inv.x, t0y = (bmin[1] - r.o.y) * r.inv.y, t0z = (bmin[2] - r.o.z) * r.inv.z;
     float t1x = (bmax[0] - r.o.x) * r.inv.x, t1y = (bmax[1] - r.o.y) * r.inv.y, t1z = (bmax[2] - r.o.z) * r.inv.z;
-    bool lx = r.inv.x < 0.0f, ly = r.inv.y < 0.0f, lz = r.inv.z < 0.0f;
-    float ax = lx ? t1x : t0x, bx = lx ? t0x : t1x;
-    float ay = ly ? t1y : t0y, by = ly ? t0y : t1y;
-    float az = lz ? t1z : t0z, bz = lz ? t0z : t1z;
-    float lo = maxps(maxps(ax, az), maxps(ay, tmin));
-    float hi = minps(minps(bx, bz), minps(by, tmax));
-    return hi > lo;
+    // A nice ray (|inv| <= 2^26, |o| <= 2^60) with a box of finite coordinates gets no NaN slab
+    // values, and (bmin - o) * inv <= (bmax - o) * inv exactly when inv >= 0: the blendv swap is a
+    // min/max, and maxps/minps (NaN-asymmetric) are plain max/min.  The result is a comparison, so
+    // the zero signs min/max may pick do not matter.
+    float lo = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0z, t1z)), fmaxf(fminf(t0y, t1y), tmin));
+    float hi = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0z, t1z)), fminf(fmaxf(t0y, t1y), tmax));
+    bool h = hi > lo;
+    if (__builtin_expect(any_lane(!r.nice), 0)) {
+        bool lx = r.inv.x < 0.0f, ly = r.inv.y < 0.0f, lz = r.inv.z < 0.0f;
+        float ax = lx ? t1x : t0x, bx = lx ? t0x : t1x;
+        float ay = ly ? t1y : t0y, by = ly ? t0y : t1y;
+        float az = lz ? t1z : t0z, bz = lz ? t0z : t1z;
+        float lo2 = maxps(maxps(ax, az), maxps(ay, tmin));
+        float hi2 = minps(minps(bx, bz), minps(by, tmax));
+        h = r.nice ? h : hi2 > lo2;
+    }
+    return h;
 }
 
 __device__ __forceinline__ bool aabb_hit(f3 bmin, f3 bmax, const Ray& r, float tmin, float tmax) {

@@ -67,22 +67,29 @@ __device__ __forceinline__ bool lin_prim_t(const OP& o, const Ray& r, float tmin
         // xy/xz/yz_rect::hit (rect.cpp:24-45, 69-90, 130-151)
         constexpr int AX = KIND == MRT_K_XY ? 2 : KIND == MRT_K_XZ ? 1 : 0;
         const float ns = o.f[5];
-        const float dn = AX == 2 ? (r.d.x * 0.0f + r.d.y * 0.0f) + r.d.z * ns
-                       : AX == 1 ? (r.d.x * 0.0f + r.d.y * ns) + r.d.z * 0.0f
-                                 : (r.d.x * ns + r.d.y * 0.0f) + r.d.z * 0.0f;
         const float oa = AX == 2 ? r.o.z : AX == 1 ? r.o.y : r.o.x;
         const float da = AX == 2 ? r.d.z : AX == 1 ? r.d.y : r.d.x;
         const float ia = AX == 2 ? r.inv.z : AX == 1 ? r.inv.y : r.inv.x;
         const float num = o.f[4] - oa;
-        float t = div_core(num, da, ia);  // (k - o_a) / d_a, exact for a nice ray (make_ray)
+        // nice ray (make_ray): (k - o_a) / d_a through div_core, and the one-sided test
+        // dot(dir, n) > 0 reduces to d_a * ns > 0 (the other products are zeros of finite values)
+        float t = div_core(num, da, ia);
+        bool back = da * ns > 0.0f;
         const bool slow = (op_flags(o) & MRT_F_SLOWDIV) != 0;  // uniform
-        if (__builtin_expect(slow || any_lane(!r.nice), 0)) t = (r.nice && !slow) ? t : num / da;
+        if (__builtin_expect(slow || any_lane(!r.nice), 0)) {  // the reference's forms
+            const float dn = AX == 2 ? (r.d.x * 0.0f + r.d.y * 0.0f) + r.d.z * ns
+                           : AX == 1 ? (r.d.x * 0.0f + r.d.y * ns) + r.d.z * 0.0f
+                                     : (r.d.x * ns + r.d.y * 0.0f) + r.d.z * 0.0f;
+            const bool ex = slow || !r.nice;
+            t = ex ? num / da : t;
+            back = ex ? dn > 0.0f : back;
+        }
         const float ob = AX == 0 ? r.o.y : r.o.x, db = AX == 0 ? r.d.y : r.d.x;
         const float oc = AX == 2 ? r.o.y : r.o.z, dc = AX == 2 ? r.d.y : r.d.z;
         const float pb = ob + t * db;
         const float pc = oc + t * dc;
         *tout = t;
-        return !(dn > 0.0f) & !((t < tmin) | (t > tmax)) & !((pb < o.f[0]) | (pb > o.f[1]) | (pc < o.f[2]) | (pc > o.f[3]));
+        return !back & !((t < tmin) | (t > tmax)) & !((pb < o.f[0]) | (pb > o.f[1]) | (pc < o.f[2]) | (pc > o.f[3]));
     }
 }
 
