@@ -28,7 +28,9 @@ METRIC = "Mrays/sec (primary+secondary), Cornell box 32-bounce; per-pixel RMSE v
 # algorithmic bytes per ray: sum over the reference's tests per ray of the compact
 # FP32 payload each test reads (aabb 24-32 B, rect 24 B, sphere 16 B, triangle 36 B, instance 20 B)
 B_RAY = {5: 256.0, 9: 434.0, 8: 1251.0, 7: 780.0, 0: 976.0}
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+WORKLOAD = {5: "C2 cornell_box", 9: "C3 wt_teapot in cornell box", 8: "C4 bunny", 7: "C5 book2 final scene",
+            0: "C1 random spheres"}  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
 
 def parse():
@@ -45,6 +47,8 @@ def parse():
                     help="work_queue tile edge; also the multi-GPU partition grain (tile k -> rank k %% N)")
     ap.add_argument("--cpu-spp", type=int, default=256, help="spp of the bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel-reps", type=int, default=3,
+                    help="extra renders after the timed region whose HIP-event kernel time feeds roofline")
     ap.add_argument("--emulate-world", type=int, default=1,
                     help="single-GPU rehearsal: render only rank --emulate-rank's share of an N-rank job "
                          "(no collectives); used to predict per-rank step time at N GPUs")
@@ -154,7 +158,7 @@ def main():
 
     # dominant kernel: mrt_path_kernel, HIP events recorded on the launch stream (3 extra renders)
     kms = []
-    for _ in range(3):
+    for _ in range(max(args.kernel_reps, 1)):
         rnd.render_device(desc, out.data_ptr(), rays.data_ptr(), stream.cuda_stream)
         ms, launches = rnd.kernel_ms()
         kms.append(ms / max(launches, 1))
@@ -189,7 +193,7 @@ def main():
             "vs_baseline": None,
             "dtype": "fp32",
             "data": "synthetic scene (reference scene builder, deterministic seeds)",
-            "config": {"workload": f"C2 cornell_box: scene {args.scene}, {args.width}x{args.height}, "
+            "config": {"workload": f"{WORKLOAD.get(args.scene, 'scene')}: scene {args.scene}, {args.width}x{args.height}, "
                                    f"{desc.sqrt_samples ** 2} spp, depth {args.depth}, draw() accumulation",
                        "scene": args.scene, "width": args.width, "height": args.height,
                        "spp": desc.sqrt_samples ** 2, "depth": args.depth, "parallelism": f"tiles{world}",
