@@ -53,6 +53,9 @@ def parse():
                     help="single-GPU rehearsal: render only rank --emulate-rank's share of an N-rank job "
                          "(no collectives); used to predict per-rank step time at N GPUs")
     ap.add_argument("--emulate-rank", type=int, default=0)
+    ap.add_argument("--pipeline", type=int, default=2,
+                    help="render contexts used round-robin on their own HIP streams: step i+1's launch "
+                         "fills the CUs freed by step i's tail instead of waiting for it")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_cornell_c2.json"))
     return ap.parse_args()
 
@@ -98,17 +101,22 @@ def main():
 
     # scene build + upload + workspace: outside the timed region (main.cpp:309 precedes 375)
     scene = m.select_scene(args.scene, args.width / args.height)
-    rnd = m.Renderer(scene, device=local)
+    npipe = max(1, args.pipeline)
+    rnds = [m.Renderer(scene, device=local) for _ in range(npipe)]
+    rnd = rnds[0]
     d_rank, d_world = rank, world
     if world == 1 and args.emulate_world > 1:
         d_rank, d_world = args.emulate_rank, args.emulate_world
     desc = m.render_desc(args.width, args.height, args.samples, depth=args.depth, tile_size=args.tile_size, rank=d_rank, world=d_world)
-    rnd.prepare(desc)
+    for r in rnds:
+        r.prepare(desc)
     px = m.local_pixels(desc)
     n_local = len(px)
-    out = torch.zeros((n_local, 4), dtype=torch.float32, device=dev)
-    rays = torch.zeros(1, dtype=torch.int64, device=dev)
+    outs = [torch.zeros((n_local, 4), dtype=torch.float32, device=dev) for _ in range(npipe)]
+    out = outs[0]
+    rays = torch.zeros(1, dtype=torch.int64, device=dev)  # every context adds its rays here (device atomics)
     stream = torch.cuda.current_stream(dev)
+    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(npipe - 1)]
 
     if world > 1:
         from miniraytracer_amd.dist import TileGather
@@ -116,15 +124,21 @@ def main():
         assert tg.n_local == n_local
 
     pending = [None]
+    it = [0]
 
     def step():
-        rnd.render_device(desc, out.data_ptr(), rays.data_ptr(), stream.cuda_stream)
-        if world > 1:
-            # the one RCCL collective of the data path (tile shards -> rank 0), overlapped with the
-            # next render: finish the previous step's gather, then start this one's
-            if pending[0] is not None:
-                tg.finish(pending[0])
-            pending[0] = tg.start(out)
+        # step i renders with context i % npipe on its stream; nothing orders it after step i-1's
+        # kernels, so its waves start on the CUs that step i-1's finished waves leave idle
+        j = it[0] % npipe
+        it[0] += 1
+        with torch.cuda.stream(streams[j]):
+            rnds[j].render_device(desc, outs[j].data_ptr(), rays.data_ptr(), streams[j].cuda_stream)
+            if world > 1:
+                # the one RCCL collective of the data path (tile shards -> rank 0), overlapped with
+                # the next render: finish the previous step's gather, then start this one's
+                if pending[0] is not None:
+                    tg.finish(pending[0])
+                pending[0] = tg.start(outs[j])
 
     def drain():
         if pending[0] is not None:
@@ -197,7 +211,7 @@ def main():
                                    f"{desc.sqrt_samples ** 2} spp, depth {args.depth}, draw() accumulation",
                        "scene": args.scene, "width": args.width, "height": args.height,
                        "spp": desc.sqrt_samples ** 2, "depth": args.depth, "parallelism": f"tiles{world}",
-                       "tile_size": args.tile_size,
+                       "tile_size": args.tile_size, "pipeline": npipe,
                        **({"emulated_share": f"rank {d_rank} of {d_world}"} if d_world != world else {}),
                        "rays_per_step": nrays // args.steps},
             "roofline": roofline,
