@@ -276,6 +276,7 @@ template <typename T>
 __device__ __forceinline__ const MRT_CONST_AS T* const_ptr(const T* p) {
     return (const MRT_CONST_AS T*)p;
 }
+__device__ __forceinline__ f3 ld3(const MRT_CONST_AS float* p) { return f3{p[0], p[1], p[2]}; }
 
 // Phase clock (experiment builds with -DMRT_PHASES): wave-uniform s_memtime deltas per phase.
 #ifdef MRT_PHASES

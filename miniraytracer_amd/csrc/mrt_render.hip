@@ -155,7 +155,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
                     // (x + dx) / W with RN(1/W) from the host: numerator >= 1/(2 sq) >= 2^-17, W <= 2^24
                     const float nu = (float)x + dd.x, nv = (float)y + dd.y;
                     float u = div_core(nu, (float)P.width, P.inv_w), v = div_core(nv, (float)P.height, P.inv_h);
-                    if (!P.fast_uv) { u = nu / (float)P.width; v = nv / (float)P.height; }
+                    if (!P.fast_uv) {  // a real (uniform) branch: the barrier keeps it from being if-converted
+                        asm volatile("" ::: "memory");
+                        u = nu / (float)P.width;
+                        v = nv / (float)P.height;
+                    }
                     const uint64_t path_id = (uint64_t)pix * P.ns + s;
                     pcg_seed(ps.rng, splitmix64(P.seed ^ path_id), path_id);
                     ps.r = camera_ray(S, ps.rng, u, v);
@@ -789,6 +793,7 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     const uint32_t prog_ops = (uint32_t)lc.prog.size();
     lc.prog.push_back(LinOp{});  // LOP_END
     UP(lc.prog.data(), lc.prog.size(), &S.prog);
+    UP(&v->camera, 1, &S.camp);
 #undef UP
     S.root = v->root;
     S.biased = v->biased;

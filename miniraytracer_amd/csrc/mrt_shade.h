@@ -219,7 +219,12 @@ __device__ __forceinline__ bool quiet_level(float4 v) {
 
 // camera::get_ray (camera.h:38-44)
 __device__ __forceinline__ Ray camera_ray(const DScene& S, Pcg& rng, float s, float t) {
-    const mrt_camera& C = S.cam;
+    // through a pointer the compiler cannot prove loop-invariant: the camera is re-read (scalar
+    // loads, constant cache) at each path start instead of being held in ~40 SGPRs across the
+    // path loop, where it spilled to VGPR lanes and cost a v_readlane per use
+    const MRT_CONST_AS mrt_camera* cp = const_ptr(S.camp);
+    asm volatile("" : "+s"(cp));
+    const MRT_CONST_AS mrt_camera& C = *cp;
     f3 rd = fmul(C.lens_radius, random_in_disk(rng));
     f3 offset = add(mulf(ld3(C.u), rd.x), mulf(ld3(C.v), rd.y));
     float time = C.time0 + (C.time1 - C.time0) * randf(rng);

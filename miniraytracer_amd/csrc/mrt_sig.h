@@ -81,14 +81,14 @@ struct SigWalk {
                 float t;
                 const bool h = lin_prim_t<F, kind>(o, w.cur, tmin, w.closest, &t) & on;
                 w.closest = h ? t : w.closest;
-                w.hnode = h ? PC : w.hnode;  // op index; mapped to the node at the end
+                w.hnode = h ? o.node : w.hnode;  // the op's node (scalar operand): no per-lane lookup later
                 w.hinst = h ? cur_inst<PC>() : w.hinst;
                 w.hdone = h ? false : w.hdone;
                 run<PC + 1, END>(S, prog, tmin, w, on, rec, L);
             } else if constexpr (op == LOP_MESH) {
                 if (on && mesh_hit(S, S.nodes[o.node], w.cur, tmin, w.closest, rec, true, L)) {
                     w.closest = rec.t;
-                    w.hnode = PC;
+                    w.hnode = o.node;
                     w.hinst = cur_inst<PC>();
                     w.hdone = true;
                 }
@@ -127,6 +127,13 @@ struct SigWalk {
         }
     }
 
+    // the program's only instance op (MRT_NONE if it has none or several)
+    __device__ static constexpr uint32_t only_inst() {
+        uint32_t found = MRT_NONE, count = 0;
+        for (uint32_t i = 0; i < G.n; i++)
+            if (G.op[i] == LOP_INST) { found = i; count++; }
+        return count == 1 ? found : MRT_NONE;
+    }
     // op index of the instance enclosing op PC (MRT_NONE: world frame)
     template <uint32_t PC>
     __device__ static constexpr uint32_t cur_inst() {
@@ -153,7 +160,7 @@ __device__ __forceinline__ bool scene_hit_sig(const DScene& S, Ray& r, float tmi
     SigWalk<F, SIG>::template run<0, kSigs[SIG].n - 1>(S, prog, tmin, w, true, rec, L);
     if (INST) r = lin_load_ray(L);
     if (w.hnode == MRT_NONE) return false;
-    const uint32_t node = S.prog[w.hnode].node;  // per-lane op index: vector load
+    const uint32_t node = w.hnode;
     if (INST && w.hinst != MRT_NONE) {
         if (!w.hdone) {
             const float* b = L.save + L.lane + 9 * 64;
@@ -162,7 +169,9 @@ __device__ __forceinline__ bool scene_hit_sig(const DScene& S, Ray& r, float tmi
             ir.d = f3{b[192], b[256], b[320]};
             lin_prim_rec<F>(S, node, ir, w.closest, rec);
         }
-        lin_untransform(S.prog[w.hinst], rec);
+        constexpr uint32_t IPC = SigWalk<F, SIG>::only_inst();
+        if constexpr (IPC != MRT_NONE) lin_untransform(prog[IPC], rec);  // known instance: scalar loads
+        else lin_untransform(S.prog[w.hinst], rec);
     } else if (!w.hdone) {
         lin_prim_rec<F>(S, node, r, w.closest, rec);
     }

@@ -67,6 +67,7 @@ struct DScene {
     uint32_t nbleaf, blist;              // leaf count; 1 if biased_objects is an object_list
     uint32_t root, biased, sky;
     mrt_camera cam;
+    const mrt_camera* __restrict__ camp;  // the camera in HBM, read at each path start (scalar loads)
 };
 
 #define MRT_NODE_KIND(n) ((n).kind & 0xFFu)

@@ -11,6 +11,11 @@ Fixtures (all small; data only -- inputs and expected outputs):
   stream_5_mode1.npz      same for draw2() (mode 1) accumulation
   shipped_5.npz           as-shipped multithreaded reference render (statistical parity)
   tonemap_<id>.npz        the reference display loop's input (linear buffer) and Drago/ARGB32 output
+  shipped_stream_5*.npz   stream-matched render by the reference AS SHIPPED (FMA contraction, glibc
+                          libm): the tolerance fixture of the per-pixel RMSE < 1e-3 criterion
+                          (SURVEY 8(d) parity 2).  Full C2 (500x500, 1024 spp): rows 200-299, 25x25
+                          block means, channel means, ray count; and 128x128 x 256 spp whole image.
+                          `--only-shipped-stream` regenerates just these two.
 """
 import gzip
 import json
@@ -60,7 +65,34 @@ def canon_scene(o):
     return o
 
 
+def read_pfm(p, w, h):
+    raw = open(p, "rb").read().split(b"\n", 3)
+    return np.frombuffer(raw[3], dtype="<f4").reshape(h, w, 3)
+
+
+def shipped_stream(tmp):
+    """The shipped build, stream-matched (same per-path key as the GPU), full C2 and a small case."""
+    img = os.path.join(tmp, "ss.pfm")
+    meta = json.loads(run(SHIPPED, ["--h-mode", "stream", "-width", 500, "-height", 500, "-samples", 1024, "-depth", 32,
+                                    "--h-threads", 8, "--h-out", img, "-scene", 5]))
+    im = read_pfm(img, 500, 500)
+    np.savez_compressed(os.path.join(OUT, "shipped_stream_5.npz"), band=im[200:300].copy(), band_rows=np.array([200, 300]),
+                        block_mean=im.reshape(20, 25, 20, 25, 3).mean(axis=(1, 3), dtype=np.float64),
+                        mean=im.reshape(-1, 3).mean(axis=0, dtype=np.float64), rays=np.array([meta["rays"]], dtype=np.int64),
+                        meta=np.array([5, 500, 500, 1024, 32], dtype=np.int64))
+    print("shipped stream C2", meta)
+    meta = json.loads(run(SHIPPED, ["--h-mode", "stream", "-width", 128, "-height", 128, "-samples", 256, "-depth", 32,
+                                    "--h-threads", 8, "--h-out", img, "-scene", 5]))
+    np.savez_compressed(os.path.join(OUT, "shipped_stream_5_small.npz"), image=read_pfm(img, 128, 128),
+                        rays=np.array([meta["rays"]], dtype=np.int64), meta=np.array([5, 128, 128, 256, 32], dtype=np.int64))
+    print("shipped stream small", meta)
+
+
 def main():
+    if "--only-shipped-stream" in sys.argv:
+        with tempfile.TemporaryDirectory() as tmp:
+            shipped_stream(tmp)
+        return
     if not (os.path.exists(EXACT) and os.path.isdir(REF)):
         sys.exit("needs oracle/_ref (run oracle/ref/build_ref.sh) and /root/reference")
     os.makedirs(OUT, exist_ok=True)
@@ -115,6 +147,8 @@ def main():
             out = np.fromfile(argb, dtype="<u4").reshape(h, w)
             np.savez_compressed(os.path.join(OUT, f"tonemap_{sid}.npz"), linear=lin, argb=out)
             print("tonemap", sid, int(out.min()), int(out.max()))
+
+        shipped_stream(tmp)
 
         # 5. shipped reference (multithreaded, its own worker seeds): statistical parity fixture
         if os.path.exists(os.path.join(OUT, "shipped_5.npz")) and "--force" not in sys.argv:
