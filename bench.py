@@ -145,6 +145,12 @@ def main():
             tg.finish(pending[0])
             pending[0] = None
 
+    # setup, untimed: one render per context, so every context's first-use costs (workspace
+    # first touch, first launch on its stream) are paid before the warmup steps
+    for j in range(npipe):
+        with torch.cuda.stream(streams[j]):
+            rnds[j].render_device(desc, outs[j].data_ptr(), rays.data_ptr(), streams[j].cuda_stream)
+    torch.cuda.synchronize(dev)
     for _ in range(args.warmup):
         step()
     drain()
