@@ -94,7 +94,19 @@ extern "C" int mrt_debug_phases(unsigned long long* out, int reset) {
 #endif
 // fold levels kept in LDS per lane (the rest in HBM): where the LDS budget at the target
 // occupancy allows it
-template <uint32_t F> struct PathLevLds { static constexpr uint32_t K = ((F & 0xFFFFu) == (FT_LIN | FT_INST)) ? 2u : 0u; };
+// (Cornell: 2 at 6 WGs/CU; wide variants at 3 WGs/CU: MRT_LEVK_WIDE; room + mesh: MRT_LEVK_MESH)
+#ifndef MRT_LEVK_WIDE
+#define MRT_LEVK_WIDE 4u
+#endif
+#ifndef MRT_LEVK_MESH
+#define MRT_LEVK_MESH 1u
+#endif
+template <uint32_t F> struct PathLevLds {
+    static constexpr uint32_t K = ((F & 0xFFFFu) == (FT_LIN | FT_INST)) ? 2u
+                                  : PathOcc<F>::kWide                  ? MRT_LEVK_WIDE
+                                  : ((F & FT_MESH) != 0)               ? MRT_LEVK_MESH
+                                                                       : 0u;
+};
 template <uint32_t F>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OCC(F)))) mrt_path_kernel(PathParams P) {
     constexpr uint32_t LK = PathLevLds<F>::K;
