@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--pipeline", type=int, default=2,
                     help="render contexts used round-robin on their own HIP streams: step i+1's launch "
                          "fills the CUs freed by step i's tail instead of waiting for it")
+    ap.add_argument("--verify", action="store_true",
+                    help="after timing, rank 0 checks the assembled framebuffer of the last step against a "
+                         "single-context full render, bit for bit")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_cornell_c2.json"))
     return ap.parse_args()
 
@@ -93,9 +96,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("MRT_SAME_GPU"):  # rehearsal hook: every rank on GPU 0 (one-GPU box)
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("MRT_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI; gloo: rehearsal hook
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -176,6 +185,19 @@ def main():
     nrays = int(total_rays.item())
     rays_per_step_local = int(rays.item()) // max(args.steps, 1)
 
+    verified = None
+    if args.verify and d_world == world and rank == 0:
+        img = tg.full.view(args.height, args.width, 4) if world > 1 else None
+        if world == 1:
+            full = np.zeros((args.width * args.height, 4), dtype=np.float32)
+            full[px] = outs[(it[0] - 1) % npipe].cpu().numpy()
+            img = full.reshape(args.height, args.width, 4)
+        ref, ref_rays = m.Renderer(scene, device=local).render(
+            m.render_desc(args.width, args.height, args.samples, depth=args.depth, tile_size=args.tile_size))
+        got = img[..., :3] if isinstance(img, np.ndarray) else img[..., :3].cpu().numpy()
+        verified = bool(np.array_equal(got.view(np.uint32), ref[..., :3].view(np.uint32))
+                        and nrays == ref_rays * args.steps)
+
     # dominant kernel: mrt_path_kernel, HIP events recorded on the launch stream (3 extra renders)
     kms = []
     for _ in range(max(args.kernel_reps, 1)):
@@ -223,6 +245,8 @@ def main():
             "roofline": roofline,
             "cpu_baseline": None,
         }
+        if verified is not None:
+            res["verify_bit_exact"] = verified
         if world == 1 and not args.no_cpu_baseline:
             try:
                 res["cpu_baseline"] = cpu_baseline(args)
