@@ -95,6 +95,9 @@ extern "C" int mrt_debug_phases(unsigned long long* out, int reset) {
 // fold levels kept in LDS per lane (the rest in HBM): where the LDS budget at the target
 // occupancy allows it
 // (Cornell: 2 at 6 WGs/CU; wide variants at 3 WGs/CU: MRT_LEVK_WIDE; room + mesh: MRT_LEVK_MESH)
+#ifndef MRT_LEVK_CORNELL
+#define MRT_LEVK_CORNELL 2u
+#endif
 #ifndef MRT_LEVK_WIDE
 #define MRT_LEVK_WIDE 4u
 #endif
@@ -102,7 +105,7 @@ extern "C" int mrt_debug_phases(unsigned long long* out, int reset) {
 #define MRT_LEVK_MESH 1u
 #endif
 template <uint32_t F> struct PathLevLds {
-    static constexpr uint32_t K = ((F & 0xFFFFu) == (FT_LIN | FT_INST)) ? 2u
+    static constexpr uint32_t K = ((F & 0xFFFFu) == (FT_LIN | FT_INST)) ? MRT_LEVK_CORNELL
                                   : PathOcc<F>::kWide                  ? MRT_LEVK_WIDE
                                   : ((F & FT_MESH) != 0)               ? MRT_LEVK_MESH
                                                                        : 0u;
