@@ -233,7 +233,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": "f32",
             "data": "synthetic scene (reference scene builder, deterministic seeds)",
             "config": {"workload": f"{WORKLOAD.get(args.scene, 'scene')}: scene {args.scene}, {args.width}x{args.height}, "
                                    f"{desc.sqrt_samples ** 2} spp, depth {args.depth}, draw() accumulation",
