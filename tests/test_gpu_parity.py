@@ -351,3 +351,17 @@ def test_concurrent_contexts_on_two_streams(gpu):
         assert np.array_equal(img.reshape(h, w, 4)[..., :3].view(np.uint32), ref[..., :3].view(np.uint32))
     for c in ctx:
         c.close()
+
+
+@pytest.mark.parametrize("sid", [5, 8, 9, 7])
+def test_gpu_within_tolerance_of_shipped_numerics(gpu, sid):
+    """GPU image vs the reference AS SHIPPED on the same per-path streams (shipped_stream_<sid>_small):
+    per-pixel RMSE < 1e-3 (north-star tolerance), channel means within 1e-4, ray totals within 1e-3."""
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", f"shipped_stream_{sid}_small.npz"))
+    _, w, h, spp, depth = (int(x) for x in g["meta"])
+    _, r = renderer(gpu, sid, w, h)
+    img, rays = r.render(gpu.render_desc(w, h, spp, depth=depth))
+    d = img[..., :3].astype(np.float64) - g["image"]
+    assert float(np.sqrt((d ** 2).mean())) < 1e-3
+    assert np.abs(d.reshape(-1, 3).mean(axis=0)).max() < 1e-4
+    assert abs(rays / float(g["rays"][0]) - 1) < 1e-3

@@ -14,7 +14,8 @@ Fixtures (all small; data only -- inputs and expected outputs):
   shipped_stream_5*.npz   stream-matched render by the reference AS SHIPPED (FMA contraction, glibc
                           libm): the tolerance fixture of the per-pixel RMSE < 1e-3 criterion
                           (SURVEY 8(d) parity 2).  Full C2 (500x500, 1024 spp): rows 200-299, 25x25
-                          block means, channel means, ray count; and 128x128 x 256 spp whole image.
+                          block means, channel means, ray count; and whole small images of scenes 5, 8, 9, 7
+                          (SHIPPED_SMALL).
                           `--only-shipped-stream` regenerates just these two.
 """
 import gzip
@@ -36,6 +37,8 @@ CWD = os.path.join(REF, "clang")  # the reference resolves ../obj and ../earthma
 # (scene id, width, height, samples, depth): small stream-matched cases per scene
 STREAM_CASES = [(0, 40, 20, 16, 8), (1, 40, 20, 9, 8), (2, 32, 16, 9, 8), (3, 32, 16, 9, 8), (4, 32, 16, 9, 8),
                 (5, 32, 32, 16, 32), (6, 32, 32, 9, 32), (7, 32, 32, 4, 32), (8, 32, 32, 9, 32), (9, 32, 32, 9, 32)]
+# shipped-numerics tolerance fixtures (stream-matched): Cornell, bunny, teapot-in-Cornell, book2
+SHIPPED_SMALL = [(5, 128, 128, 256), (8, 128, 128, 256), (9, 128, 128, 256), (7, 64, 64, 4096)]
 SCENE_SIZES = {0: (200, 100), 1: (200, 100), 2: (200, 100), 3: (200, 100), 4: (200, 100), 5: (500, 500),
                6: (500, 500), 7: (2048, 2048), 8: (1024, 1024), 9: (800, 800)}
 
@@ -81,11 +84,12 @@ def shipped_stream(tmp):
                         mean=im.reshape(-1, 3).mean(axis=0, dtype=np.float64), rays=np.array([meta["rays"]], dtype=np.int64),
                         meta=np.array([5, 500, 500, 1024, 32], dtype=np.int64))
     print("shipped stream C2", meta)
-    meta = json.loads(run(SHIPPED, ["--h-mode", "stream", "-width", 128, "-height", 128, "-samples", 256, "-depth", 32,
-                                    "--h-threads", 8, "--h-out", img, "-scene", 5]))
-    np.savez_compressed(os.path.join(OUT, "shipped_stream_5_small.npz"), image=read_pfm(img, 128, 128),
-                        rays=np.array([meta["rays"]], dtype=np.int64), meta=np.array([5, 128, 128, 256, 32], dtype=np.int64))
-    print("shipped stream small", meta)
+    for sid, w, h, spp in SHIPPED_SMALL:
+        meta = json.loads(run(SHIPPED, ["--h-mode", "stream", "-width", w, "-height", h, "-samples", spp, "-depth", 32,
+                                        "--h-threads", 8, "--h-out", img] + scene_args(sid)))
+        np.savez_compressed(os.path.join(OUT, f"shipped_stream_{sid}_small.npz"), image=read_pfm(img, w, h),
+                            rays=np.array([meta["rays"]], dtype=np.int64), meta=np.array([sid, w, h, spp, 32], dtype=np.int64))
+        print("shipped stream small", sid, meta)
 
 
 def main():
