@@ -48,6 +48,31 @@ struct BvhWide {
 };
 #define BVHW_LEAF 0x80000000u
 
+// A wide node (MeshWide / BvhWide: both children's boxes, refs, order, flags) fetched whole: four
+// 16-byte loads issued together, so one memory round trip per node visit.  (Read field by field,
+// the compiler split the node into dependent loads -- left box, right box, order, then the child
+// ref at a computed offset -- four round trips per visit.)
+struct WideNode {
+    f3 lmin, lmax, rmin, rmax;
+    uint32_t lref, rref, order, flags;
+};
+template <typename W>
+__device__ __forceinline__ WideNode load_wide(const W* p) {
+    static_assert(sizeof(W) == 64, "wide node is 64 B");
+    const float4* q = reinterpret_cast<const float4*>(p);
+    const float4 a = q[0], b = q[1], c = q[2], d = q[3];
+    WideNode n;
+    n.lmin = f3{a.x, a.y, a.z};
+    n.lref = __float_as_uint(a.w);
+    n.lmax = f3{b.x, b.y, b.z};
+    n.rref = __float_as_uint(b.w);
+    n.rmin = f3{c.x, c.y, c.z};
+    n.order = __float_as_uint(c.w);
+    n.rmax = f3{d.x, d.y, d.z};
+    n.flags = __float_as_uint(d.w);
+    return n;
+}
+
 // Device-side scene: the mrt_scene_view arrays resident in HBM.
 struct DScene {
     const mrt_node* __restrict__ nodes;
@@ -260,7 +285,7 @@ __device__ __forceinline__ bool mesh_hit(const DScene& S, const mrt_node& n, con
     // on the teapot (C3) than the one-step-per-iteration walk below, so kept as an experiment.
     for (;;) {
         while (!(ref & MESH_LEAF)) {
-            const MeshWide& W = S.mwide[ref];
+            const WideNode W = load_wide(S.mwide + ref);
             const bool hl = aabb_hit(W.lmin, W.lmax, r, tmin, tmax);
             const bool hr = aabb_hit(W.rmin, W.rmax, r, tmin, tmax);
             const bool left_first = (W.order & r.mask) != 0;
@@ -285,7 +310,7 @@ __device__ __forceinline__ bool mesh_hit(const DScene& S, const mrt_node& n, con
         if (ref & MESH_LEAF) {
             if (mesh_leaf(S, ref, n, r, tmin, tmax, rec, full)) return true;
         } else {
-            const MeshWide& W = S.mwide[ref];
+            const WideNode W = load_wide(S.mwide + ref);
             const bool hl = aabb_hit(W.lmin, W.lmax, r, tmin, tmax);
             const bool hr = aabb_hit(W.rmin, W.rmax, r, tmin, tmax);
             const bool left_first = (W.order & r.mask) != 0;
@@ -364,7 +389,7 @@ __device__ __forceinline__ bool bvhw_hit(const DScene& S, const mrt_node& n, con
     // visits the same nodes in the same order as the reference's recursion: results unchanged.
     for (;;) {
         while (!(ref & BVHW_LEAF)) {
-            const BvhWide& W = S.bwide[ref];
+            const WideNode W = load_wide(S.bwide + ref);
             const bool hl = !(W.flags & 1u) || aabb_hit(W.lmin, W.lmax, r, tmin, tmax);
             const bool hr = !(W.flags & 2u) || aabb_hit(W.rmin, W.rmax, r, tmin, tmax);
             const bool left_first = (W.order & r.mask) != 0;
@@ -389,7 +414,7 @@ __device__ __forceinline__ bool bvhw_hit(const DScene& S, const mrt_node& n, con
         if (ref & BVHW_LEAF) {
             if (bvhw_leaf<F>(S, ref & ~BVHW_LEAF, r, tmin, tmax, rec, full)) return true;
         } else {
-            const BvhWide& W = S.bwide[ref];
+            const WideNode W = load_wide(S.bwide + ref);
             const bool hl = !(W.flags & 1u) || aabb_hit(W.lmin, W.lmax, r, tmin, tmax);
             const bool hr = !(W.flags & 2u) || aabb_hit(W.rmin, W.rmax, r, tmin, tmax);
             const bool left_first = (W.order & r.mask) != 0;
