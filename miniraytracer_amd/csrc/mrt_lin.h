@@ -93,26 +93,35 @@ __device__ __forceinline__ bool lin_prim_t(const OP& o, const Ray& r, float tmin
     }
 }
 
-// the record the primitive's hit() writes for a hit at t.  The node is per lane: each field is
-// loaded where it is used so few registers are live at once.
+// the record the primitive's hit() writes for a hit at t.  The node is per lane; its 64 B are
+// fetched whole (four 16-byte loads in flight together) rather than field by field, which the
+// compiler turned into two dependent round trips (kind/mat, then the kind's fields).
 template <uint32_t F>
 __device__ __forceinline__ void lin_prim_rec(const DScene& S, uint32_t node, const Ray& r, float t, HitRec& rec) {
+#ifndef MRT_REC_FIELDWISE
+    const float4* q = reinterpret_cast<const float4*>(S.nodes + node);
+    const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+    const uint32_t code = __float_as_uint(q0.x), nmat = __float_as_uint(q0.w);
+    const float nf[12] = {q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+#else
     const mrt_node* n = S.nodes + node;
-    const uint32_t code = n->kind;
+    const uint32_t code = n->kind, nmat = n->mat;
+    const float* nf = n->f;
+#endif
     const uint32_t kind = code & 0xFFu;
     const bool needuv = (F & FT_UV) && ((code >> 16) & MRT_F_NEEDUV);
     rec.t = t;
-    rec.mat = n->mat;
+    rec.mat = nmat;
     rec.p = eval(r, t);
     if (kind == MRT_K_SPHERE) {
-        f3 cen = f3{n->f[0], n->f[1], n->f[2]};
+        f3 cen = f3{nf[0], nf[1], nf[2]};
         if ((F & FT_MOVING) && ((code >> 16) & MRT_F_MOVING))
-            cen = add(cen, fmul((r.time - n->f[6]) / (n->f[7] - n->f[6]), sub(f3{n->f[3], n->f[4], n->f[5]}, cen)));
-        rec.n = divf(sub(rec.p, cen), n->f[8]);
+            cen = add(cen, fmul((r.time - nf[6]) / (nf[7] - nf[6]), sub(f3{nf[3], nf[4], nf[5]}, cen)));
+        rec.n = divf(sub(rec.p, cen), nf[8]);
         if (needuv) sphere_uv(rec.n, &rec.u, &rec.v);
         return;
     }
-    const float ns = n->f[5];
+    const float ns = nf[5];
     float pb, pc;
     if (kind == MRT_K_XY) {
         rec.n = f3{0, 0, ns};
@@ -125,8 +134,8 @@ __device__ __forceinline__ void lin_prim_rec(const DScene& S, uint32_t node, con
         if (needuv) { pb = r.o.y + t * r.d.y; pc = r.o.z + t * r.d.z; }
     }
     if (needuv) {
-        rec.u = (pb - n->f[0]) / (n->f[1] - n->f[0]);
-        rec.v = (pc - n->f[2]) / (n->f[3] - n->f[2]);
+        rec.u = (pb - nf[0]) / (nf[1] - nf[0]);
+        rec.v = (pc - nf[2]) / (nf[3] - nf[2]);
     }
 }
 
@@ -207,7 +216,7 @@ __device__ __forceinline__ bool scene_hit_lin(const DScene& S, Ray& r, float tmi
             hinst = h ? inst : hinst;
             hdone = h ? false : hdone;
         } else if ((F & FT_MESH) && op == LOP_MESH) {
-            if (on && mesh_hit(S, S.nodes[o.node], cur, tmin, closest, rec, true, L)) {
+            if (on && mesh_hit<true>(S, ld_node(const_ptr(S.nodes) + o.node), cur, tmin, closest, rec, true, L)) {
                 closest = rec.t;
                 hnode = o.node;
                 hinst = inst;

@@ -113,16 +113,6 @@ __device__ __forceinline__ float leaf_pdf_value(const DScene& S, const mrt_node&
     }
     return 0;
 }
-// a node record read through the constant address space (scalar loads at a uniform address)
-__device__ __forceinline__ mrt_node ld_node(const MRT_CONST_AS mrt_node* p) {
-    mrt_node n;
-    n.kind = p->kind;
-    n.a = p->a;
-    n.b = p->b;
-    n.mat = p->mat;
-    for (int k = 0; k < 12; k++) n.f[k] = p->f[k];
-    return n;
-}
 
 // object_list::pdf_value over the biased list (scene_object.h:64-70): the leaves are read through
 // the constant address space (uniform index: scalar loads, no node -> children -> node chain)

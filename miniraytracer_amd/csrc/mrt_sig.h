@@ -86,7 +86,7 @@ struct SigWalk {
                 w.hdone = h ? false : w.hdone;
                 run<PC + 1, END>(S, prog, tmin, w, on, rec, L);
             } else if constexpr (op == LOP_MESH) {
-                if (on && mesh_hit(S, S.nodes[o.node], w.cur, tmin, w.closest, rec, true, L)) {
+                if (on && mesh_hit<true>(S, ld_node(const_ptr(S.nodes) + o.node), w.cur, tmin, w.closest, rec, true, L)) {
                     w.closest = rec.t;
                     w.hnode = o.node;
                     w.hinst = cur_inst<PC>();

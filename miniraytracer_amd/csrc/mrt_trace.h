@@ -73,6 +73,17 @@ __device__ __forceinline__ WideNode load_wide(const W* p) {
     return n;
 }
 
+// a node record read through the constant address space (scalar loads at a uniform address)
+__device__ __forceinline__ mrt_node ld_node(const MRT_CONST_AS mrt_node* p) {
+    mrt_node n;
+    n.kind = p->kind;
+    n.a = p->a;
+    n.b = p->b;
+    n.mat = p->mat;
+    for (int k = 0; k < 12; k++) n.f[k] = p->f[k];
+    return n;
+}
+
 // Device-side scene: the mrt_scene_view arrays resident in HBM.
 struct DScene {
     const mrt_node* __restrict__ nodes;
@@ -218,6 +229,11 @@ __device__ __forceinline__ bool rect_hit(const mrt_node& n, const Ray& r, float 
 __device__ __forceinline__ bool tri_hit(const DScene& S, uint32_t i, const Ray& r, float tmin, float tmax, float* tout, float* uout, float* vout) {
     const float4* g = S.tri_geo + (size_t)i * 3;
     f3 m = ld3(g[0]), u = ld3(g[1]), v = ld3(g[2]);
+#if defined(__HIP_DEVICE_COMPILE__)
+    // the three rows in one round trip: otherwise m's load sinks below the det test and becomes a
+    // second dependent fetch for every triangle that passes it
+    asm volatile("" ::"v"(m.x), "v"(m.y), "v"(m.z));
+#endif
     f3 pvec = cross(r.d, v);
     float det = dot(u, pvec);
     float sign = 1.0f;
@@ -275,10 +291,18 @@ __device__ __forceinline__ bool mesh_leaf(const DScene& S, uint32_t ref, const m
     }
     return has;
 }
+// UNIFORM: the mesh node is the same for the whole wave (linear programs): the root box is read
+// through the constant address space (scalar loads) instead of by a per-lane load chain.
+template <bool UNIFORM = false>
 __device__ __forceinline__ bool mesh_hit(const DScene& S, const mrt_node& n, const Ray& r, float tmin, float tmax, HitRec& rec, bool full,
                                          const LStack& L) {
-    const mrt_mesh_node& root = S.mnodes[n.a];
-    if (!aabb_hit(root.bmin, root.bmax, r, tmin, tmax)) return false;
+    if constexpr (UNIFORM) {
+        const MRT_CONST_AS mrt_mesh_node& root = const_ptr(S.mnodes)[n.a];
+        if (!aabb_hit(f3{root.bmin[0], root.bmin[1], root.bmin[2]}, f3{root.bmax[0], root.bmax[1], root.bmax[2]}, r, tmin, tmax)) return false;
+    } else {
+        const mrt_mesh_node& root = S.mnodes[n.a];
+        if (!aabb_hit(root.bmin, root.bmax, r, tmin, tmax)) return false;
+    }
     uint32_t ref = n.b, msp = 0;
 #ifdef MRT_MESH_WW
     // "while-while" (Aila & Laine 2009), as bvhw_hit: measured 20% slower on the bunny (C4) and 1%
