@@ -11,6 +11,7 @@
 //   mrt_final_kernel  mode 0: color /= ns, luminance clamp (main.cpp:168-173); writes the float4
 //                     output in local-pixel order.
 #include <hip/hip_runtime.h>
+#include <atomic>
 
 #include <algorithm>
 #include <functional>
@@ -49,6 +50,7 @@ struct PathParams {
     float* __restrict__ rad;              // n_paths * 3 floats, [s - s0][lp]
     uint32_t* __restrict__ path_rays;     // optional (debug): n_paths
     unsigned long long* __restrict__ counter;  // work counter (paths handed out)
+    unsigned long long* hprog;            // host-coherent pinned snapshot of `counter` (mrt_progress), or null
     const int* cancel;                    // device flag: non-zero makes the launch exit (G_isRunning)
     unsigned long long* __restrict__ rays;
     float4* __restrict__ lev;             // fold levels, lane-major: [slot][lev_rows]
@@ -151,7 +153,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
             const uint32_t batch = pool_end + P.tail_zone >= P.n_paths ? MRT_TAIL_BATCH : MRT_BATCH;
             uint64_t nb = 0;
             if (have < c) {
-                if (lane == 0) nb = atomicAdd(P.counter, (unsigned long long)batch);
+                if (lane == 0) {
+                    nb = atomicAdd(P.counter, (unsigned long long)batch);
+                    // every 32nd claim: a system-scope store to host memory, read by mrt_progress
+                    // without any GPU queue (a device-to-host copy could wait behind this launch)
+                    if (P.hprog && ((nb / MRT_BATCH) & 31u) == 0)
+                        __hip_atomic_store(P.hprog, nb + batch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
                 nb = __shfl(nb, 0);
             }
             PH_MARK(ph, 0);
@@ -396,8 +404,14 @@ struct mrt_scene {
     size_t cnt_cap = 0;
     std::vector<uint64_t> chunk_paths;
     hipStream_t pstream = nullptr;   // non-blocking stream for progress reads
+    // host-coherent pinned memory: per-launch snapshots of the work counters, stored by the path
+    // kernel itself (mrt_progress reads them with no GPU work), and the cancel flag's source
+    uint64_t* h_prog = nullptr;
+    size_t h_prog_cap = 0;
+    std::vector<uint64_t> h_seen;  // largest snapshot read per launch (waves store out of order)
+    int* h_one = nullptr;
     hipEvent_t ev_reset = nullptr;   // recorded once this render's counters are zeroed
-    uint32_t n_chunks = 0;           // launches of the current render
+    std::atomic<uint32_t> n_chunks{0};  // launches of the current render (0 until all are enqueued)
     unsigned long long* d_rays = nullptr;
     int grid = 0;
     uint32_t features = 0, variant = 0;
@@ -863,6 +877,8 @@ extern "C" void mrt_scene_free(mrt_scene* s) {
     for (void* p : s->allocs) (void)hipFree(p);
     for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
     if (s->pstream) (void)hipStreamDestroy(s->pstream);
+    if (s->h_prog) (void)hipHostFree(s->h_prog);
+    if (s->h_one) (void)hipHostFree(s->h_one);
     if (s->ev_reset) (void)hipEventDestroy(s->ev_reset);
     for (void* p : {(void*)s->d_counters, (void*)s->d_pixels, (void*)s->d_sdist, (void*)s->d_rad, (void*)s->d_path_rays, (void*)s->d_acc, (void*)s->d_lev})
         if (p) (void)hipFree(p);
@@ -932,6 +948,18 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
     uint32_t launches = (ns + s->chunk - 1) / s->chunk;
     if ((st = grow((void**)&s->d_counters, &s->cnt_cap, (size_t)launches * 8))) return st;
     if (!s->pstream) HIPCHK(hipStreamCreateWithFlags(&s->pstream, hipStreamNonBlocking));
+    if (s->h_prog_cap < (size_t)launches) {
+        if (s->h_prog) (void)hipHostFree(s->h_prog);
+        s->h_prog = nullptr;
+        s->h_prog_cap = 0;
+        HIPCHK(hipHostMalloc((void**)&s->h_prog, (size_t)launches * 8, hipHostMallocPortable | hipHostMallocCoherent));
+        s->h_prog_cap = launches;
+    }
+    if (s->h_seen.size() < (size_t)launches) s->h_seen.resize(launches, 0);
+    if (!s->h_one) {
+        HIPCHK(hipHostMalloc((void**)&s->h_one, sizeof(int), hipHostMallocPortable));
+        *s->h_one = 1;
+    }
     if (!s->ev_reset) HIPCHK(hipEventCreateWithFlags(&s->ev_reset, hipEventDisableTiming));
     if (s->chunk_paths.size() < launches) s->chunk_paths.resize(launches, 0);
     while (s->ev.size() < 2 * (size_t)launches) {
@@ -955,8 +983,11 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
     HIPCHK(hipMemsetAsync(s->d_counters, 0, (size_t)launches * 8, q));
     HIPCHK(hipMemsetAsync(s->d_counter + 4, 0, 8, q));  // cancel flag
     HIPCHK(hipEventRecord(s->ev_reset, q));
-    for (uint32_t k = 0; k < launches; k++) s->chunk_paths[k] = (uint64_t)s->npix * (std::min(ns, (k + 1) * s->chunk) - k * s->chunk);
-    s->n_chunks = launches;
+    for (uint32_t k = 0; k < launches; k++) {
+        s->chunk_paths[k] = (uint64_t)s->npix * (std::min(ns, (k + 1) * s->chunk) - k * s->chunk);
+        __atomic_store_n(&s->h_prog[k], (uint64_t)0, __ATOMIC_RELAXED);
+        __atomic_store_n(&s->h_seen[k], (uint64_t)0, __ATOMIC_RELAXED);
+    }
     s->n_launch = 0;
     for (uint32_t s0 = 0; s0 < ns; s0 += s->chunk) {
         uint32_t s1 = std::min(ns, s0 + s->chunk);
@@ -985,6 +1016,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.rad = s->d_rad;
         P.path_rays = (d->flags & MRT_RF_PATH_DEBUG) ? s->d_path_rays : nullptr;
         P.counter = (unsigned long long*)(s->d_counters + s->n_launch);
+        P.hprog = (unsigned long long*)(s->h_prog + s->n_launch);
         P.cancel = (const int*)(s->d_counter + 4);
         P.rays = d_rays ? (unsigned long long*)d_rays : s->d_rays;
         P.lev = s->d_lev;
@@ -999,6 +1031,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         HIPCHK(hipGetLastError());
         s->last_paths = P.n_paths;
     }
+    s->n_chunks = launches;  // progress reads start once every launch and its events are enqueued
     uint32_t blocks = (s->npix + 255) / 256;
     hipLaunchKernelGGL(mrt_final_kernel, dim3(blocks), dim3(256), 0, q, s->d_acc, (float4*)d_local, s->npix, ns, d->mode, d->max_luminance);
     HIPCHK(hipGetLastError());
@@ -1033,8 +1066,7 @@ extern "C" mrt_status mrt_render(mrt_scene* s, const mrt_render_desc* d, float* 
             return mrt_internal_fail(MRT_ERR_HIP, hipGetErrorString(q));
         }
         if (cancel && *cancel && !cancelled) {
-            static const int one = 1;
-            HIPCHK(hipMemcpyAsync(s->d_counter + 4, &one, sizeof(int), hipMemcpyHostToDevice, s->pstream));
+            HIPCHK(hipMemcpyAsync(s->d_counter + 4, s->h_one, sizeof(int), hipMemcpyHostToDevice, s->pstream));
             HIPCHK(hipStreamSynchronize(s->pstream));
             cancelled = true;
         }
@@ -1063,20 +1095,26 @@ extern "C" mrt_status mrt_render_debug(mrt_scene* s, float* path_rgb, uint32_t* 
 }
 
 // work_queue::getPercentDone (work_queue.cpp:142-175): paths handed out over all paths of the
-// render.  Reads the per-launch counters on a non-blocking stream, so it can be called from
-// another host thread while the render runs.
+// render, callable from another host thread while the render runs.  Needs no GPU work: a finished
+// launch counts whole (its stop event), a running one by the snapshot of its work counter that
+// the path kernel stores into host memory, a launch not yet started as 0.
 extern "C" mrt_status mrt_progress(mrt_scene* s, float* pct) {
     if (!s || !pct) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_progress: null");
     *pct = 0.0f;
     const size_t n = s->n_chunks;
-    if (n == 0 || !s->pstream || hipEventQuery(s->ev_reset) != hipSuccess) return MRT_OK;  // not started
-    std::vector<uint64_t> c(n);
-    HIPCHK(hipMemcpyAsync(c.data(), s->d_counters, n * 8, hipMemcpyDeviceToHost, s->pstream));
-    HIPCHK(hipStreamSynchronize(s->pstream));
+    if (n == 0 || !s->h_prog || s->h_prog_cap < n || s->ev.size() < 2 * n || s->h_seen.size() < n) return MRT_OK;  // not started
     double done = 0, total = 0;
     for (size_t k = 0; k < n; k++) {
-        done += (double)std::min<uint64_t>(c[k], s->chunk_paths[k]);
         total += (double)s->chunk_paths[k];
+        if (hipEventQuery(s->ev[2 * k + 1]) == hipSuccess) {
+            done += (double)s->chunk_paths[k];
+        } else if (hipEventQuery(s->ev[2 * k]) == hipSuccess) {
+            // snapshots from different waves land out of order: report the largest seen so far
+            uint64_t c = __atomic_load_n(&s->h_prog[k], __ATOMIC_RELAXED);
+            c = std::max(c, __atomic_load_n(&s->h_seen[k], __ATOMIC_RELAXED));
+            __atomic_store_n(&s->h_seen[k], c, __ATOMIC_RELAXED);
+            done += (double)std::min<uint64_t>(c, s->chunk_paths[k]);
+        }
     }
     *pct = total > 0 ? (float)std::min(100.0, done * 100.0 / total) : 0.0f;
     return MRT_OK;

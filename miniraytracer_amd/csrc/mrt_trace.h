@@ -84,6 +84,21 @@ __device__ __forceinline__ mrt_node ld_node(const MRT_CONST_AS mrt_node* p) {
     return n;
 }
 
+// a per-lane node record fetched whole (four 16-byte loads in flight together)
+__device__ __forceinline__ mrt_node ld_node_v(const mrt_node* p) {
+    const float4* q = reinterpret_cast<const float4*>(p);
+    const float4 a = q[0], b = q[1], c = q[2], d = q[3];
+    mrt_node n;
+    n.kind = __float_as_uint(a.x);
+    n.a = __float_as_uint(a.y);
+    n.b = __float_as_uint(a.z);
+    n.mat = __float_as_uint(a.w);
+    n.f[0] = b.x; n.f[1] = b.y; n.f[2] = b.z; n.f[3] = b.w;
+    n.f[4] = c.x; n.f[5] = c.y; n.f[6] = c.z; n.f[7] = c.w;
+    n.f[8] = d.x; n.f[9] = d.y; n.f[10] = d.z; n.f[11] = d.w;
+    return n;
+}
+
 // Device-side scene: the mrt_scene_view arrays resident in HBM.
 struct DScene {
     const mrt_node* __restrict__ nodes;
@@ -371,18 +386,18 @@ __device__ __forceinline__ bool leaf_prim_hit(const mrt_node& n, uint32_t kind, 
 // the running closest narrowing across children (scene_object.h:79-103)
 template <uint32_t F>
 __device__ __forceinline__ bool bvhw_leaf(const DScene& S, uint32_t node, const Ray& r, float tmin, float tmax, HitRec& rec, bool full) {
-    const mrt_node& n = S.nodes[node];
+    const mrt_node n = ld_node_v(S.nodes + node);
     const uint32_t k = MRT_NODE_KIND(n);
     if (k != MRT_K_LIST) return leaf_prim_hit<F>(n, k, r, tmin, tmax, rec, full);
     float closest = tmax;
     bool hit = false;
     for (uint32_t i = 0; i < n.b; i++) {
-        const mrt_node& c = S.nodes[S.children[n.a + i]];
+        const mrt_node c = ld_node_v(S.nodes + S.children[n.a + i]);
         const uint32_t ck = MRT_NODE_KIND(c);
         if (ck == MRT_K_LIST) {
             if ((MRT_NODE_FLAGS(c) & MRT_F_HASBOX) && !aabb_hit(c.f, c.f + 3, r, tmin, closest)) continue;
             for (uint32_t j = 0; j < c.b; j++) {
-                const mrt_node& g = S.nodes[S.children[c.a + j]];
+                const mrt_node g = ld_node_v(S.nodes + S.children[c.a + j]);
                 if (leaf_prim_hit<F>(g, MRT_NODE_KIND(g), r, tmin, closest, rec, full)) {
                     hit = true;
                     closest = rec.t;
