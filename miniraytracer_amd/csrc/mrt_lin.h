@@ -160,6 +160,35 @@ __device__ __forceinline__ Ray lin_load_ray(const LStack& L) {
     r.inv = ray_inv(r.d, r.nice);
     return r;
 }
+// An op's 64 B as one batch of scalar loads with a single wait: the asm makes every word live at
+// one point, so the loads cannot be sunk to their uses (the compiler otherwise split each op into
+// three load + s_waitcnt round trips to the scalar cache).
+template <uint32_t F, uint32_t KIND>
+__device__ __forceinline__ LinOp lin_fetch_op(const MRT_CONST_AS LinOp& o) {
+    const MRT_CONST_AS uint32_t* q = reinterpret_cast<const MRT_CONST_AS uint32_t*>(&o);
+    LinOp r;
+    r.code = q[0];
+    r.node = q[1];
+    r.skip = 0;
+    r.mat = 0;
+    if constexpr (KIND == MRT_K_SPHERE) {  // centre, radius (+ the moving centre's fields)
+        uint32_t c0 = q[4], c1 = q[5], c2 = q[6], rad = q[12];
+#if defined(__HIP_DEVICE_COMPILE__)
+        asm volatile("" : "+s"(r.code), "+s"(r.node), "+s"(c0), "+s"(c1), "+s"(c2), "+s"(rad));
+#endif
+        r.f[0] = __uint_as_float(c0); r.f[1] = __uint_as_float(c1); r.f[2] = __uint_as_float(c2); r.f[8] = __uint_as_float(rad);
+        if (F & FT_MOVING)
+            for (int k = 3; k < 8; k++) r.f[k] = o.f[k];
+    } else {  // rect: bounds, plane, normal sign
+        uint32_t b0 = q[4], b1 = q[5], b2 = q[6], b3 = q[7], k = q[8], ns = q[9];
+#if defined(__HIP_DEVICE_COMPILE__)
+        asm volatile("" : "+s"(r.code), "+s"(r.node), "+s"(b0), "+s"(b1), "+s"(b2), "+s"(b3), "+s"(k), "+s"(ns));
+#endif
+        r.f[0] = __uint_as_float(b0); r.f[1] = __uint_as_float(b1); r.f[2] = __uint_as_float(b2); r.f[3] = __uint_as_float(b3);
+        r.f[4] = __uint_as_float(k); r.f[5] = __uint_as_float(ns);
+    }
+    return r;
+}
 // aabb::hit (invDir = 1/dir of the ray, aabb.h:49)
 __device__ __forceinline__ bool lin_box(const MRT_CONST_AS LinOp& o, const Ray& r, float tmin, float tmax) {
     const float b[6] = {o.f[0], o.f[1], o.f[2], o.f[3], o.f[4], o.f[5]};

@@ -79,9 +79,20 @@ struct SigWalk {
             const MRT_CONST_AS LinOp& o = prog[PC];
             if constexpr (op == LOP_PRIM) {
                 float t;
-                const bool h = lin_prim_t<F, kind>(o, w.cur, tmin, w.closest, &t) & on;
+                bool h;
+                uint32_t node;
+                if constexpr (SIG == SIG_ROOM_MESH) {
+                    // each op's words by one batch of scalar loads (+2% on the mesh scenes; -2% on
+                    // the Cornell box, whose walk is short of SGPRs: there the loads stay lazy)
+                    const LinOp ov = lin_fetch_op<F, kind>(o);
+                    h = lin_prim_t<F, kind>(ov, w.cur, tmin, w.closest, &t) & on;
+                    node = ov.node;
+                } else {
+                    h = lin_prim_t<F, kind>(o, w.cur, tmin, w.closest, &t) & on;
+                    node = o.node;
+                }
                 w.closest = h ? t : w.closest;
-                w.hnode = h ? o.node : w.hnode;  // the op's node (scalar operand): no per-lane lookup later
+                w.hnode = h ? node : w.hnode;  // the op's node (scalar operand): no per-lane lookup later
                 w.hinst = h ? cur_inst<PC>() : w.hinst;
                 w.hdone = h ? false : w.hdone;
                 run<PC + 1, END>(S, prog, tmin, w, on, rec, L);
