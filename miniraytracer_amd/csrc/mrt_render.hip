@@ -68,12 +68,15 @@ struct PathParams {
 // variant on MI355X (DESIGN.md "Occupancy").
 // (compact variants -- Cornell, Cornell room + mesh, plain interpreter -- reach 80 VGPRs without
 // spills at 6; the wide-feature variants spill there and run best at 3 waves, 168 VGPRs)
+#ifndef MRT_WPE_WIDE
+#define MRT_WPE_WIDE 3
+#endif
 #ifndef MRT_WPE_MESH
 #define MRT_WPE_MESH 6
 #endif
 template <uint32_t F> struct PathOcc {
     static constexpr bool kWide = (F & (FT_BVHW | FT_TEX | FT_VOLUME)) != 0 || !(F & FT_LIN);
-    static constexpr int W = kWide ? 3 : ((F & FT_MESH) != 0 ? MRT_WPE_MESH : 6);
+    static constexpr int W = kWide ? MRT_WPE_WIDE : ((F & FT_MESH) != 0 ? MRT_WPE_MESH : 6);
 };
 #ifndef MRT_BATCH
 #define MRT_BATCH 256u  // paths a wave claims per atomic on the work counter (one hot address)
