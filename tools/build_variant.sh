@@ -1,7 +1,7 @@
 #!/bin/bash
 # Experiment builds: exp/libmrt_<tag>.so from the current sources with extra device defines.
 #   tools/build_variant.sh <tag> "<extra hipcc flags>"
-# (exp/ is git-ignored; it travels to the GPU box for A/B runs with tools/_cmp.sh)
+# (exp/ is git-ignored; it travels to the GPU box for A/B runs with tools/_ab.sh / tools/_abs.sh)
 set -e
 cd "$(dirname "$0")/.."
 tag=$1; shift
