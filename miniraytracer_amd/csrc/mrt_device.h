@@ -184,6 +184,22 @@ __device__ __forceinline__ f3 random_cosine_direction(Pcg& r) {
     sincos_(phi, &sp, &cp);
     return f3{(cp * 2) * s2, (sp * 2) * s2, z};
 }
+__device__ __forceinline__ f3 random_cosine_direction_pre(float r1, float r2) {  // r1, r2: its two draws
+    float z = sqrt_core(1 - r2);
+    float phi = (2 * PI_F) * r1;
+    float s2 = sqrt_core(r2);
+    float sp, cp;
+    sincos_(phi, &sp, &cp);
+    return f3{(cp * 2) * s2, (sp * 2) * s2, z};
+}
+__device__ __forceinline__ f3 random_towards_sphere_pre(float r1, float r2, float radius, float dist_sq) {
+    float z = 1 + r2 * (sqrt_(1 - (radius * radius) / dist_sq) - 1);
+    float phi = (2 * PI_F) * r1;
+    float q = sqrt_(1 - z * z);
+    float sp, cp;
+    sincos_(phi, &sp, &cp);
+    return f3{cp * q, sp * q, z};
+}
 __device__ __forceinline__ f3 random_towards_sphere(Pcg& r, float radius, float dist_sq) {
     float r1 = randf(r), r2 = randf(r);
     float z = 1 + r2 * (sqrt_(1 - (radius * radius) / dist_sq) - 1);

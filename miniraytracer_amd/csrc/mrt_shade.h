@@ -85,6 +85,19 @@ __device__ __forceinline__ f3 onb_apply(f3 w, f3 vec) {
     return add(add(fmul(vec.x, u), fmul(vec.y, v)), fmul(vec.z, w));
 }
 
+// The next randf() values of a path's stream, two of them drawn ahead: every direction generator
+// of the lambertian mix starts with two draws, so they are drawn once before the light/surface
+// branch instead of inside both sides (same values, same stream order).
+struct Draws {
+    float v0, v1;
+    uint32_t used;
+    __device__ __forceinline__ float next(Pcg& rng) {
+        if (used == 0) { used = 1; return v0; }
+        if (used == 1) { used = 2; return v1; }
+        return randf(rng);
+    }
+};
+
 // biased object pdfs: object_list / xz_rect / sphere pdf_value & pdf_generate
 // (scene_object.h:64-77, rect.cpp:92-107, sphere.cpp:63-78, scene_object.h:24-29)
 template <uint32_t F>
@@ -131,12 +144,12 @@ __device__ __forceinline__ float biased_pdf_value(const DScene& S, f3 origin, f3
     return sum / (float)S.nbleaf;
 }
 template <uint32_t F>
-__device__ __forceinline__ f3 leaf_pdf_generate(const DScene& S, const mrt_node& n, f3 origin, float time, Pcg& rng) {
+__device__ __forceinline__ f3 leaf_pdf_generate(const DScene& S, const mrt_node& n, f3 origin, float time, Pcg& rng, Draws& dr) {
     uint32_t k = MRT_NODE_KIND(n);
     if (k == MRT_K_XZ) {
-        float a = randf(rng);
+        float a = dr.next(rng);
         float x = n.f[0] + a * (n.f[1] - n.f[0]);
-        float b = randf(rng);
+        float b = dr.next(rng);
         float z = n.f[2] + b * (n.f[3] - n.f[2]);
         return sub(f3{x, n.f[4], z}, origin);
     }
@@ -144,22 +157,23 @@ __device__ __forceinline__ f3 leaf_pdf_generate(const DScene& S, const mrt_node&
         f3 dir = sub(sphere_center<F>(n, time), origin);
         float dist_sq = sdot(dir);
         f3 w = normalize(dir);
-        return onb_apply(w, random_towards_sphere(rng, n.f[8], dist_sq));
+        const float r1 = dr.next(rng), r2 = dr.next(rng);
+        return onb_apply(w, random_towards_sphere_pre(r1, r2, n.f[8], dist_sq));
     }
     return f3{1, 0, 0};
 }
 template <uint32_t F>
-__device__ __forceinline__ f3 biased_pdf_generate(const DScene& S, f3 origin, float time, Pcg& rng) {
+__device__ __forceinline__ f3 biased_pdf_generate(const DScene& S, f3 origin, float time, Pcg& rng, Draws& dr) {
     if (!S.blist) {
         const mrt_node n = ld_node(const_ptr(S.bleaf));
-        return leaf_pdf_generate<F>(S, n, origin, time, rng);
+        return leaf_pdf_generate<F>(S, n, origin, time, rng, dr);
     }
-    const int i = int(randf(rng) * (float)S.nbleaf);  // object_list::pdf_generate (scene_object.h:72-77)
+    const int i = int(dr.next(rng) * (float)S.nbleaf);  // object_list::pdf_generate (scene_object.h:72-77)
     if (S.nbleaf == 1) {
         const mrt_node n = ld_node(const_ptr(S.bleaf));
-        return leaf_pdf_generate<F>(S, n, origin, time, rng);
+        return leaf_pdf_generate<F>(S, n, origin, time, rng, dr);
     }
-    return leaf_pdf_generate<F>(S, S.bleaf[i], origin, time, rng);
+    return leaf_pdf_generate<F>(S, S.bleaf[i], origin, time, rng, dr);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -305,12 +319,16 @@ __device__ __forceinline__ bool trace_segment(const DScene& S, PathState& ps, ui
     const bool lamb = !(F & FT_ISO) || M.kind == MRT_M_LAMBERTIAN;
     const f3 att = mat_color<F>(S, M, rec);
     f3 gen;
-    bool surface = true;
-    if (S.biased != MRT_NONE && randf(ps.rng) < 0.5f) {
-        gen = biased_pdf_generate<F>(S, rec.p, r.time, ps.rng);
-        surface = false;
+    const bool light = S.biased != MRT_NONE && randf(ps.rng) < 0.5f;
+    // both sides of the mix start with two draws when the surface side is cosine sampling
+    Draws dr{0.0f, 0.0f, 2u};
+    if (lamb) {
+        dr.v0 = randf(ps.rng);
+        dr.v1 = randf(ps.rng);
+        dr.used = 0;
     }
-    if (surface) gen = lamb ? onb_apply(rec.n, random_cosine_direction(ps.rng)) : random_in_sphere(ps.rng);
+    if (light) gen = biased_pdf_generate<F>(S, rec.p, r.time, ps.rng, dr);
+    else gen = lamb ? onb_apply(rec.n, random_cosine_direction_pre(dr.v0, dr.v1)) : random_in_sphere(ps.rng);
     PH_MARK(ph, 6);
     const Ray sc = make_ray(rec.p, gen, r.time, 0);
     float sval, spdf;
