@@ -147,6 +147,108 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
 #ifdef MRT_PHASES
     ph.t = __builtin_amdgcn_s_memtime();
 #endif
+    // mesh variants keep one constructor per branch: the shared-constructor loop spills there
+    // (bunny -4%, teapot -5%; Cornell +1.8%, book2 0)
+    constexpr bool kShared = (F & FT_MESH) == 0;
+    if constexpr (kShared) {
+    // One iteration: (1) every lane with a ray traces one segment; a path that ends is folded and
+    // stored; (2) lanes without a path take new ones (camera ray arguments); (3) ONE make_ray for
+    // every lane with a next ray -- camera and scattered rays alike, instead of one constructor per
+    // branch at partial lane occupancy; (4) diffuse scatters finish their pdfs on the new ray.
+    PendRay pr;
+    for (;;) {
+        bool want_ray = false;
+        if (active) {
+            f3 L;
+            const bool ended = trace_split<F, LK>(S, ps, P.max_bounces, lev, Ls, &L, &pr, ph);
+            PH_MARK(ph, 2);
+            if (ended) {
+                L = fold_levels(lev, ps.nlev, L);
+                PH_MARK(ph, 5);
+                float* dst = P.rad + (size_t)idx * 3;
+                dst[0] = L.x;
+                dst[1] = L.y;
+                dst[2] = L.z;
+                if (P.path_rays) P.path_rays[idx] = ps.rays;
+                done_rays += ps.rays;
+                active = false;
+            } else {
+                want_ray = true;
+            }
+        }
+        PH_MARK(ph, 3);
+        const uint64_t need = __ballot(!active);
+        if (need && !exhausted) {
+            const uint32_t c = (uint32_t)__popcll(need);
+            const uint32_t have = (uint32_t)(pool_end - pool_next);
+            // near the end of the launch, claims shrink so the last ones finish together
+            const uint32_t batch = pool_end + P.tail_zone >= P.n_paths ? MRT_TAIL_BATCH : MRT_BATCH;
+            uint64_t nb = 0;
+            if (have < c) {
+                if (lane == 0) {
+                    nb = atomicAdd(P.counter, (unsigned long long)batch);
+                    // every 32nd claim: a system-scope store to host memory, read by mrt_progress
+                    // without any GPU queue (a device-to-host copy could wait behind this launch)
+                    if (P.hprog && ((nb / MRT_BATCH) & 31u) == 0)
+                        __hip_atomic_store(P.hprog, nb + batch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+                nb = __shfl(nb, 0);
+            }
+            PH_MARK(ph, 0);
+            if (!active) {
+                const uint32_t rank = (uint32_t)__popcll(need & lt_mask);
+                const uint64_t i = rank < have ? pool_next + rank : nb + (rank - have);
+                if (i < P.n_paths) {
+                    idx = (uint32_t)i;
+                    // idx = sl * npix + lp; the double estimate is off by at most one either way
+                    uint32_t sl = (uint32_t)((double)idx * P.inv_npix);
+                    uint32_t lp = idx - sl * P.npix;
+                    if ((int32_t)lp < 0) { sl--; lp += P.npix; }
+                    if (lp >= P.npix) { sl++; lp -= P.npix; }
+                    const uint32_t s = P.s0 + sl;
+                    const uint2 xy = P.pixels[lp];
+                    const uint32_t x = xy.x, y = xy.y;
+                    const uint32_t pix = x + y * P.width;
+                    const float2 dd = P.sdist[s];  // ((i + 0.5) / sq, (j + 0.5) / sq), s = i*sq + j
+                    // (x + dx) / W with RN(1/W) from the host: numerator >= 1/(2 sq) >= 2^-17, W <= 2^24
+                    const float nu = (float)x + dd.x, nv = (float)y + dd.y;
+                    float u = div_core(nu, (float)P.width, P.inv_w), v = div_core(nv, (float)P.height, P.inv_h);
+                    if (!P.fast_uv) {  // a real (uniform) branch: the barrier keeps it from being if-converted
+                        asm volatile("" ::: "memory");
+                        u = nu / (float)P.width;
+                        v = nv / (float)P.height;
+                    }
+                    const uint64_t path_id = (uint64_t)pix * P.ns + s;
+                    pcg_seed(ps.rng, splitmix64(P.seed ^ path_id), path_id);
+                    camera_ray_args(S, ps.rng, u, v, &pr.o, &pr.dir, &pr.time);
+                    pr.inside = 0;
+                    pr.kind = 0;
+                    want_ray = true;
+                    ps.depth = 0;
+                    ps.nlev = 0;
+                    ps.rays = 0;
+                    active = true;
+                }
+            }
+            PH_MARK(ph, 4);
+            if (have < c) {
+                pool_next = nb + (c - have);
+                pool_end = nb + batch;
+                if (nb >= P.n_paths) exhausted = true;
+            } else {
+                pool_next += c;
+            }
+            if (pool_next >= P.n_paths) exhausted = true;
+        }
+        if (!__any(active)) break;
+        PH_MARK(ph, 0);
+        if (want_ray) {
+            ps.r = make_ray(pr.o, pr.dir, pr.time, pr.inside);
+            if (pr.kind) finish_scatter<F, LK>(S, ps, lev, pr);
+        }
+        PH_MARK(ph, 7);
+    }
+    } else {
     for (;;) {
         const uint64_t need = __ballot(!active);
         if (need && !exhausted) {
@@ -233,6 +335,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
         }
         PH_MARK(ph, 3);
     }
+}
 #ifdef MRT_PHASES
     if (lane == 0)
         for (int i = 0; i < 8; i++) atomicAdd(&g_phases[i], (unsigned long long)ph.a[i]);

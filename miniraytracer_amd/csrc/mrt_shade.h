@@ -237,6 +237,21 @@ __device__ __forceinline__ Ray camera_ray(const DScene& S, Pcg& rng, float s, fl
     return make_ray(add(origin, offset), dir, time, 0);
 }
 
+// camera::get_ray without the ray constructor: origin, direction argument and time of the ray
+// (the constructor -- normalize, 1/dir, dirMask -- runs once per iteration for every lane that
+// has a new ray, see PendRay)
+__device__ __forceinline__ void camera_ray_args(const DScene& S, Pcg& rng, float s, float t, f3* o, f3* dir, float* time) {
+    const MRT_CONST_AS mrt_camera* cp = const_ptr(S.camp);
+    asm volatile("" : "+s"(cp));
+    const MRT_CONST_AS mrt_camera& C = *cp;
+    f3 rd = fmul(C.lens_radius, random_in_disk(rng));
+    f3 offset = add(mulf(ld3(C.u), rd.x), mulf(ld3(C.v), rd.y));
+    *time = C.time0 + (C.time1 - C.time0) * randf(rng);
+    f3 origin = ld3(C.origin);
+    *dir = sub(sub(add(add(ld3(C.llcorner), fmul(s, ld3(C.horz))), fmul(t, ld3(C.vert))), origin), offset);
+    *o = add(origin, offset);
+}
+
 // One segment.  Returns true when the path has ended; its radiance is then in *L.
 template <uint32_t F, uint32_t LK>
 __device__ __forceinline__ bool trace_segment(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev,
@@ -350,6 +365,139 @@ __device__ __forceinline__ bool trace_segment(const DScene& S, PathState& ps, ui
     ps.nlev = (ps.nlev + 1) | (quiet_level(lv) ? 0u : LEV_LOUD);
     r = sc;
     return false;
+}
+
+// The next ray of a lane, built by make_ray once per iteration for all lanes at once (camera
+// rays of new paths and scattered rays alike), plus what a diffuse scatter still has to do once
+// the scattered ray exists (its pdfs need the normalized direction).
+struct PendRay {
+    f3 o, dir;
+    float time;
+    int inside;
+    f3 att, n;      // diffuse scatter: attenuation, normal
+    uint32_t kind;  // 0: nothing after the ray; 1: lambertian mix; 2: isotropic
+};
+
+// trace_segment up to the next ray's constructor arguments.  Returns true when the path has
+// ended (radiance in *L); otherwise *pr holds the next ray's arguments.
+template <uint32_t F, uint32_t LK>
+__device__ __forceinline__ bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev,
+                                            const LStack& Ls, f3* L, PendRay* pr, PhaseClock& ph) {
+    ps.rays++;
+    HitRec rec;
+    Ray& r = ps.r;
+    bool hit;
+    if constexpr (MRT_SIG_OF(F) != SIG_NONE) hit = scene_hit_sig<F>(S, r, 0.001f, rec, Ls);
+    else if constexpr ((F & FT_LIN) != 0) hit = scene_hit_lin<F>(S, r, 0.001f, rec, Ls, ps.rng);
+    else hit = scene_hit<F>(S, r, 0.001f, rec, ps.rng, Ls);
+    PH_MARK(ph, 1);
+    if (!hit) {
+        if ((F & FT_SKY) && S.sky) {  // main.cpp:113-115
+            float tt = 0.5f * (r.d.y + 1.0f);
+            float o = 1.0f - tt;
+            *L = f3{o + tt * 0.5f, o + tt * 0.7f, o + tt * 1.0f};
+        } else {
+            *L = f3{0, 0, 0};
+        }
+        return true;
+    }
+    const DMat M = S.mats[rec.mat];
+    if (M.kind == MRT_M_LIGHT) {  // diffuse_light: sampleEmissive, never scatters (material.h:190-199)
+        *L = dot(rec.n, r.d) < 0.0f ? fmul(M.p, mat_color<F>(S, M, rec)) : f3{0, 0, 0};
+        return true;
+    }
+    if (ps.depth >= max_bounces) {  // the emitted term of a non-emissive material
+        *L = f3{0, 0, 0};
+        return true;
+    }
+    ps.depth++;
+    pr->o = rec.p;
+    pr->time = r.time;
+    pr->inside = 0;
+    pr->kind = 0;
+    if ((F & FT_METAL) && M.kind == MRT_M_METAL) {  // metal::scatter (material.h:91-98)
+        f3 reflected = sub(r.d, fmul(2.0f * dot(r.d, rec.n), rec.n));
+        f3 rs = random_in_sphere(ps.rng);
+        pr->dir = add(reflected, fmul(1 - M.p, rs));
+        f3 att = mat_color<F>(S, M, rec);
+        const float4 lv = make_float4(att.x, att.y, att.z, -1.0f);
+        lev.put(ps.nlev & ~LEV_LOUD, lv);
+        ps.nlev = (ps.nlev + 1) | (quiet_level(lv) ? 0u : LEV_LOUD);
+        return false;
+    }
+    if (M.kind == MRT_M_DIELECTRIC) {  // dielectric::scatter (material.h:121-175)
+        const float ref = M.p;
+        const float cosI = -dot(r.d, rec.n);
+        f3 facing;
+        float nio;
+        if (cosI < 0) {
+            facing = f3{-rec.n.x, -rec.n.y, -rec.n.z};
+            nio = ref;
+        } else {
+            facing = rec.n;
+            nio = M.col[0];  // 1.0f / ref, computed on upload (the same IEEE quotient)
+        }
+        f3 nd = sub(r.d, fmul(2.0f * dot(r.d, rec.n), rec.n));  // reflect (vec3.h:178-181)
+        int inside = r.inside;
+        const float ncosI = dot(r.d, facing);
+        const float sinT2 = (nio * nio) * (1.0f - ncosI * ncosI);
+        if (sinT2 <= 1.0f) {
+            const float cosT = sqrt_(1.0f - sinT2);
+            const float cs = cosI < 0 ? sqrt_(1.0f - (nio * nio) * (1.0f - cosI * cosI)) : cosI;
+            const float r0 = M.col[1];  // ((1 - ref) / (1 + ref))^2, computed on upload
+            const float reflect_prob = r0 + (1 - r0) * pow5_((1 - cs));
+            if (!(randf(ps.rng) < reflect_prob)) {
+                nd = add(fmul(nio, r.d), fmul(nio * -ncosI - cosT, facing));
+                if (cosI < 0) {
+                    inside--;
+                    if (inside < 0) inside = 0;
+                } else {
+                    inside++;
+                }
+            }
+        }
+        pr->dir = nd;
+        pr->inside = inside;
+        return false;
+    }
+    // lambertian / isotropic (material.h:48-74): the direction now, the pdfs after the ray exists
+    const bool lamb = !(F & FT_ISO) || M.kind == MRT_M_LAMBERTIAN;
+    pr->att = mat_color<F>(S, M, rec);
+    pr->n = rec.n;
+    pr->kind = lamb ? 1u : 2u;
+    const bool light = S.biased != MRT_NONE && randf(ps.rng) < 0.5f;
+    Draws dr{0.0f, 0.0f, 2u};
+    if (lamb) {
+        dr.v0 = randf(ps.rng);
+        dr.v1 = randf(ps.rng);
+        dr.used = 0;
+    }
+    if (light) pr->dir = biased_pdf_generate<F>(S, rec.p, r.time, ps.rng, dr);
+    else pr->dir = lamb ? onb_apply(rec.n, random_cosine_direction_pre(dr.v0, dr.v1)) : random_in_sphere(ps.rng);
+    PH_MARK(ph, 6);
+    return false;
+}
+
+// the rest of a diffuse scatter once ps.r = make_ray(pr): mix_pdf value (main.cpp:84-102), level
+template <uint32_t F, uint32_t LK>
+__device__ __forceinline__ void finish_scatter(const DScene& S, PathState& ps, const LevStore<LK>& lev, const PendRay& pr) {
+    const Ray& sc = ps.r;
+    float sval, spdf;
+    if (pr.kind == 1u) {
+        const float cosine = dot(sc.d, pr.n);
+        constexpr float INV_PI = 1.0f / PI_F;
+        float sv = div_core(cosine, PI_F, INV_PI);
+        if (__builtin_expect(any_lane((cosine > 0) & (cosine < 0x1p-100f)), 0)) sv = cosine < 0x1p-100f ? cosine / PI_F : sv;
+        sval = cosine > 0 ? sv : 0;
+        spdf = cosine < 0 ? 0 : cosine * (1.0f / PI_F);
+    } else {
+        sval = 1 / (2 * PI_F);
+        spdf = 1.0f / (2.0f * PI_F);
+    }
+    const float pdf_v = S.biased != MRT_NONE ? 0.5f * (biased_pdf_value<F>(S, sc.o, sc.d, sc.time) + sval) : sval;
+    const float4 lv = make_float4(pr.att.x * spdf, pr.att.y * spdf, pr.att.z * spdf, pdf_v);
+    lev.put(ps.nlev & ~LEV_LOUD, lv);
+    ps.nlev = (ps.nlev + 1) | (quiet_level(lv) ? 0u : LEV_LOUD);
 }
 
 // the recursion's return path, deepest level first; the lane's levels are contiguous, so they
