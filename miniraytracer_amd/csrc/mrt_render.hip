@@ -130,9 +130,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
     const LStack Ls{wb, (float*)(wb + P.lds_frames * 128), wmesh, (float*)(wmesh + P.lds_mesh * 64), lane};
     const DScene& S = P.sc;
     const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const LevStore<LK> lev{(MRT_GLOBAL_AS v4f*)(P.lev + slot * P.lev_rows),
+    const LevStore<LK> lev{(MRT_GLOBAL_AS v4f*)P.lev, P.lev_rows, (uint32_t)slot,
                            (MRT_LDS_AS v4f*)((float4*)(wmesh + (P.lds_mesh + P.lds_save) * 64) + lane)};
-    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    // set bits of a wave mask below this lane (v_mbcnt: no per-lane 64-bit mask kept live)
+    auto rank_below = [](uint64_t m) -> uint32_t {
+        return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    };
 
     // main.cpp:180/235 stop on !G_isRunning: a launch of a cancelled render does no work (mrt_render
     // splits a cancellable render into several launches)
@@ -196,7 +199,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
             }
             PH_MARK(ph, 0);
             if (!active) {
-                const uint32_t rank = (uint32_t)__popcll(need & lt_mask);
+                const uint32_t rank = rank_below(need);
                 const uint64_t i = rank < have ? pool_next + rank : nb + (rank - have);
                 if (i < P.n_paths) {
                     idx = (uint32_t)i;
@@ -269,7 +272,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
             }
             PH_MARK(ph, 0);
             if (!active) {
-                const uint32_t rank = (uint32_t)__popcll(need & lt_mask);
+                const uint32_t rank = rank_below(need);
                 const uint64_t i = rank < have ? pool_next + rank : nb + (rank - have);
                 if (i < P.n_paths) {
                     idx = (uint32_t)i;

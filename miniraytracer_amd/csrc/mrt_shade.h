@@ -199,17 +199,28 @@ struct LevStore {
     // explicit address spaces: a generic pointer here made the compiler merge the two cases into
     // one flat access, which counts against vmcnt AND lgkmcnt (every later LDS wait then waited
     // for the level store to reach memory)
-    MRT_GLOBAL_AS v4f* g;  // this lane's HBM rows
-    MRT_LDS_AS v4f* lds;   // this lane's first LDS slot (stride 64 float4 per level)
+    // this lane's HBM row = base + slot * rows, formed at each use: a 32-bit slot stays live across
+    // the path loop instead of a 64-bit pointer (which the register allocator spilled to scratch)
+    MRT_GLOBAL_AS v4f* base;  // uniform
+    uint32_t rows;            // uniform: levels per lane
+    uint32_t slot;
+    MRT_LDS_AS v4f* lds;      // this lane's first LDS slot (stride 64 float4 per level)
+    __device__ __forceinline__ MRT_GLOBAL_AS v4f* g() const {
+        uint32_t sl = slot;
+#if defined(__HIP_DEVICE_COMPILE__)
+        asm volatile("" : "+v"(sl));  // keeps the address from being hoisted out of the loop
+#endif
+        return base + (uint64_t)sl * rows;
+    }
     __device__ __forceinline__ void put(uint32_t d, float4 v) const {
         const v4f w = {v.x, v.y, v.z, v.w};
         if (LK > 0 && d < LK) lds[d * 64] = w;
-        else g[d] = w;
+        else g()[d] = w;
     }
     __device__ __forceinline__ float4 get(uint32_t d) const {
         v4f w;
         if (LK > 0 && d < LK) w = lds[d * 64];
-        else w = g[d];
+        else w = g()[d];
         return make_float4(w.x, w.y, w.z, w.w);
     }
 };
