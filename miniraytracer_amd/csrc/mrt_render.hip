@@ -131,7 +131,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OC
     const DScene& S = P.sc;
     const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const LevStore<LK> lev{(MRT_GLOBAL_AS v4f*)P.lev, P.lev_rows, (uint32_t)slot,
-                           (MRT_LDS_AS v4f*)((float4*)(wmesh + (P.lds_mesh + P.lds_save) * 64) + lane)};
+                           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)(MRT_LDS_AS uint32_t*)(wmesh + (P.lds_mesh + P.lds_save) * 64))};
     // set bits of a wave mask below this lane (v_mbcnt: no per-lane 64-bit mask kept live)
     auto rank_below = [](uint64_t m) -> uint32_t {
         return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));

@@ -204,7 +204,17 @@ struct LevStore {
     MRT_GLOBAL_AS v4f* base;  // uniform
     uint32_t rows;            // uniform: levels per lane
     uint32_t slot;
-    MRT_LDS_AS v4f* lds;      // this lane's first LDS slot (stride 64 float4 per level)
+    uint32_t lds_base;        // uniform: LDS byte address of this wave's level 0 row (64 float4)
+    // this lane's first LDS slot, formed at use from the lane id (a per-lane pointer kept live
+    // across the path loop was spilled)
+    __device__ __forceinline__ MRT_LDS_AS v4f* lds() const {
+#if defined(__HIP_DEVICE_COMPILE__)
+        const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+#else
+        const uint32_t lane = 0;
+#endif
+        return (MRT_LDS_AS v4f*)(uintptr_t)(lds_base + lane * 16u);
+    }
     __device__ __forceinline__ MRT_GLOBAL_AS v4f* g() const {
         uint32_t sl = slot;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -214,12 +224,12 @@ struct LevStore {
     }
     __device__ __forceinline__ void put(uint32_t d, float4 v) const {
         const v4f w = {v.x, v.y, v.z, v.w};
-        if (LK > 0 && d < LK) lds[d * 64] = w;
+        if (LK > 0 && d < LK) lds()[d * 64] = w;
         else g()[d] = w;
     }
     __device__ __forceinline__ float4 get(uint32_t d) const {
         v4f w;
-        if (LK > 0 && d < LK) w = lds[d * 64];
+        if (LK > 0 && d < LK) w = lds()[d * 64];
         else w = g()[d];
         return make_float4(w.x, w.y, w.z, w.w);
     }
