@@ -7,7 +7,9 @@ CC      ?= gcc
 ARCH    ?= gfx950
 JOBS    ?= 8
 # Numerics contract: no FMA contraction, IEEE division/sqrt, denormals kept.
-HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function
+# No SLP vectorisation: it packed unrelated float ops into v_pk_* pairs whose constant halves
+# were kept live in VGPR pairs and spilled (C2 +8%, bunny +7% without it; results identical).
+HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -Wall -Wno-unused-function
 # per-lane traversal stacks stay in scratch instead of being promoted into VGPR vectors
 HIPDEV   = -mllvm -disable-promote-alloca-to-vector
 CSRC     = miniraytracer_amd/csrc

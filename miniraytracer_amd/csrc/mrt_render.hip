@@ -67,16 +67,20 @@ struct PathParams {
 // latency-bound, so a few spilled registers cost less than the lost occupancy.  Tuned per
 // variant on MI355X (DESIGN.md "Occupancy").
 // (compact variants -- Cornell, Cornell room + mesh, plain interpreter -- reach 80 VGPRs without
-// spills at 6; the wide-feature variants spill there and run best at 3 waves, 168 VGPRs)
+// spills at 6; built without SLP vectorisation (Makefile), the wide-feature variants run best at
+// 4 waves (128 VGPRs) and the room + mesh variant at 7 (72 VGPRs, no LDS fold levels))
 #ifndef MRT_WPE_WIDE
-#define MRT_WPE_WIDE 3
+#define MRT_WPE_WIDE 4
+#endif
+#ifndef MRT_WPE_LIN
+#define MRT_WPE_LIN 6
 #endif
 #ifndef MRT_WPE_MESH
-#define MRT_WPE_MESH 6
+#define MRT_WPE_MESH 7
 #endif
 template <uint32_t F> struct PathOcc {
     static constexpr bool kWide = (F & (FT_BVHW | FT_TEX | FT_VOLUME)) != 0 || !(F & FT_LIN);
-    static constexpr int W = kWide ? MRT_WPE_WIDE : ((F & FT_MESH) != 0 ? MRT_WPE_MESH : 6);
+    static constexpr int W = kWide ? MRT_WPE_WIDE : ((F & FT_MESH) != 0 ? MRT_WPE_MESH : MRT_WPE_LIN);
 };
 #ifndef MRT_BATCH
 #define MRT_BATCH 256u  // paths a wave claims per atomic on the work counter (one hot address)
@@ -107,10 +111,10 @@ extern "C" int mrt_debug_phases(unsigned long long* out, int reset) {
 #define MRT_LEVK_CORNELL 2u
 #endif
 #ifndef MRT_LEVK_WIDE
-#define MRT_LEVK_WIDE 4u
+#define MRT_LEVK_WIDE 2u
 #endif
 #ifndef MRT_LEVK_MESH
-#define MRT_LEVK_MESH 1u
+#define MRT_LEVK_MESH 0u
 #endif
 template <uint32_t F> struct PathLevLds {
     static constexpr uint32_t K = ((F & 0xFFFFu) == (FT_LIN | FT_INST)) ? MRT_LEVK_CORNELL
