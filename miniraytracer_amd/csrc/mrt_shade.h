@@ -531,7 +531,23 @@ template <uint32_t LK>
 __device__ __forceinline__ f3 fold_levels(const LevStore<LK>& lev, uint32_t nlev, f3 L) {
     // a black end through quiet levels stays +0 (the common escaped path): nothing to fold
     if (!(nlev & LEV_LOUD) && ((__float_as_uint(L.x) | __float_as_uint(L.y) | __float_as_uint(L.z)) == 0)) return L;
-    for (int d = (int)(nlev & ~LEV_LOUD) - 1; d >= 0; d--) L = fold_level(lev.get((uint32_t)d), L);
+    int d = (int)(nlev & ~LEV_LOUD) - 1;
+#ifndef MRT_FOLD_SERIAL
+    // HBM levels four at a time: the four loads (contiguous in the lane's row, indices clamped to
+    // stay inside it) are in flight together, then folded deepest first: one memory round trip per
+    // four levels (C2 +1.6%)
+    while (d >= (int)LK) {
+        const int lo = (int)LK;
+        const float4 a = lev.get((uint32_t)d), b = lev.get((uint32_t)max(d - 1, lo)), c = lev.get((uint32_t)max(d - 2, lo)),
+                     e = lev.get((uint32_t)max(d - 3, lo));
+        L = fold_level(a, L);
+        if (d - 1 >= lo) L = fold_level(b, L);
+        if (d - 2 >= lo) L = fold_level(c, L);
+        if (d - 3 >= lo) L = fold_level(e, L);
+        d = max(d - 4, lo - 1);
+    }
+#endif
+    for (; d >= 0; d--) L = fold_level(lev.get((uint32_t)d), L);
     return L;
 }
 
