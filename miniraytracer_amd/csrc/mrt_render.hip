@@ -69,6 +69,12 @@ struct PathParams {
 // (compact variants -- Cornell, Cornell room + mesh, plain interpreter -- reach 80 VGPRs without
 // spills at 6; built without SLP vectorisation (Makefile), the wide-feature variants run best at
 // 4 waves (128 VGPRs) and the room + mesh variant at 7 (72 VGPRs, no LDS fold levels))
+// threads per path-kernel workgroup (each wave owns its own LDS slice; a smaller group frees its
+// CU slot as soon as its own waves finish, which matters in a launch's tail)
+#ifndef MRT_PATH_WG
+#define MRT_PATH_WG 64
+#endif
+static constexpr uint32_t kWavesPerWG = MRT_PATH_WG / 64;
 #ifndef MRT_WPE_WIDE
 #define MRT_WPE_WIDE 4
 #endif
@@ -123,7 +129,7 @@ template <uint32_t F> struct PathLevLds {
                                                                        : 0u;
 };
 template <uint32_t F>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MRT_OCC(F)))) mrt_path_kernel(PathParams P) {
+__global__ void __launch_bounds__(MRT_PATH_WG) __attribute__((amdgpu_waves_per_eu(MRT_OCC(F)))) mrt_path_kernel(PathParams P) {
     constexpr uint32_t LK = PathLevLds<F>::K;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t lane = threadIdx.x & 63u;
@@ -963,17 +969,18 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     s->lds_rays = lin_kernel ? 0 : (uint32_t)gc.max_rays;
     s->lds_mesh = (uint32_t)gc.max_mesh;
     s->lds_save = (lin_kernel && (kVariants[s->variant] & FT_INST)) ? 15u : 0u;
-    s->lds_bytes = (size_t)4 * 64 * 4 * (s->lds_frames * 2 + s->lds_rays * 11 + s->lds_mesh + s->lds_save + kLevK[s->variant] * 4);
+    s->lds_bytes = (size_t)kWavesPerWG * 64 * 4 * (s->lds_frames * 2 + s->lds_rays * 11 + s->lds_mesh + s->lds_save + kLevK[s->variant] * 4);
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
     if (s->lds_bytes > (size_t)prop.sharedMemPerBlock) { mrt_scene_free(s); return mrt_internal_fail(MRT_ERR_INVALID, "scene graph too deep for the LDS stacks"); }
-    // resident workgroups per CU: one 256-thread group = one wave per SIMD; VGPRs (512 per SIMD
+    // resident workgroups per CU: one 256-thread group = one wave per SIMD (a 64-thread group =
+    // a quarter of that); VGPRs (512 per SIMD
     // lane, granule 8) and LDS (160 KiB per CU) bound it.  (The runtime occupancy query
     // under-counts gfx950 register budgets, so it is computed from the kernel's attributes.)
     hipFuncAttributes fa{};
     HIPCHK(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(kernel_for(s->variant))));
     const int vg = std::max(8, (fa.numRegs + 7) & ~7);
-    int nb = std::min(8, 512 / vg);
+    int nb = std::min(8, 512 / vg) * (int)(4 / kWavesPerWG);  // waves per SIMD x groups per wave slot
     if (s->lds_bytes) nb = std::min<int>(nb, (int)((160u * 1024u) / s->lds_bytes));
     if (nb < 1) nb = 1;
     s->vgprs = (uint32_t)fa.numRegs;
@@ -1057,7 +1064,7 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
     if (d->flags & MRT_RF_PATH_DEBUG)
         if ((st = grow((void**)&s->d_path_rays, &s->pr_cap, paths * 4))) return st;
     s->lev_rows = std::max<uint32_t>(d->max_bounces, 1);
-    if ((st = grow((void**)&s->d_lev, &s->lev_cap, (size_t)s->lev_rows * s->grid * 256 * 16))) return st;
+    if ((st = grow((void**)&s->d_lev, &s->lev_cap, (size_t)s->lev_rows * s->grid * MRT_PATH_WG * 16))) return st;
     uint32_t launches = (ns + s->chunk - 1) / s->chunk;
     if ((st = grow((void**)&s->d_counters, &s->cnt_cap, (size_t)launches * 8))) return st;
     if (!s->pstream) HIPCHK(hipStreamCreateWithFlags(&s->pstream, hipStreamNonBlocking));
@@ -1123,7 +1130,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.ns = ns;
         P.s0 = s0;
         P.n_paths = s->npix * (s1 - s0);
-        P.tail_zone = (uint32_t)std::min<uint64_t>((uint64_t)s->grid * 4 * 2 * MRT_BATCH, P.n_paths);  // ~2 big claims per wave
+        P.tail_zone = (uint32_t)std::min<uint64_t>((uint64_t)s->grid * kWavesPerWG * 2 * MRT_BATCH, P.n_paths);  // ~2 big claims per wave
         P.seed = d->seed;
         P.max_bounces = d->max_bounces;
         P.rad = s->d_rad;
@@ -1135,7 +1142,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.lev = s->d_lev;
         P.lev_rows = s->lev_rows;
         HIPCHK(hipEventRecord(s->ev[2 * s->n_launch], q));
-        hipLaunchKernelGGL(kernel_for(s->variant), dim3(s->grid), dim3(256), s->lds_bytes, q, P);
+        hipLaunchKernelGGL(kernel_for(s->variant), dim3(s->grid), dim3(MRT_PATH_WG), s->lds_bytes, q, P);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(s->ev[2 * s->n_launch + 1], q));
         s->n_launch++;
