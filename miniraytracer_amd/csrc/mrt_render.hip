@@ -94,6 +94,8 @@ template <uint32_t F> struct PathOcc {
 #ifndef MRT_TAIL_BATCH
 #define MRT_TAIL_BATCH 64u  // claim size within the last `tail_zone` paths of a launch
 #endif
+// one claim must cover a whole wave's idle lanes (the pool hands out at most 64 at once)
+static_assert(MRT_TAIL_BATCH >= 64u && MRT_BATCH >= MRT_TAIL_BATCH, "claims must be at least a wave wide");
 #ifdef MRT_PHASES
 __device__ unsigned long long g_phases[8];
 extern "C" int mrt_debug_phases(unsigned long long* out, int reset) {
