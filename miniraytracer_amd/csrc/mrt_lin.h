@@ -93,6 +93,41 @@ __device__ __forceinline__ bool lin_prim_t(const OP& o, const Ray& r, float tmin
     }
 }
 
+// lin_prim_rec for a primitive op whose kind is known at compile time, its data read through the
+// constant address space (wave-uniform op: scalar loads).  Same arithmetic as lin_prim_rec.
+template <uint32_t F, uint32_t KIND>
+__device__ __forceinline__ void lin_prim_rec_op(const MRT_CONST_AS LinOp& o, const Ray& r, float t, HitRec& rec) {
+    const uint32_t fl = LOP_FLAGS(o);
+    const bool needuv = (F & FT_UV) && (fl & MRT_F_NEEDUV);
+    rec.t = t;
+    rec.mat = o.mat;
+    rec.p = eval(r, t);
+    if constexpr (KIND == MRT_K_SPHERE) {
+        f3 cen = f3{o.f[0], o.f[1], o.f[2]};
+        if ((F & FT_MOVING) && (fl & MRT_F_MOVING))
+            cen = add(cen, fmul((r.time - o.f[6]) / (o.f[7] - o.f[6]), sub(f3{o.f[3], o.f[4], o.f[5]}, cen)));
+        rec.n = divf(sub(rec.p, cen), o.f[8]);
+        if (needuv) sphere_uv(rec.n, &rec.u, &rec.v);
+    } else {
+        const float ns = o.f[5];
+        float pb = 0, pc = 0;
+        if constexpr (KIND == MRT_K_XY) {
+            rec.n = f3{0, 0, ns};
+            if (needuv) { pb = r.o.x + t * r.d.x; pc = r.o.y + t * r.d.y; }
+        } else if constexpr (KIND == MRT_K_XZ) {
+            rec.n = f3{0, ns, 0};
+            if (needuv) { pb = r.o.x + t * r.d.x; pc = r.o.z + t * r.d.z; }
+        } else {
+            rec.n = f3{ns, 0, 0};
+            if (needuv) { pb = r.o.y + t * r.d.y; pc = r.o.z + t * r.d.z; }
+        }
+        if (needuv) {
+            rec.u = (pb - o.f[0]) / (o.f[1] - o.f[0]);
+            rec.v = (pc - o.f[2]) / (o.f[3] - o.f[2]);
+        }
+    }
+}
+
 // the record the primitive's hit() writes for a hit at t.  The node is per lane; its 64 B are
 // fetched whole (four 16-byte loads in flight together) rather than field by field, which the
 // compiler turned into two dependent round trips (kind/mat, then the kind's fields).

@@ -68,6 +68,9 @@ struct SigState {
 template <uint32_t F, uint32_t SIG>
 struct SigWalk {
     static constexpr const LinSig& G = kSigs[SIG];
+    // room + mesh: the record is derived op by op with scalar loads (teapot +1.4%); the Cornell
+    // walk keeps the per-lane node record (neutral there, shorter code)
+    static constexpr bool kDerive = SIG == SIG_ROOM_MESH;
 
     // ops [PC, END) of the program, lanes `on` taking part
     template <uint32_t PC, uint32_t END>
@@ -92,14 +95,15 @@ struct SigWalk {
                     node = o.node;
                 }
                 w.closest = h ? t : w.closest;
-                w.hnode = h ? node : w.hnode;  // the op's node (scalar operand): no per-lane lookup later
+                if constexpr (kDerive) w.hnode = h ? PC : w.hnode;  // op index: the record is derived op by op
+                else w.hnode = h ? node : w.hnode;  // the op's node (scalar operand): no per-lane lookup later
                 w.hinst = h ? cur_inst<PC>() : w.hinst;
                 w.hdone = h ? false : w.hdone;
                 run<PC + 1, END>(S, prog, tmin, w, on, rec, L);
             } else if constexpr (op == LOP_MESH) {
                 if (on && mesh_hit<true>(S, ld_node(const_ptr(S.nodes) + o.node), w.cur, tmin, w.closest, rec, true, L)) {
                     w.closest = rec.t;
-                    w.hnode = o.node;
+                    w.hnode = kDerive ? PC : o.node;
                     w.hinst = cur_inst<PC>();
                     w.hdone = true;
                 }
@@ -138,6 +142,20 @@ struct SigWalk {
         }
     }
 
+    // the record of the closest hit, op by op: for each primitive op some lane hit, that op's
+    // data by scalar loads and its compile-time kind (no per-lane node loads or kind switch)
+    template <uint32_t PC>
+    __device__ static __forceinline__ void derive(const MRT_CONST_AS LinOp* prog, const SigState& w, const Ray& r, const Ray& ir,
+                                                  HitRec& rec) {
+        if constexpr (PC < G.n) {
+            if constexpr (G.op[PC] == LOP_PRIM) {
+                if (__any(w.hnode == PC)) {
+                    if (w.hnode == PC) lin_prim_rec_op<F, G.kind[PC]>(prog[PC], cur_inst<PC>() != MRT_NONE ? ir : r, w.closest, rec);
+                }
+            }
+            derive<PC + 1>(prog, w, r, ir, rec);
+        }
+    }
     // the program's only instance op (MRT_NONE if it has none or several)
     __device__ static constexpr uint32_t only_inst() {
         uint32_t found = MRT_NONE, count = 0;
@@ -171,20 +189,35 @@ __device__ __forceinline__ bool scene_hit_sig(const DScene& S, Ray& r, float tmi
     SigWalk<F, SIG>::template run<0, kSigs[SIG].n - 1>(S, prog, tmin, w, true, rec, L);
     if (INST) r = lin_load_ray(L);
     if (w.hnode == MRT_NONE) return false;
-    const uint32_t node = w.hnode;
-    if (INST && w.hinst != MRT_NONE) {
-        if (!w.hdone) {
+    if constexpr (SigWalk<F, SIG>::kDerive) {
+        Ray ir = r;
+        if (INST && __any(w.hinst != MRT_NONE && !w.hdone)) {  // instance-frame ray of the hit (LDS)
             const float* b = L.save + L.lane + 9 * 64;
-            Ray ir = r;
             ir.o = f3{b[0], b[64], b[128]};
             ir.d = f3{b[192], b[256], b[320]};
-            lin_prim_rec<F>(S, node, ir, w.closest, rec);
         }
-        constexpr uint32_t IPC = SigWalk<F, SIG>::only_inst();
-        if constexpr (IPC != MRT_NONE) lin_untransform(prog[IPC], rec);  // known instance: scalar loads
-        else lin_untransform(S.prog[w.hinst], rec);
-    } else if (!w.hdone) {
-        lin_prim_rec<F>(S, node, r, w.closest, rec);
+        if (!w.hdone) SigWalk<F, SIG>::template derive<0>(prog, w, r, ir, rec);
+        if (INST && w.hinst != MRT_NONE) {
+            constexpr uint32_t IPC = SigWalk<F, SIG>::only_inst();
+            if constexpr (IPC != MRT_NONE) lin_untransform(prog[IPC], rec);
+            else lin_untransform(S.prog[w.hinst], rec);
+        }
+    } else {
+        const uint32_t node = w.hnode;
+        if (INST && w.hinst != MRT_NONE) {
+            if (!w.hdone) {
+                const float* b = L.save + L.lane + 9 * 64;
+                Ray ir = r;
+                ir.o = f3{b[0], b[64], b[128]};
+                ir.d = f3{b[192], b[256], b[320]};
+                lin_prim_rec<F>(S, node, ir, w.closest, rec);
+            }
+            constexpr uint32_t IPC = SigWalk<F, SIG>::only_inst();
+            if constexpr (IPC != MRT_NONE) lin_untransform(prog[IPC], rec);  // known instance: scalar loads
+            else lin_untransform(S.prog[w.hinst], rec);
+        } else if (!w.hdone) {
+            lin_prim_rec<F>(S, node, r, w.closest, rec);
+        }
     }
     return true;
 }
