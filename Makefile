@@ -10,8 +10,9 @@ JOBS    ?= 8
 # No SLP vectorisation: it packed unrelated float ops into v_pk_* pairs whose constant halves
 # were kept live in VGPR pairs and spilled (C2 +8%, bunny +7% without it; results identical).
 HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -Wall -Wno-unused-function
-# per-lane traversal stacks stay in scratch instead of being promoted into VGPR vectors
-HIPDEV   = -mllvm -disable-promote-alloca-to-vector
+# per-lane traversal stacks stay in scratch instead of being promoted into VGPR vectors; uniform
+# regions keep plain scalar branches instead of exec-mask structurisation (C2 +1.7%)
+HIPDEV   = -mllvm -disable-promote-alloca-to-vector -mllvm -structurizecfg-skip-uniform-regions
 CSRC     = miniraytracer_amd/csrc
 OBJDIR   = build/obj
 

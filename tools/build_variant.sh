@@ -9,7 +9,7 @@ flags="$*"
 make -s build/obj/scene_builder.o build/obj/mrt_common.o
 mkdir -p exp/obj_$tag
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -w \
-    -mllvm -disable-promote-alloca-to-vector $flags -c miniraytracer_amd/csrc/mrt_render.hip -o exp/obj_$tag/mrt_render.o
+    -mllvm -disable-promote-alloca-to-vector -mllvm -structurizecfg-skip-uniform-regions $flags -c miniraytracer_amd/csrc/mrt_render.hip -o exp/obj_$tag/mrt_render.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC exp/obj_$tag/mrt_render.o build/obj/scene_builder.o \
     build/obj/mrt_common.o -ldl -o exp/libmrt_$tag.so
 echo "built exp/libmrt_$tag.so"

@@ -4,7 +4,7 @@
 tag=$1; shift
 d=$(mktemp -d)
 ( cd $d && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -Wno-unused-function \
-    -mllvm -disable-promote-alloca-to-vector "$@" --save-temps -c /root/repo/miniraytracer_amd/csrc/mrt_render.hip -o r.o 2>/dev/null \
+    -mllvm -disable-promote-alloca-to-vector -mllvm -structurizecfg-skip-uniform-regions "$@" --save-temps -c /root/repo/miniraytracer_amd/csrc/mrt_render.hip -o r.o 2>/dev/null \
   && cp mrt_render-hip-amdgcn-amd-amdhsa-gfx950.s /tmp/isa_$tag.s )
 rm -rf $d
 awk '/^_Z15mrt_path_kernel.*:/{k=$1; n=0; inb=1} inb && /^[ \t]+[sv]_|^[ \t]+(global|ds|scratch|buffer|flat)_/{n++} /^\.Lfunc_end/{if(inb) ins[k]=n; inb=0}
