@@ -155,8 +155,12 @@ __global__ void __launch_bounds__(MRT_PATH_WG) __attribute__((amdgpu_waves_per_e
     bool active = false;
     uint32_t idx = 0;
     PathState ps;
-    uint64_t pool_next = 0, pool_end = 0;  // wave-uniform
-    bool exhausted = false;
+    // every wave's first claim is static (wave w: paths [w*B, (w+1)*B)); the work counter hands
+    // out what follows, so a launch does not open with one atomic per wave on one address
+    const uint64_t static_paths = (uint64_t)gridDim.x * (blockDim.x >> 6) * MRT_BATCH;
+    uint64_t pool_next = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + wave) * MRT_BATCH;  // wave-uniform
+    uint64_t pool_end = pool_next + MRT_BATCH;
+    bool exhausted = pool_next >= P.n_paths;
     uint32_t done_rays = 0;
     PhaseClock ph{};
 #ifdef MRT_PHASES
@@ -201,7 +205,7 @@ __global__ void __launch_bounds__(MRT_PATH_WG) __attribute__((amdgpu_waves_per_e
             uint64_t nb = 0;
             if (have < c) {
                 if (lane == 0) {
-                    nb = atomicAdd(P.counter, (unsigned long long)batch);
+                    nb = static_paths + atomicAdd(P.counter, (unsigned long long)batch);
                     // every 32nd claim: a system-scope store to host memory, read by mrt_progress
                     // without any GPU queue (a device-to-host copy could wait behind this launch)
                     if (P.hprog && ((nb / MRT_BATCH) & 31u) == 0)
@@ -274,7 +278,7 @@ __global__ void __launch_bounds__(MRT_PATH_WG) __attribute__((amdgpu_waves_per_e
             uint64_t nb = 0;
             if (have < c) {
                 if (lane == 0) {
-                    nb = atomicAdd(P.counter, (unsigned long long)batch);
+                    nb = static_paths + atomicAdd(P.counter, (unsigned long long)batch);
                     // every 32nd claim: a system-scope store to host memory, read by mrt_progress
                     // without any GPU queue (a device-to-host copy could wait behind this launch)
                     if (P.hprog && ((nb / MRT_BATCH) & 31u) == 0)
