@@ -45,6 +45,7 @@ struct PathParams {
     uint32_t s0;                          // first sample of this chunk
     uint32_t n_paths;                     // npix * chunk samples (< 2^32, enforced on the host)
     uint32_t tail_zone;                   // last paths of the launch handed out MRT_TAIL_BATCH at a time
+    uint32_t static_first;                // every wave's first claim is static (short launches)
     uint64_t seed;
     uint32_t max_bounces;
     float* __restrict__ rad;              // n_paths * 3 floats, [s - s0][lp]
@@ -157,10 +158,13 @@ __global__ void __launch_bounds__(MRT_PATH_WG) __attribute__((amdgpu_waves_per_e
     PathState ps;
     // every wave's first claim is static (wave w: paths [w*B, (w+1)*B)); the work counter hands
     // out what follows, so a launch does not open with one atomic per wave on one address
-    const uint64_t static_paths = (uint64_t)gridDim.x * (blockDim.x >> 6) * MRT_BATCH;
-    uint64_t pool_next = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + wave) * MRT_BATCH;  // wave-uniform
-    uint64_t pool_end = pool_next + MRT_BATCH;
-    bool exhausted = pool_next >= P.n_paths;
+    // (short launches only -- P.static_first, set by the host when a wave gets fewer than 64
+    // claims: there the opening atomics are a visible share; in long launches the static batch of
+    // a wave that starts late in a pipelined step delays that launch's end)
+    const uint64_t static_paths = P.static_first ? (uint64_t)gridDim.x * (blockDim.x >> 6) * MRT_BATCH : 0;
+    uint64_t pool_next = P.static_first ? ((uint64_t)blockIdx.x * (blockDim.x >> 6) + wave) * MRT_BATCH : 0;  // wave-uniform
+    uint64_t pool_end = P.static_first ? pool_next + MRT_BATCH : 0;
+    bool exhausted = P.static_first && pool_next >= P.n_paths;
     uint32_t done_rays = 0;
     PhaseClock ph{};
 #ifdef MRT_PHASES
@@ -1137,6 +1141,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.s0 = s0;
         P.n_paths = s->npix * (s1 - s0);
         P.tail_zone = (uint32_t)std::min<uint64_t>((uint64_t)s->grid * kWavesPerWG * 2 * MRT_BATCH, P.n_paths);  // ~2 big claims per wave
+        P.static_first = (uint64_t)P.n_paths < (uint64_t)s->grid * kWavesPerWG * MRT_BATCH * 64u;
         P.seed = d->seed;
         P.max_bounces = d->max_bounces;
         P.rad = s->d_rad;
