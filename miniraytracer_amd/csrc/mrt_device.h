@@ -173,10 +173,10 @@ __device__ __forceinline__ f3 random_in_disk(Pcg& r) {
     } while ((p.x * p.x + p.y * p.y) >= 1.0f);
     return p;
 }
-// NOTE: x,y scaled by 2*sqrt(r2), as the reference does (pcg.cpp:92-93)
-__device__ __forceinline__ f3 random_cosine_direction(Pcg& r) {
-    float r1 = randf(r), r2 = randf(r);
-    // randf() is 0 or >= 2^-23: both radicands are 0 or in [2^-23, 1], where sqrt_core is exact
+// random_cosine_direction (pcg.cpp:87-95) given its two draws r1, r2 (the caller draws them, in
+// that order).  NOTE: x,y scaled by 2*sqrt(r2), as the reference does (pcg.cpp:92-93).
+// randf() is 0 or >= 2^-23: both radicands are 0 or in [2^-23, 1], where sqrt_core is exact.
+__device__ __forceinline__ f3 random_cosine_direction_pre(float r1, float r2) {
     float z = sqrt_core(1 - r2);
     float phi = (2 * PI_F) * r1;
     float s2 = sqrt_core(r2);
@@ -184,24 +184,8 @@ __device__ __forceinline__ f3 random_cosine_direction(Pcg& r) {
     sincos_(phi, &sp, &cp);
     return f3{(cp * 2) * s2, (sp * 2) * s2, z};
 }
-__device__ __forceinline__ f3 random_cosine_direction_pre(float r1, float r2) {  // r1, r2: its two draws
-    float z = sqrt_core(1 - r2);
-    float phi = (2 * PI_F) * r1;
-    float s2 = sqrt_core(r2);
-    float sp, cp;
-    sincos_(phi, &sp, &cp);
-    return f3{(cp * 2) * s2, (sp * 2) * s2, z};
-}
+// random_towards_sphere (pcg.cpp:125-133) given its two draws r1, r2 (sphere::pdf_generate, sphere.cpp:63-78)
 __device__ __forceinline__ f3 random_towards_sphere_pre(float r1, float r2, float radius, float dist_sq) {
-    float z = 1 + r2 * (sqrt_(1 - (radius * radius) / dist_sq) - 1);
-    float phi = (2 * PI_F) * r1;
-    float q = sqrt_(1 - z * z);
-    float sp, cp;
-    sincos_(phi, &sp, &cp);
-    return f3{cp * q, sp * q, z};
-}
-__device__ __forceinline__ f3 random_towards_sphere(Pcg& r, float radius, float dist_sq) {
-    float r1 = randf(r), r2 = randf(r);
     float z = 1 + r2 * (sqrt_(1 - (radius * radius) / dist_sq) - 1);
     float phi = (2 * PI_F) * r1;
     float q = sqrt_(1 - z * z);
