@@ -16,10 +16,21 @@ HIPDEV   = -mllvm -disable-promote-alloca-to-vector -mllvm -structurizecfg-skip-
 CSRC     = miniraytracer_amd/csrc
 OBJDIR   = build/obj
 
-LIB_OBJS = $(OBJDIR)/mrt_render.o $(OBJDIR)/scene_builder.o $(OBJDIR)/mrt_common.o
+LIB_OBJS = $(OBJDIR)/mrt_render.o $(OBJDIR)/mrt_kernels_exact.o $(OBJDIR)/mrt_kernels_fast.o $(OBJDIR)/scene_builder.o $(OBJDIR)/mrt_common.o
+# the path kernels twice: exact contract (no contraction, IEEE division) and tolerance contract
+# (FMA contraction, reciprocal division, hardware rcp/sqrt/rsq, f32 transcendentals)
+FASTFLAGS = -DMRT_FAST=1 -ffp-contract=fast -freciprocal-math
 HDRS     = include/mrt.h include/mrt_scene.h include/mrt_mathfn.h $(wildcard $(CSRC)/*.h) Makefile
 
 all: miniraytracer_amd/libmrt.so bin/mrt oracle/liboracle.so
+
+$(OBJDIR)/mrt_kernels_exact.o: $(CSRC)/mrt_kernels.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) $(HIPDEV) -DMRT_FAST=0 -c $< -o $@
+
+$(OBJDIR)/mrt_kernels_fast.o: $(CSRC)/mrt_kernels.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) $(HIPDEV) $(FASTFLAGS) -c $< -o $@
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)

@@ -47,6 +47,12 @@ def parse():
                     help="work_queue tile edge; also the multi-GPU partition grain (tile k -> rank k %% N)")
     ap.add_argument("--cpu-spp", type=int, default=256, help="spp of the bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-quick", action="store_true", help="time the CPU baseline on the quota threads only")
+    ap.add_argument("--numerics", choices=["fast", "exact"], default="fast",
+                    help="numerics contract of the timed render: fast = tolerance contract (per-pixel RMSE < 1e-3 "
+                         "vs the reference as shipped, tests/test_gpu_parity.py), exact = bit-for-bit the reference "
+                         "built exact; the other one is timed too and reported as other_numerics")
+    ap.add_argument("--no-compare-numerics", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=3,
                     help="extra renders after the timed region whose HIP-event kernel time feeds roofline")
     ap.add_argument("--emulate-world", type=int, default=1,
@@ -63,32 +69,113 @@ def parse():
     return ap.parse_args()
 
 
+def _cpu_quota():
+    """CPUs this process may use: affinity mask, capped by a cgroup v2 cpu.max quota if one is set."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def cpu_baseline(args):
     """The reference as shipped (multithreaded work_queue, mode 1, atomic ray counter) on this
-    host's cores, over a bounded sample of the same scene; its own Mrays/s formula."""
+    host, over a bounded sample of the same scene; its own Mrays/s formula (main.cpp:403-405).
+    Timed twice: with as many threads as this process may use (affinity / cgroup quota) and with
+    -threads = os.cpu_count() (every CPU the machine reports; on a shared GPU box that is more than
+    the box's share, so the two differ)."""
     import oracle
-    threads = int(os.environ.get("MRT_CPU_THREADS", min(16, os.cpu_count() or 1)))
-    b = oracle.ref_binary(exact=False)
+    total = os.cpu_count() or 1
+    quota = _cpu_quota()
+    used = int(os.environ.get("MRT_CPU_THREADS", quota))
     sample = (f"scene {args.scene}, {args.width}x{args.height}, {args.cpu_spp} spp (of {args.samples}), "
-              f"depth {args.depth}")
+              f"depth {args.depth}, -mode 1")
+    b = oracle.ref_binary(exact=False)
     if b is not None:
-        r = oracle.run_ref(["-scene", args.scene, "-width", args.width, "-height", args.height, "-samples",
-                            args.cpu_spp, "-depth", args.depth, "-threads", threads], exact=False, timeout=900)
-        return {"value": round(r["mrays_per_s"], 3), "unit": "Mrays/s", "cores": threads, "kind": "reference",
-                "sample": sample + f", reference build oracle/_ref/mrt_ref as shipped (-mode 1), "
-                                   f"{r['rays']} rays in {r['trace_seconds']:.2f} s"}
+        def run(threads):
+            return oracle.run_ref(["-scene", args.scene, "-width", args.width, "-height", args.height, "-samples",
+                                   args.cpu_spp, "-depth", args.depth, "-threads", threads], exact=False, timeout=900)
+        r = run(used)
+        res = {"value": round(r["mrays_per_s"], 3), "unit": "Mrays/s", "cores": used, "cores_used": used,
+               "cores_total": total, "cores_quota": quota, "kind": "reference",
+               "sample": sample + f", reference build oracle/_ref/mrt_ref as shipped, {r['rays']} rays in "
+                                  f"{r['trace_seconds']:.2f} s on {used} threads"}
+        if total != used and not args.cpu_quick:
+            ra = run(total)
+            res["value_all_cores"] = round(ra["mrays_per_s"], 3)
+            res["sample_all_cores"] = f"-threads {total} (os.cpu_count()): {ra['rays']} rays in {ra['trace_seconds']:.2f} s"
+        return res
     import miniraytracer_amd as m
     sc = m.select_scene(args.scene, args.width / args.height)
-    d = oracle.desc(args.width, args.height, args.cpu_spp, depth=args.depth, threads=threads)
+    d = oracle.desc(args.width, args.height, args.cpu_spp, depth=args.depth, threads=used)
     t0 = time.perf_counter()
     _, rays, _, _ = oracle.render(sc, d)
     dt = time.perf_counter() - t0
-    return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+    return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": used, "cores_used": used,
+            "cores_total": total, "cores_quota": quota, "kind": "port",
             "sample": sample + f", C restatement oracle/liboracle.so, {rays} rays in {dt:.2f} s"}
+
+
+def roofline_counters(args, k_ms):
+    """Counter-derived figures of the dominant kernel from the committed rocprofv3 PMC summary of
+    the same workload (profiles/pmc_cornell_c2.json -> profiles/<tag>_pmc.json, tools/pmc_summary.py):
+    measured HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md), VALU issue
+    busy and VALU lane utilisation.  hbm_frac prices the measured bytes over the live kernel time."""
+    if not os.path.exists(args.pmc_json):
+        return {}
+    pmc = json.load(open(args.pmc_json))
+    if pmc.get("config") != [args.scene, args.width, args.height, args.samples, args.depth]:
+        return {}
+    e = pmc.get("by_numerics", {}).get(args.numerics)
+    if not e:
+        return {}
+    out = {"traffic": e.get("hbm_bytes_per_launch"), "pmc_source": pmc.get("source")}
+    if out["traffic"]:
+        out["hbm_frac"] = round(out["traffic"] / (k_ms * 1e-3) / (HBM_PEAK_GBS * 1e9), 5)
+    for k in ("valu_busy", "valu_lane_util"):
+        if e.get(k) is not None:
+            out[k] = round(e[k], 4)
+    return out
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` without a launcher: start N rank processes of this script (one per GPU,
+    RANK/LOCAL_RANK/WORLD_SIZE set, rendezvous on 127.0.0.1), like main() spawns one thread per
+    worker (main.cpp:376-382).  This parent never touches the GPU or imports the package."""
+    import socket
+    import torch  # device_count() does not initialise HIP
+    same = bool(os.environ.get("MRT_SAME_GPU"))
+    ndev = torch.cuda.device_count()
+    if args.gpus > ndev and not same:
+        print(f"bench.py: --gpus {args.gpus} but {ndev} GPU(s) visible (set MRT_SAME_GPU=1 to rehearse "
+              f"several ranks on one GPU)", file=sys.stderr)
+        return 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
 
 
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    if env_world is not None and int(env_world) != args.gpus and "--gpus" in " ".join(sys.argv):
+        print(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={env_world}", file=sys.stderr)
+        sys.exit(2)
     import torch
     import torch.distributed as dist
     import miniraytracer_amd as m
@@ -116,7 +203,11 @@ def main():
     d_rank, d_world = rank, world
     if world == 1 and args.emulate_world > 1:
         d_rank, d_world = args.emulate_rank, args.emulate_world
-    desc = m.render_desc(args.width, args.height, args.samples, depth=args.depth, tile_size=args.tile_size, rank=d_rank, world=d_world)
+    def desc_of(numerics):
+        return m.render_desc(args.width, args.height, args.samples, depth=args.depth, tile_size=args.tile_size,
+                             rank=d_rank, world=d_world, numerics=numerics)
+
+    desc = desc_of(args.numerics)
     for r in rnds:
         r.prepare(desc)
     px = m.local_pixels(desc)
@@ -135,13 +226,13 @@ def main():
     pending = [None]
     it = [0]
 
-    def step():
+    def step(d):
         # step i renders with context i % npipe on its stream; nothing orders it after step i-1's
         # kernels, so its waves start on the CUs that step i-1's finished waves leave idle
         j = it[0] % npipe
         it[0] += 1
         with torch.cuda.stream(streams[j]):
-            rnds[j].render_device(desc, outs[j].data_ptr(), rays.data_ptr(), streams[j].cuda_stream)
+            rnds[j].render_device(d, outs[j].data_ptr(), rays.data_ptr(), streams[j].cuda_stream)
             if world > 1:
                 # the one RCCL collective of the data path (tile shards -> rank 0), overlapped with
                 # the next render: finish the previous step's gather, then start this one's
@@ -154,36 +245,40 @@ def main():
             tg.finish(pending[0])
             pending[0] = None
 
-    # setup, untimed: one render per context, so every context's first-use costs (workspace
-    # first touch, first launch on its stream) are paid before the warmup steps
-    for j in range(npipe):
-        with torch.cuda.stream(streams[j]):
-            rnds[j].render_device(desc, outs[j].data_ptr(), rays.data_ptr(), streams[j].cuda_stream)
-    torch.cuda.synchronize(dev)
-    for _ in range(args.warmup):
-        step()
-    drain()
-    torch.cuda.synchronize(dev)
-    rays.zero_()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    drain()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    total_rays = rays.clone()
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-        dist.all_reduce(total_rays, op=dist.ReduceOp.SUM)
-    secs = float(elapsed.item())
-    nrays = int(total_rays.item())
-    rays_per_step_local = int(rays.item()) // max(args.steps, 1)
+    def measure(d):
+        """W untimed warmup steps, then EXACTLY K steps between barrier + synchronize on both
+        sides; (max-over-ranks seconds, total rays of all ranks, this rank's rays per step)."""
+        # setup, untimed: one render per context, so every context's first-use costs (workspace
+        # first touch, first launch on its stream) are paid before the warmup steps
+        for j in range(npipe):
+            with torch.cuda.stream(streams[j]):
+                rnds[j].render_device(d, outs[j].data_ptr(), rays.data_ptr(), streams[j].cuda_stream)
+        torch.cuda.synchronize(dev)
+        for _ in range(args.warmup):
+            step(d)
+        drain()
+        torch.cuda.synchronize(dev)
+        rays.zero_()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step(d)
+        drain()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+        total_rays = rays.clone()
+        if world > 1:
+            dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+            dist.all_reduce(total_rays, op=dist.ReduceOp.SUM)
+        return float(elapsed.item()), int(total_rays.item()), int(rays.item()) // max(args.steps, 1)
+
+    desc = desc_of(args.numerics)
+    secs, nrays, rays_per_step_local = measure(desc)
 
     verified = None
     if args.verify and d_world == world and rank == 0:
@@ -193,33 +288,44 @@ def main():
             full[px] = outs[(it[0] - 1) % npipe].cpu().numpy()
             img = full.reshape(args.height, args.width, 4)
         ref, ref_rays = m.Renderer(scene, device=local).render(
-            m.render_desc(args.width, args.height, args.samples, depth=args.depth, tile_size=args.tile_size))
+            m.render_desc(args.width, args.height, args.samples, depth=args.depth, tile_size=args.tile_size,
+                          numerics=args.numerics))
         got = img[..., :3] if isinstance(img, np.ndarray) else img[..., :3].cpu().numpy()
         verified = bool(np.array_equal(got.view(np.uint32), ref[..., :3].view(np.uint32))
                         and nrays == ref_rays * args.steps)
 
     # dominant kernel: mrt_path_kernel, HIP events recorded on the launch stream (3 extra renders)
-    kms = []
-    for _ in range(max(args.kernel_reps, 1)):
-        rnd.render_device(desc, out.data_ptr(), rays.data_ptr(), stream.cuda_stream)
-        ms, launches = rnd.kernel_ms()
-        kms.append(ms / max(launches, 1))
-    launches = max(launches, 1)
-    k_ms = float(np.mean(kms))
+    def kernel_ms(d):
+        kms = []
+        for _ in range(max(args.kernel_reps, 1)):
+            rnd.render_device(d, out.data_ptr(), rays.data_ptr(), stream.cuda_stream)
+            ms, launches = rnd.kernel_ms()
+            kms.append(ms / max(launches, 1))
+        return float(np.mean(kms)), max(launches, 1)
+
+    k_ms, launches = kernel_ms(desc)
     b_ray = B_RAY.get(args.scene)
     roofline = None
     if b_ray is not None:
         bytes_per_launch = rays_per_step_local / launches * b_ray
         achieved = bytes_per_launch / (k_ms * 1e-3) / 1e9
-        traffic = None
-        if os.path.exists(args.pmc_json):
-            pmc = json.load(open(args.pmc_json))
-            if pmc.get("config") == [args.scene, args.width, args.height, args.samples, args.depth]:
-                traffic = pmc.get("hbm_bytes_per_launch")
         roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                    "kernel": "mrt_path_kernel", "kernel_ms": round(k_ms, 3), "bytes_per_ray": b_ray,
+                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                    "kernel": "mrt_path_kernel" + ("_fast" if args.numerics == "fast" else ""),
+                    "kernel_ms": round(k_ms, 3), "bytes_per_ray": b_ray,
                     **{k: rnd.kernel_info()[k] for k in ("grid", "lds_bytes", "vgprs")}}
+        roofline.update(roofline_counters(args, k_ms))
+
+    # the other numerics contract, same protocol (reported beside the headline, never as `value`)
+    other = None
+    if not args.no_compare_numerics:
+        alt = "exact" if args.numerics == "fast" else "fast"
+        a_secs, a_rays, a_local = measure(desc_of(alt))
+        a_kms, a_launches = kernel_ms(desc_of(alt))
+        other = {"numerics": alt, "value": round(a_rays / a_secs / 1e6, 2), "ms_per_step": round(a_secs / args.steps * 1e3, 3),
+                 "kernel_ms": round(a_kms, 3)}
+        if b_ray is not None:
+            other["roofline_frac"] = round(a_local / a_launches * b_ray / (a_kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
 
     if rank == 0:
         res = {
@@ -239,11 +345,12 @@ def main():
                                    f"{desc.sqrt_samples ** 2} spp, depth {args.depth}, draw() accumulation",
                        "scene": args.scene, "width": args.width, "height": args.height,
                        "spp": desc.sqrt_samples ** 2, "depth": args.depth, "parallelism": f"tiles{world}",
-                       "tile_size": args.tile_size, "pipeline": npipe,
+                       "tile_size": args.tile_size, "pipeline": npipe, "numerics": args.numerics,
                        **({"emulated_share": f"rank {d_rank} of {d_world}"} if d_world != world else {}),
                        "rays_per_step": nrays // args.steps},
             "roofline": roofline,
             "cpu_baseline": None,
+            "other_numerics": other,
         }
         if verified is not None:
             res["verify_bit_exact"] = verified

@@ -43,7 +43,7 @@ typedef struct mrt_params {
     uint32_t buffer_width, buffer_height;
     uint32_t samples_per_pixel;
     uint32_t tile_size;
-    uint32_t num_threads;     /* reference CPU threads; here: GPUs to shard over (0 = all) */
+    uint32_t num_threads;     /* CPU worker threads, as in the reference (0 = all); the GPU backend has none */
     uint32_t max_bounces;
     uint32_t scene_select;
     uint32_t threading_mode;  /* 0 = draw() per-pixel mean, 1 = draw2() progressive average */
@@ -51,6 +51,8 @@ typedef struct mrt_params {
     uint32_t delay;
     /* additions (not in the reference): */
     uint64_t seed;            /* path stream-key seed, default = the reference main seed */
+    uint32_t gpus;            /* -gpus: GPUs to shard the work_queue tiles over (0 = every visible GPU) */
+    uint32_t numerics;        /* -numerics: 0 exact contract, 1 tolerance contract (MRT_RF_FAST) */
 } mrt_params;
 
 void mrt_default_params(mrt_params* p);
@@ -91,6 +93,10 @@ typedef struct mrt_render_desc {
     uint32_t flags;          /* MRT_RF_* */
 } mrt_render_desc;
 #define MRT_RF_PATH_DEBUG 0x1u /* also keep per-path radiance + ray counts (mrt_render_debug) */
+#define MRT_RF_FAST 0x2u       /* tolerance numerics contract: FMA contraction, hardware rcp/sqrt/rsq,
+                                  f32 transcendentals; per-pixel RMSE < 1e-3 vs the reference as
+                                  shipped (DESIGN.md "Numerics contracts").  Unset: the exact
+                                  contract, bit-for-bit the reference built exact. */
 
 void mrt_default_render_desc(const mrt_params* p, mrt_render_desc* d);
 

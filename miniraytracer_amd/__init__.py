@@ -79,9 +79,18 @@ def select_scene(scene, aspect, asset_dir=None):
     return Scene(h.value, scene)
 
 
+NUMERICS = ("exact", "fast")
+
+
 def render_desc(width, height, samples, depth=32, max_luminance=1000.0, mode=0, seed=MAIN_SEED, tile_size=32,
-                rank=0, world=1, chunk_samples=0, flags=0):
-    """Render description; `samples` is floored to a perfect square like main.cpp:319-320."""
+                rank=0, world=1, chunk_samples=0, flags=0, numerics="exact"):
+    """Render description; `samples` is floored to a perfect square like main.cpp:319-320.
+    numerics: "exact" (bit-for-bit the reference built exact) or "fast" (tolerance contract:
+    per-pixel RMSE < 1e-3 vs the reference as shipped; MRT_RF_FAST)."""
+    if numerics not in NUMERICS:
+        raise ValueError(f"numerics must be one of {NUMERICS}")
+    if numerics == "fast":
+        flags |= _lib.RF_FAST
     sq = int(np.sqrt(np.float32(samples)))
     return MrtRenderDesc(width, height, sq, depth, max_luminance, mode, seed, tile_size, rank, world,
                          chunk_samples, flags)

@@ -9,9 +9,13 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmrt.so")
+# experiment hook (tools/ab.sh): load an A/B build from exp/ instead of the in-tree library
+if os.environ.get("MRT_EXPERIMENT_LIB"):
+    LIB_PATH = os.path.abspath(os.environ["MRT_EXPERIMENT_LIB"])
 
 MRT_NONE = 0xFFFFFFFF
 RF_PATH_DEBUG = 0x1
+RF_FAST = 0x2  # tolerance numerics contract (include/mrt.h MRT_RF_FAST)
 
 
 class MrtParams(C.Structure):
@@ -21,7 +25,8 @@ class MrtParams(C.Structure):
                 ("samples_per_pixel", C.c_uint32), ("tile_size", C.c_uint32),
                 ("num_threads", C.c_uint32), ("max_bounces", C.c_uint32),
                 ("scene_select", C.c_uint32), ("threading_mode", C.c_uint32),
-                ("max_luminance", C.c_float), ("delay", C.c_uint32), ("seed", C.c_uint64)]
+                ("max_luminance", C.c_float), ("delay", C.c_uint32), ("seed", C.c_uint64),
+                ("gpus", C.c_uint32), ("numerics", C.c_uint32)]
 
 
 class MrtRenderDesc(C.Structure):

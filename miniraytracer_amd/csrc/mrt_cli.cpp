@@ -3,8 +3,9 @@
 // MI355X(s) through the C-ABI, prints the reference's "Trace: ... Mrays/s" line (main.cpp:403-406)
 // and writes the image (-o out.pfm: linear; -o out.ppm: Drago tone map, main.cpp:416-444).
 //
-// -threads N shards the work_queue tiles over N GPUs (one host thread per device, tile k -> GPU
-// k % N); 0 = every visible GPU.
+// -gpus N shards the work_queue tiles over N GPUs (one host thread per device, tile k -> GPU
+// k % N); 0 = every visible GPU.  -threads keeps the reference's meaning (CPU worker threads) and
+// has nothing to do on the GPU backend.  -numerics exact|fast picks the arithmetic contract.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -37,8 +38,11 @@ int main(int argc, char** argv) {
 
     int ndev = 0;
     if ((st = mrt_init(&ndev))) return fail("mrt_init", st);
-    int world = p.num_threads ? (int)p.num_threads : ndev;
-    if (world > ndev) world = ndev;
+    int world = p.gpus ? (int)p.gpus : ndev;
+    if (world > ndev) {
+        fprintf(stderr, "-gpus %u: only %d GPU(s) visible\n", p.gpus, ndev);
+        return 1;
+    }
 
     std::vector<mrt_scene*> scenes(world, nullptr);
     std::vector<mrt_render_desc> descs(world);
@@ -63,8 +67,10 @@ int main(int argc, char** argv) {
         if (sts[r]) return fail("render", sts[r]);
     uint64_t total = 0;
     for (uint64_t x : rays) total += x;
-    printf("MiniRayTracer - Scene: %.0fms - Trace: %.2fs - %.3f Mrays/s | %.3f us/ray  [%d x MI355X, %u spp]\n", gen_ms, secs,
-           (total * 0.000001) / secs, (secs * 1000000.0) / (double)total, world, descs[0].sqrt_samples * descs[0].sqrt_samples);
+    printf("MiniRayTracer - Scene: %.0fms - Trace: %.2fs - %.3f Mrays/s | %.3f us/ray  [%d x MI355X, %u spp, %s numerics]\n", gen_ms,
+           secs, (total * 0.000001) / secs, (secs * 1000000.0) / (double)total, world, descs[0].sqrt_samples * descs[0].sqrt_samples,
+           p.numerics ? "fast" : "exact");
+    printf("rays %llu\n", (unsigned long long)total);
 
     if (out) {
         std::string o = out;

@@ -63,6 +63,8 @@ extern "C" void mrt_default_params(mrt_params* p) {
     p->max_luminance = 1000;
     p->delay = 0;
     p->seed = 11350390909718046443ull;  // main.cpp:302
+    p->gpus = 0;
+    p->numerics = 1;  // tolerance contract (DESIGN.md "Numerics contracts"); -numerics exact for bit-exact
 }
 
 // ReadParameter (cmdline_parser.cpp:41-62): first occurrence wins, value range-checked, a bad
@@ -123,7 +125,10 @@ extern "C" mrt_status mrt_parse_argv(int argc, char** argv, mrt_params* out) {
                "  -samples  \t<value>\t\tSamples per pixel\n"
                "  -depth    \t<value>\t\tMaximum bounce depth per primary ray\n"
                "  -maxlum   \t<value>\t\tClamp maximum luminance (introduces bias)\n"
-               "  -threads  \t<value>\t\tNumber of GPUs to shard tiles over (0 selects all)\n"
+               "  -threads  \t<value>\t\tNumber of CPU threads (0 selects all; CPU backend only)\n"
+               "  -gpus     \t<value>\t\tNumber of GPUs to shard tiles over (0 selects all)\n"
+               "  -numerics \t[exact, fast]\tArithmetic contract (exact: bit-for-bit the reference built\n"
+               "            \t\t\twithout contraction; fast: per-pixel RMSE < 1e-3, default)\n"
                "  -tilesize \t<value>\t\tSize of image tiles (GPUs own interleaved tiles)\n"
                "  -mode     \t[0, 1]\t\tAccumulation mode (0 per-pixel mean, 1 progressive average)\n"
                "  -scene    \t[0, 9]\t\tSelect the scene (9 = wt_teapot in the Cornell box)\n"
@@ -146,6 +151,13 @@ extern "C" mrt_status mrt_parse_argv(int argc, char** argv, mrt_params* out) {
     if (int i = check_param(argc, argv, "-seed"))
         if (i + 1 < argc) p.seed = strtoull(argv[i + 1], nullptr, 0);
     if (check_param(argc, argv, "-delay")) p.delay = 1;
+    read_param<uint32_t>(argc, argv, "-gpus", &p.gpus, 0u, UMAX);
+    if (int i = check_param(argc, argv, "-numerics")) {
+        const char* v = i + 1 < argc ? argv[i + 1] : "";
+        if (!strcmp(v, "exact") || !strcmp(v, "0")) p.numerics = 0;
+        else if (!strcmp(v, "fast") || !strcmp(v, "1")) p.numerics = 1;
+        else printf("Warning: Invalid value for parameter '-numerics', must be exact or fast.\n");
+    }
     if (out) *out = p;
     return MRT_OK;
 }
@@ -162,6 +174,7 @@ extern "C" void mrt_default_render_desc(const mrt_params* p, mrt_render_desc* d)
     d->tile_size = p->tile_size;
     d->rank = 0;
     d->world = 1;
+    d->flags = p->numerics ? MRT_RF_FAST : 0u;
 }
 
 // ---- work_queue tile order (work_queue.cpp:6-128) ----

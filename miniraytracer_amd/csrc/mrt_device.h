@@ -22,6 +22,14 @@
 #include "../../include/mrt_mathfn.h"
 #include "../../include/mrt_scene.h"
 
+// MRT_FAST=1 builds the tolerance-contract kernels (DESIGN.md "Numerics contracts"): hardware
+// reciprocal / square root / reciprocal square root, f32 transcendentals, no exactness range
+// guards; the translation unit is compiled with FMA contraction and reciprocal division (as the
+// reference as shipped contracts a*b+c).  MRT_FAST=0 (default) is the exact contract.
+#ifndef MRT_FAST
+#define MRT_FAST 0
+#endif
+
 namespace mrtd {
 
 struct f3 {
@@ -33,7 +41,14 @@ __device__ __forceinline__ f3 sub(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, 
 __device__ __forceinline__ f3 mul(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
 __device__ __forceinline__ f3 mulf(f3 a, float f) { return f3{a.x * f, a.y * f, a.z * f}; }
 __device__ __forceinline__ f3 fmul(float f, f3 a) { return f3{f * a.x, f * a.y, f * a.z}; }
+#if MRT_FAST && defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ f3 divf(f3 a, float f) {
+    const float y = __builtin_amdgcn_rcpf(f);
+    return f3{a.x * y, a.y * y, a.z * y};
+}
+#else
 __device__ __forceinline__ f3 divf(f3 a, float f) { return f3{a.x / f, a.y / f, a.z / f}; }
+#endif
 __device__ __forceinline__ float dot(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 __device__ __forceinline__ float sdot(f3 a) { return (a.x * a.x + a.y * a.y) + a.z * a.z; }
 // ---- exact f32 division on a short path (tools/numcheck/markstein_check.hip) ----------------------
@@ -47,7 +62,9 @@ __device__ __forceinline__ float sdot(f3 a) { return (a.x * a.x + a.y * a.y) + a
 // tests on their operands (a ray's `nice` flag, normalize's own test) and take the IEEE division in
 // a wave-uniform branch otherwise (never taken on real scenes).
 __device__ __forceinline__ float recip_nr(float b) {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if MRT_FAST && defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcpf(b);
+#elif defined(__HIP_DEVICE_COMPILE__)
     const float y0 = __builtin_amdgcn_rcpf(b);
     return __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0);
 #else
@@ -55,6 +72,9 @@ __device__ __forceinline__ float recip_nr(float b) {
 #endif
 }
 __device__ __forceinline__ float div_core(float a, float b, float y) {
+#if MRT_FAST
+    return a * y;
+#endif
     const float q = a * y;
     const float r = __builtin_fmaf(-b, q, a);
     return __builtin_copysignf(__builtin_fmaf(r, y, q), q);
@@ -77,7 +97,9 @@ __device__ __forceinline__ uint32_t mag2(float x) { return __float_as_uint(x) <<
 // tools/numcheck/sqrt_check.hip).  (RN32(v_sqrt_f64(x)) is NOT exact: v_sqrt_f64 misrounds 3.9% of
 // f32 inputs, tools/numcheck/divsqrt_check.hip.)
 __device__ __forceinline__ float sqrt_core(float x) {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if MRT_FAST && defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_sqrtf(x);
+#elif defined(__HIP_DEVICE_COMPILE__)
     const float s = __builtin_amdgcn_sqrtf(x);
     const float sdn = __uint_as_float(__float_as_uint(s) - 1u), sup = __uint_as_float(__float_as_uint(s) + 1u);
     const float r = __builtin_fmaf(-sdn, s, x) <= 0.0f ? sdn : s;
@@ -88,6 +110,7 @@ __device__ __forceinline__ float sqrt_core(float x) {
 }
 __device__ __forceinline__ float sqrt_(float x) {
     float r = sqrt_core(x);
+    if (MRT_FAST) return r;
     const bool ok = mag2(x) - 1u >= MRT_MAG2(-96) - 1u;  // |x| >= 2^-96 or x == +-0
     if (__builtin_expect(any_lane(!ok), 0)) r = ok ? r : __builtin_sqrtf(x);
     return r;
@@ -97,6 +120,10 @@ __device__ __forceinline__ float sqrt_(float x) {
 // or normal, and y is normal).
 __device__ __forceinline__ f3 normalize(f3 a) {
     const float dd = sdot(a);
+#if MRT_FAST && defined(__HIP_DEVICE_COMPILE__)
+    const float ry = __builtin_amdgcn_rsqf(dd);
+    return f3{a.x * ry, a.y * ry, a.z * ry};
+#endif
     const float len = sqrt_core(dd);  // |a|^2 in [2^-52, 2^52): the core is exact, |a| in [2^-26, 2^26)
     const float y = recip_nr(len);
     f3 q{div_core(a.x, len, y), div_core(a.y, len, y), div_core(a.z, len, y)};
@@ -115,6 +142,24 @@ __device__ __forceinline__ bool finite3(f3 a) { return isfinite(a.x) && isfinite
 static constexpr float PI_F = 3.14159265358979323846f;
 static constexpr float FLT_MAX_ = 3.402823466e+38f;
 
+#if MRT_FAST && defined(__HIP_DEVICE_COMPILE__)
+// tolerance contract: f32 library functions; sincos of a path angle in [0, 2 pi) by the hardware
+// v_sin/v_cos (argument in revolutions), log by v_log (log2)
+__device__ __forceinline__ float sin_(float x) { return sinf(x); }
+__device__ __forceinline__ float cos_(float x) { return cosf(x); }
+__device__ __forceinline__ void sincos_(float x, float* s, float* c) {
+    const float rev = x * 0.15915494309189535f;
+    *s = __builtin_amdgcn_sinf(rev);
+    *c = __builtin_amdgcn_cosf(rev);
+}
+__device__ __forceinline__ float log_(float x) { return __builtin_amdgcn_logf(x) * 0.69314718055994531f; }
+__device__ __forceinline__ float pow5_(float x) {
+    const float x2 = x * x;
+    return (x2 * x2) * x;
+}
+__device__ __forceinline__ float atan2_(float y, float x) { return atan2f(y, x); }
+__device__ __forceinline__ float asin_(float x) { return asinf(x); }
+#else
 // transcendentals: the numerics contract of include/mrt_mathfn.h (same bits as host and oracle)
 __device__ __forceinline__ float sin_(float x) { return mrt_sinf(x); }
 __device__ __forceinline__ float cos_(float x) { return mrt_cosf(x); }
@@ -128,6 +173,7 @@ __device__ __forceinline__ float log_(float x) { return mrt_logf(x); }
 __device__ __forceinline__ float pow5_(float x) { return mrt_pow5f(x); }
 __device__ __forceinline__ float atan2_(float y, float x) { return mrt_atan2f(y, x); }
 __device__ __forceinline__ float asin_(float x) { return mrt_asinf(x); }
+#endif
 
 // ---------------------------------------------------------------- PCG32 (pcg.cpp:13-62)
 struct Pcg {
@@ -207,6 +253,7 @@ struct Ray {
 // (k - o_a) / d_a may use div_core with inv (the difference of two such coordinates -- rect planes are
 // checked on upload, MRT_F_SLOWDIV -- is 0 or >= 2^-100, and the quotient stays normal).
 __device__ __forceinline__ bool ray_nice(f3 o, f3 d) {
+    if (MRT_FAST) return true;  // no exactness guards: every ray takes the hardware reciprocal
     const bool dn = MRT_MAG_IN(d.x, -26, 1) & MRT_MAG_IN(d.y, -26, 1) & MRT_MAG_IN(d.z, -26, 1);
     const uint32_t mn = min(min(mag2(o.x) - 1u, mag2(o.y) - 1u), mag2(o.z) - 1u);  // 0 -> UINT_MAX
     const float mx = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));

@@ -1,0 +1,338 @@
+// mrt_kernels.hip -- the path kernel (DESIGN.md "Kernels"), built twice from this one source:
+//   build/obj/mrt_kernels_exact.o  MRT_FAST=0, -ffp-contract=off: the exact numerics contract,
+//                                  bit-for-bit the reference built exact (tests/golden/stream_*.npz)
+//   build/obj/mrt_kernels_fast.o   MRT_FAST=1, FMA contraction + reciprocal division + hardware
+//                                  rcp/sqrt/rsq + f32 transcendentals: the tolerance contract
+//                                  (per-pixel RMSE < 1e-3 vs the reference as shipped)
+// Each build exports its KernelTable (mrt_launch.h); the host picks one per render
+// (mrt_render_desc.flags & MRT_RF_FAST).
+//
+// mrt_path_kernel: persistent waves pull 256-path batches (64 near the end of a launch) from one
+// device counter (one atomic per wave per batch, like work_queue::getWork pulls a tile,
+// work_queue.cpp:158-166) and run trace() for each lane's path to completion; per-path radiance
+// is written sample-major [s][local pixel] (coalesced).
+#include <hip/hip_runtime.h>
+
+#include "mrt_launch.h"
+
+using namespace mrtd;
+
+#if MRT_FAST
+#define MRT_PATH_KERNEL mrt_path_kernel_fast
+#else
+#define MRT_PATH_KERNEL mrt_path_kernel
+#endif
+
+
+// Persistent waves with per-lane path regeneration: every loop iteration advances each busy lane
+// by one segment (one trace() call); a lane whose path ended takes the next path index from its
+// wave's pool at once (ballot + mbcnt compaction), and a wave refills its pool 64 paths at a time
+// with one atomic (work_queue::getWork, work_queue.cpp:158-166).  Lanes stay busy until the pool
+// runs dry instead of idling until the longest path of a 64-path batch finishes.
+// Waves per SIMD the register allocator must reach (caps VGPRs at 512/W): the path loop is
+// latency-bound, so a few spilled registers cost less than the lost occupancy.  Tuned per
+// variant on MI355X (DESIGN.md "Occupancy").
+// (compact variants -- Cornell, Cornell room + mesh, plain interpreter -- reach 80 VGPRs without
+// spills at 6; built without SLP vectorisation (Makefile), the wide-feature variants run best at
+// 4 waves (128 VGPRs) and the room + mesh variant at 7 (72 VGPRs, no LDS fold levels))
+#ifndef MRT_WPE_WIDE
+#define MRT_WPE_WIDE 4
+#endif
+#ifndef MRT_WPE_LIN
+#define MRT_WPE_LIN 6
+#endif
+#ifndef MRT_WPE_MESH
+#define MRT_WPE_MESH 7
+#endif
+template <uint32_t F> struct PathOcc {
+    static constexpr bool kWide = (F & (FT_BVHW | FT_TEX | FT_VOLUME)) != 0 || !(F & FT_LIN);
+    static constexpr int W = kWide ? MRT_WPE_WIDE : ((F & FT_MESH) != 0 ? MRT_WPE_MESH : MRT_WPE_LIN);
+};
+#if defined(MRT_EXPERIMENTS) && defined(MRT_PHASES) && !MRT_FAST
+__device__ unsigned long long g_phases[8];
+extern "C" int mrt_debug_phases(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phases), sizeof(g_phases)) != hipSuccess) return 1;
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_phases), z, sizeof(z)) != hipSuccess) return 1;
+    }
+    return 0;
+}
+#endif
+#if defined(MRT_EXPERIMENTS) && defined(MRT_WPE)  // experiment hook: override for every variant
+#define MRT_OCC(F) MRT_WPE
+#else
+#define MRT_OCC(F) PathOcc<F>::W
+#endif
+// fold levels kept in LDS per lane (the rest in HBM): where the LDS budget at the target
+// occupancy allows it
+// (Cornell: 2 at 6 WGs/CU; wide variants at 3 WGs/CU: MRT_LEVK_WIDE; room + mesh: MRT_LEVK_MESH)
+#ifndef MRT_LEVK_CORNELL
+#define MRT_LEVK_CORNELL 2u
+#endif
+#ifndef MRT_LEVK_WIDE
+#define MRT_LEVK_WIDE 2u
+#endif
+#ifndef MRT_LEVK_MESH
+#define MRT_LEVK_MESH 0u
+#endif
+template <uint32_t F> struct PathLevLds {
+    static constexpr uint32_t K = ((F & 0xFFFFu) == (FT_LIN | FT_INST)) ? MRT_LEVK_CORNELL
+                                  : PathOcc<F>::kWide                  ? MRT_LEVK_WIDE
+                                  : ((F & FT_MESH) != 0)               ? MRT_LEVK_MESH
+                                                                       : 0u;
+};
+template <uint32_t F>
+__global__ void __launch_bounds__(MRT_PATH_WG) __attribute__((amdgpu_waves_per_eu(MRT_OCC(F)))) MRT_PATH_KERNEL(PathParams P) {
+    constexpr uint32_t LK = PathLevLds<F>::K;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t words = (P.lds_frames * 2 + P.lds_rays * 11 + P.lds_mesh + P.lds_save + LK * 4) * 64;
+    uint32_t* wb = lds + wave * words;
+    uint32_t* const wmesh = wb + P.lds_frames * 128 + P.lds_rays * 704;
+    const LStack Ls{wb, (float*)(wb + P.lds_frames * 128), wmesh, (float*)(wmesh + P.lds_mesh * 64), lane};
+    const DScene& S = P.sc;
+    const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const LevStore<LK> lev{(MRT_GLOBAL_AS v4f*)P.lev, P.lev_rows, (uint32_t)slot,
+                           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)(MRT_LDS_AS uint32_t*)(wmesh + (P.lds_mesh + P.lds_save) * 64))};
+    // set bits of a wave mask below this lane (v_mbcnt: no per-lane 64-bit mask kept live)
+    auto rank_below = [](uint64_t m) -> uint32_t {
+        return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    };
+
+    // main.cpp:180/235 stop on !G_isRunning: a launch of a cancelled render does no work (mrt_render
+    // splits a cancellable render into several launches)
+    if (__hip_atomic_load(P.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return;
+    bool active = false;
+    uint32_t idx = 0;
+    PathState ps;
+    // every wave's first claim is static (wave w: paths [w*B, (w+1)*B)); the work counter hands
+    // out what follows, so a launch does not open with one atomic per wave on one address
+    // (short launches only -- P.static_first, set by the host when a wave gets fewer than 64
+    // claims: there the opening atomics are a visible share; in long launches the static batch of
+    // a wave that starts late in a pipelined step delays that launch's end)
+    const uint64_t static_paths = P.static_first ? (uint64_t)gridDim.x * (blockDim.x >> 6) * MRT_BATCH : 0;
+    uint64_t pool_next = P.static_first ? ((uint64_t)blockIdx.x * (blockDim.x >> 6) + wave) * MRT_BATCH : 0;  // wave-uniform
+    uint64_t pool_end = P.static_first ? pool_next + MRT_BATCH : 0;
+    bool exhausted = P.static_first && pool_next >= P.n_paths;
+    uint32_t done_rays = 0;
+    PhaseClock ph{};
+#ifdef MRT_PHASES
+    ph.t = __builtin_amdgcn_s_memtime();
+#endif
+    // mesh variants keep one constructor per branch: the shared-constructor loop spills there
+    // (bunny -4%, teapot -5%; Cornell +1.8%, book2 0)
+    constexpr bool kShared = (F & FT_MESH) == 0;
+    if constexpr (kShared) {
+    // One iteration: (1) every lane with a ray traces one segment; a path that ends is folded and
+    // stored; (2) lanes without a path take new ones (camera ray arguments); (3) ONE make_ray for
+    // every lane with a next ray -- camera and scattered rays alike, instead of one constructor per
+    // branch at partial lane occupancy; (4) diffuse scatters finish their pdfs on the new ray.
+    PendRay pr;
+    for (;;) {
+        bool want_ray = false;
+        if (active) {
+            f3 L;
+            const bool ended = trace_split<F, LK>(S, ps, P.max_bounces, lev, Ls, &L, &pr, ph);
+            PH_MARK(ph, 2);
+            if (ended) {
+                L = fold_levels(lev, ps.nlev, L);
+                PH_MARK(ph, 5);
+                float* dst = P.rad + (size_t)idx * 3;
+                dst[0] = L.x;
+                dst[1] = L.y;
+                dst[2] = L.z;
+                if (P.path_rays) P.path_rays[idx] = ps.rays;
+                done_rays += ps.rays;
+                active = false;
+            } else {
+                want_ray = true;
+            }
+        }
+        PH_MARK(ph, 3);
+        const uint64_t need = __ballot(!active);
+        if (need && !exhausted) {
+            const uint32_t c = (uint32_t)__popcll(need);
+            const uint32_t have = (uint32_t)(pool_end - pool_next);
+            // near the end of the launch, claims shrink so the last ones finish together
+            const uint32_t batch = pool_end + P.tail_zone >= P.n_paths ? MRT_TAIL_BATCH : MRT_BATCH;
+            uint64_t nb = 0;
+            if (have < c) {
+                if (lane == 0) {
+                    nb = static_paths + atomicAdd(P.counter, (unsigned long long)batch);
+                    // every 32nd claim: a system-scope store to host memory, read by mrt_progress
+                    // without any GPU queue (a device-to-host copy could wait behind this launch)
+                    if (P.hprog && ((nb / MRT_BATCH) & 31u) == 0)
+                        __hip_atomic_store(P.hprog, nb + batch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+                nb = __shfl(nb, 0);
+            }
+            PH_MARK(ph, 0);
+            if (!active) {
+                const uint32_t rank = rank_below(need);
+                const uint64_t i = rank < have ? pool_next + rank : nb + (rank - have);
+                if (i < P.n_paths) {
+                    idx = (uint32_t)i;
+                    // idx = sl * npix + lp; the double estimate is off by at most one either way
+                    uint32_t sl = (uint32_t)((double)idx * P.inv_npix);
+                    uint32_t lp = idx - sl * P.npix;
+                    if ((int32_t)lp < 0) { sl--; lp += P.npix; }
+                    if (lp >= P.npix) { sl++; lp -= P.npix; }
+                    const uint32_t s = P.s0 + sl;
+                    const uint2 xy = P.pixels[lp];
+                    const uint32_t x = xy.x, y = xy.y;
+                    const uint32_t pix = x + y * P.width;
+                    const float2 dd = P.sdist[s];  // ((i + 0.5) / sq, (j + 0.5) / sq), s = i*sq + j
+                    // (x + dx) / W with RN(1/W) from the host: numerator >= 1/(2 sq) >= 2^-17, W <= 2^24
+                    const float nu = (float)x + dd.x, nv = (float)y + dd.y;
+                    float u = div_core(nu, (float)P.width, P.inv_w), v = div_core(nv, (float)P.height, P.inv_h);
+                    if (!P.fast_uv) {  // a real (uniform) branch: the barrier keeps it from being if-converted
+                        asm volatile("" ::: "memory");
+                        u = nu / (float)P.width;
+                        v = nv / (float)P.height;
+                    }
+                    const uint64_t path_id = (uint64_t)pix * P.ns + s;
+                    pcg_seed(ps.rng, splitmix64(P.seed ^ path_id), path_id);
+                    camera_ray_args(S, ps.rng, u, v, &pr.o, &pr.dir, &pr.time);
+                    pr.inside = 0;
+                    pr.kind = 0;
+                    want_ray = true;
+                    ps.depth = 0;
+                    ps.nlev = 0;
+                    ps.rays = 0;
+                    active = true;
+                }
+            }
+            PH_MARK(ph, 4);
+            if (have < c) {
+                pool_next = nb + (c - have);
+                pool_end = nb + batch;
+                if (nb >= P.n_paths) exhausted = true;
+            } else {
+                pool_next += c;
+            }
+            if (pool_next >= P.n_paths) exhausted = true;
+        }
+        if (!__any(active)) break;
+        PH_MARK(ph, 0);
+        if (want_ray) {
+            ps.r = make_ray(pr.o, pr.dir, pr.time, pr.inside);
+            if (pr.kind) finish_scatter<F, LK>(S, ps, lev, pr);
+        }
+        PH_MARK(ph, 7);
+    }
+    } else {
+    for (;;) {
+        const uint64_t need = __ballot(!active);
+        if (need && !exhausted) {
+            const uint32_t c = (uint32_t)__popcll(need);
+            const uint32_t have = (uint32_t)(pool_end - pool_next);
+            // near the end of the launch, claims shrink so the last ones finish together
+            const uint32_t batch = pool_end + P.tail_zone >= P.n_paths ? MRT_TAIL_BATCH : MRT_BATCH;
+            uint64_t nb = 0;
+            if (have < c) {
+                if (lane == 0) {
+                    nb = static_paths + atomicAdd(P.counter, (unsigned long long)batch);
+                    // every 32nd claim: a system-scope store to host memory, read by mrt_progress
+                    // without any GPU queue (a device-to-host copy could wait behind this launch)
+                    if (P.hprog && ((nb / MRT_BATCH) & 31u) == 0)
+                        __hip_atomic_store(P.hprog, nb + batch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+                nb = __shfl(nb, 0);
+            }
+            PH_MARK(ph, 0);
+            if (!active) {
+                const uint32_t rank = rank_below(need);
+                const uint64_t i = rank < have ? pool_next + rank : nb + (rank - have);
+                if (i < P.n_paths) {
+                    idx = (uint32_t)i;
+                    // idx = sl * npix + lp; the double estimate is off by at most one either way
+                    uint32_t sl = (uint32_t)((double)idx * P.inv_npix);
+                    uint32_t lp = idx - sl * P.npix;
+                    if ((int32_t)lp < 0) { sl--; lp += P.npix; }
+                    if (lp >= P.npix) { sl++; lp -= P.npix; }
+                    const uint32_t s = P.s0 + sl;
+                    const uint2 xy = P.pixels[lp];
+                    const uint32_t x = xy.x, y = xy.y;
+                    const uint32_t pix = x + y * P.width;
+                    const float2 dd = P.sdist[s];  // ((i + 0.5) / sq, (j + 0.5) / sq), s = i*sq + j
+                    // (x + dx) / W with RN(1/W) from the host: numerator >= 1/(2 sq) >= 2^-17, W <= 2^24
+                    const float nu = (float)x + dd.x, nv = (float)y + dd.y;
+                    float u = div_core(nu, (float)P.width, P.inv_w), v = div_core(nv, (float)P.height, P.inv_h);
+                    if (!P.fast_uv) {  // a real (uniform) branch: the barrier keeps it from being if-converted
+                        asm volatile("" ::: "memory");
+                        u = nu / (float)P.width;
+                        v = nv / (float)P.height;
+                    }
+                    const uint64_t path_id = (uint64_t)pix * P.ns + s;
+                    pcg_seed(ps.rng, splitmix64(P.seed ^ path_id), path_id);
+                    ps.r = camera_ray(S, ps.rng, u, v);
+                    ps.depth = 0;
+                    ps.nlev = 0;
+                    ps.rays = 0;
+                    active = true;
+                }
+            }
+            PH_MARK(ph, 4);
+            if (have < c) {
+                pool_next = nb + (c - have);
+                pool_end = nb + batch;
+                if (nb >= P.n_paths) exhausted = true;
+            } else {
+                pool_next += c;
+            }
+            if (pool_next >= P.n_paths) exhausted = true;
+        }
+        if (!__any(active)) break;
+        PH_MARK(ph, 0);
+        if (active) {
+            f3 L;
+            const bool ended = trace_segment<F, LK>(S, ps, P.max_bounces, lev, Ls, &L, ph);
+            PH_MARK(ph, 2);
+            if (ended) {
+                L = fold_levels(lev, ps.nlev, L);
+                PH_MARK(ph, 5);
+                float* dst = P.rad + (size_t)idx * 3;
+                dst[0] = L.x;
+                dst[1] = L.y;
+                dst[2] = L.z;
+                if (P.path_rays) P.path_rays[idx] = ps.rays;
+                done_rays += ps.rays;
+                active = false;
+            }
+        }
+        PH_MARK(ph, 3);
+    }
+}
+#ifdef MRT_PHASES
+    if (lane == 0)
+        for (int i = 0; i < 8; i++) atomicAdd(&g_phases[i], (unsigned long long)ph.a[i]);
+#endif
+    // one 64-bit add per wave
+    uint64_t my = done_rays;
+    for (int off = 32; off > 0; off >>= 1) my += __shfl_xor(my, off);
+    if (lane == 0 && my) atomicAdd(P.rays, (unsigned long long)my);
+}
+
+template <uint32_t F>
+static constexpr path_kernel_t kfn() {
+    return MRT_PATH_KERNEL<F>;
+}
+
+#if MRT_FAST
+const KernelTable& mrtd::kernel_table_fast() {
+    static const KernelTable t = {
+        "fast",
+#else
+const KernelTable& mrtd::kernel_table_exact() {
+    static const KernelTable t = {
+        "exact",
+#endif
+        {kfn<kVariants[0]>(), kfn<kVariants[1]>(), kfn<kVariants[2]>(), kfn<kVariants[3]>(), kfn<kVariants[4]>(),
+         kfn<kVariants[5]>(), kfn<kVariants[6]>()},
+        {PathLevLds<kVariants[0]>::K, PathLevLds<kVariants[1]>::K, PathLevLds<kVariants[2]>::K, PathLevLds<kVariants[3]>::K,
+         PathLevLds<kVariants[4]>::K, PathLevLds<kVariants[5]>::K, PathLevLds<kVariants[6]>::K}};
+    static_assert(kNumVariants == 7, "one table entry per variant");
+    return t;
+}

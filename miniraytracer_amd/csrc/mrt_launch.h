@@ -1,0 +1,75 @@
+// mrt_launch.h -- the interface between the host code (mrt_render.hip) and the path-kernel
+// translation unit (mrt_kernels.hip), which is compiled twice: once under the exact numerics
+// contract (MRT_FAST=0, -ffp-contract=off) and once under the tolerance contract (MRT_FAST=1,
+// FMA contraction, hardware reciprocal/sqrt, f32 transcendentals).  DESIGN.md "Numerics contracts".
+#pragma once
+#include <hip/hip_runtime.h>
+#include "mrt_shade.h"
+
+namespace mrtd {
+
+struct PathParams {
+    DScene sc;                            // by value: kernarg (constant) memory, scalar-loaded
+    const uint2* __restrict__ pixels;     // local pixel -> (x, y), row 0 = bottom
+    const float2* __restrict__ sdist;     // sample s -> grid offsets (main.cpp:324-331)
+    uint32_t npix;                        // local pixel count
+    double inv_npix;                      // 1.0 / npix (path index -> sample row without a divide)
+    uint32_t width, height, sq, ns;
+    float inv_w, inv_h;                   // RN(1/width), RN(1/height)
+    uint32_t fast_uv;                     // width, height <= 2^24 and sq <= 2^16: u, v through div_core
+    uint32_t s0;                          // first sample of this chunk
+    uint32_t n_paths;                     // npix * chunk samples (< 2^32, enforced on the host)
+    uint32_t tail_zone;                   // last paths of the launch handed out MRT_TAIL_BATCH at a time
+    uint32_t static_first;                // every wave's first claim is static (short launches)
+    uint64_t seed;
+    uint32_t max_bounces;
+    float* __restrict__ rad;              // n_paths * 3 floats, [s - s0][lp]
+    uint32_t* __restrict__ path_rays;     // optional (debug): n_paths
+    unsigned long long* __restrict__ counter;  // work counter (paths handed out)
+    unsigned long long* hprog;            // host-coherent pinned snapshot of `counter` (mrt_progress), or null
+    const int* cancel;                    // device flag: non-zero makes the launch exit (G_isRunning)
+    unsigned long long* __restrict__ rays;
+    float4* __restrict__ lev;             // fold levels, lane-major: [slot][lev_rows]
+    uint32_t lev_rows;                    // levels per lane (max_bounces, at least 1)
+    uint32_t lds_frames, lds_rays, lds_mesh, lds_save;  // LDS stack slots / words per lane
+};
+
+typedef void (*path_kernel_t)(PathParams);
+
+// threads per path-kernel workgroup (each wave owns its own LDS slice; a smaller group frees its
+// CU slot as soon as its own waves finish, which matters in a launch's tail)
+#ifndef MRT_PATH_WG
+#define MRT_PATH_WG 64
+#endif
+static constexpr uint32_t kWavesPerWG = MRT_PATH_WG / 64;
+#ifndef MRT_BATCH
+#define MRT_BATCH 256u  // paths a wave claims per atomic on the work counter (one hot address)
+#endif
+#ifndef MRT_TAIL_BATCH
+#define MRT_TAIL_BATCH 64u  // claim size within the last `tail_zone` paths of a launch
+#endif
+// one claim must cover a whole wave's idle lanes (the pool hands out at most 64 at once)
+static_assert(MRT_TAIL_BATCH >= 64u && MRT_BATCH >= MRT_TAIL_BATCH, "claims must be at least a wave wide");
+
+// kernel variants by scene features (the first instantiated superset is launched); FT_LIN
+// variants need the scene's linear hit program (mrt_lin.h), FT_ALL runs any graph.  The same list
+// in both numerics builds.
+static constexpr uint32_t kVariants[] = {FT_LIN | FT_INST | MRT_SIG_BITS(SIG_CORNELL),
+                                         FT_LIN | FT_MESH | FT_METAL | MRT_SIG_BITS(SIG_ROOM_MESH),
+                                         FT_LIN | FT_INST,
+                                         FT_LIN | FT_MESH | FT_METAL,
+                                         FT_LIN | FT_BVHW | FT_TEX | FT_METAL | FT_MOVING | FT_SKY | FT_UV,
+                                         FT_LIN | FT_ALL,
+                                         FT_ALL};
+static constexpr uint32_t kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+
+// One numerics build of the path kernels: a kernel per variant and the LDS fold levels it keeps.
+struct KernelTable {
+    const char* numerics;  // "exact" | "fast"
+    path_kernel_t kernel[kNumVariants];
+    uint32_t lev_k[kNumVariants];
+};
+const KernelTable& kernel_table_exact();
+const KernelTable& kernel_table_fast();
+
+}  // namespace mrtd

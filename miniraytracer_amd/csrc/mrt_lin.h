@@ -75,7 +75,7 @@ __device__ __forceinline__ bool lin_prim_t(const OP& o, const Ray& r, float tmin
         // dot(dir, n) > 0 reduces to d_a * ns > 0 (the other products are zeros of finite values)
         float t = div_core(num, da, ia);
         bool back = da * ns > 0.0f;
-        const bool slow = (op_flags(o) & MRT_F_SLOWDIV) != 0;  // uniform
+        const bool slow = !MRT_FAST && (op_flags(o) & MRT_F_SLOWDIV) != 0;  // uniform
         if (__builtin_expect(slow || any_lane(!r.nice), 0)) {  // the reference's forms
             const float dn = AX == 2 ? (r.d.x * 0.0f + r.d.y * 0.0f) + r.d.z * ns
                            : AX == 1 ? (r.d.x * 0.0f + r.d.y * ns) + r.d.z * 0.0f

@@ -12,6 +12,7 @@
 //                     output in local-pixel order.
 #include <hip/hip_runtime.h>
 #include <atomic>
+#include <mutex>
 
 #include <algorithm>
 #include <functional>
@@ -22,7 +23,7 @@
 #include <unistd.h>
 
 #include "mrt_internal.h"
-#include "mrt_shade.h"
+#include "mrt_launch.h"
 #include "../../include/mrt_tonemap.h"
 
 using namespace mrtd;
@@ -33,367 +34,6 @@ using namespace mrtd;
         if (e_ != hipSuccess) return mrt_internal_fail(MRT_ERR_HIP, (std::string(#x) + ": " + hipGetErrorString(e_)).c_str()); \
     } while (0)
 
-struct PathParams {
-    DScene sc;                            // by value: kernarg (constant) memory, scalar-loaded
-    const uint2* __restrict__ pixels;     // local pixel -> (x, y), row 0 = bottom
-    const float2* __restrict__ sdist;     // sample s -> grid offsets (main.cpp:324-331)
-    uint32_t npix;                        // local pixel count
-    double inv_npix;                      // 1.0 / npix (path index -> sample row without a divide)
-    uint32_t width, height, sq, ns;
-    float inv_w, inv_h;                   // RN(1/width), RN(1/height)
-    uint32_t fast_uv;                     // width, height <= 2^24 and sq <= 2^16: u, v through div_core
-    uint32_t s0;                          // first sample of this chunk
-    uint32_t n_paths;                     // npix * chunk samples (< 2^32, enforced on the host)
-    uint32_t tail_zone;                   // last paths of the launch handed out MRT_TAIL_BATCH at a time
-    uint32_t static_first;                // every wave's first claim is static (short launches)
-    uint64_t seed;
-    uint32_t max_bounces;
-    float* __restrict__ rad;              // n_paths * 3 floats, [s - s0][lp]
-    uint32_t* __restrict__ path_rays;     // optional (debug): n_paths
-    unsigned long long* __restrict__ counter;  // work counter (paths handed out)
-    unsigned long long* hprog;            // host-coherent pinned snapshot of `counter` (mrt_progress), or null
-    const int* cancel;                    // device flag: non-zero makes the launch exit (G_isRunning)
-    unsigned long long* __restrict__ rays;
-    float4* __restrict__ lev;             // fold levels, lane-major: [slot][lev_rows]
-    uint32_t lev_rows;                    // levels per lane (max_bounces, at least 1)
-    uint32_t lds_frames, lds_rays, lds_mesh, lds_save;  // LDS stack slots / words per lane
-};
-
-// Persistent waves with per-lane path regeneration: every loop iteration advances each busy lane
-// by one segment (one trace() call); a lane whose path ended takes the next path index from its
-// wave's pool at once (ballot + mbcnt compaction), and a wave refills its pool 64 paths at a time
-// with one atomic (work_queue::getWork, work_queue.cpp:158-166).  Lanes stay busy until the pool
-// runs dry instead of idling until the longest path of a 64-path batch finishes.
-// Waves per SIMD the register allocator must reach (caps VGPRs at 512/W): the path loop is
-// latency-bound, so a few spilled registers cost less than the lost occupancy.  Tuned per
-// variant on MI355X (DESIGN.md "Occupancy").
-// (compact variants -- Cornell, Cornell room + mesh, plain interpreter -- reach 80 VGPRs without
-// spills at 6; built without SLP vectorisation (Makefile), the wide-feature variants run best at
-// 4 waves (128 VGPRs) and the room + mesh variant at 7 (72 VGPRs, no LDS fold levels))
-// threads per path-kernel workgroup (each wave owns its own LDS slice; a smaller group frees its
-// CU slot as soon as its own waves finish, which matters in a launch's tail)
-#ifndef MRT_PATH_WG
-#define MRT_PATH_WG 64
-#endif
-static constexpr uint32_t kWavesPerWG = MRT_PATH_WG / 64;
-#ifndef MRT_WPE_WIDE
-#define MRT_WPE_WIDE 4
-#endif
-#ifndef MRT_WPE_LIN
-#define MRT_WPE_LIN 6
-#endif
-#ifndef MRT_WPE_MESH
-#define MRT_WPE_MESH 7
-#endif
-template <uint32_t F> struct PathOcc {
-    static constexpr bool kWide = (F & (FT_BVHW | FT_TEX | FT_VOLUME)) != 0 || !(F & FT_LIN);
-    static constexpr int W = kWide ? MRT_WPE_WIDE : ((F & FT_MESH) != 0 ? MRT_WPE_MESH : MRT_WPE_LIN);
-};
-#ifndef MRT_BATCH
-#define MRT_BATCH 256u  // paths a wave claims per atomic on the work counter (one hot address)
-#endif
-#ifndef MRT_TAIL_BATCH
-#define MRT_TAIL_BATCH 64u  // claim size within the last `tail_zone` paths of a launch
-#endif
-// one claim must cover a whole wave's idle lanes (the pool hands out at most 64 at once)
-static_assert(MRT_TAIL_BATCH >= 64u && MRT_BATCH >= MRT_TAIL_BATCH, "claims must be at least a wave wide");
-#ifdef MRT_PHASES
-__device__ unsigned long long g_phases[8];
-extern "C" int mrt_debug_phases(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phases), sizeof(g_phases)) != hipSuccess) return 1;
-    if (reset) {
-        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_phases), z, sizeof(z)) != hipSuccess) return 1;
-    }
-    return 0;
-}
-#endif
-#ifdef MRT_WPE  // experiment hook: override for every variant
-#define MRT_OCC(F) MRT_WPE
-#else
-#define MRT_OCC(F) PathOcc<F>::W
-#endif
-// fold levels kept in LDS per lane (the rest in HBM): where the LDS budget at the target
-// occupancy allows it
-// (Cornell: 2 at 6 WGs/CU; wide variants at 3 WGs/CU: MRT_LEVK_WIDE; room + mesh: MRT_LEVK_MESH)
-#ifndef MRT_LEVK_CORNELL
-#define MRT_LEVK_CORNELL 2u
-#endif
-#ifndef MRT_LEVK_WIDE
-#define MRT_LEVK_WIDE 2u
-#endif
-#ifndef MRT_LEVK_MESH
-#define MRT_LEVK_MESH 0u
-#endif
-template <uint32_t F> struct PathLevLds {
-    static constexpr uint32_t K = ((F & 0xFFFFu) == (FT_LIN | FT_INST)) ? MRT_LEVK_CORNELL
-                                  : PathOcc<F>::kWide                  ? MRT_LEVK_WIDE
-                                  : ((F & FT_MESH) != 0)               ? MRT_LEVK_MESH
-                                                                       : 0u;
-};
-template <uint32_t F>
-__global__ void __launch_bounds__(MRT_PATH_WG) __attribute__((amdgpu_waves_per_eu(MRT_OCC(F)))) mrt_path_kernel(PathParams P) {
-    constexpr uint32_t LK = PathLevLds<F>::K;
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t words = (P.lds_frames * 2 + P.lds_rays * 11 + P.lds_mesh + P.lds_save + LK * 4) * 64;
-    uint32_t* wb = lds + wave * words;
-    uint32_t* const wmesh = wb + P.lds_frames * 128 + P.lds_rays * 704;
-    const LStack Ls{wb, (float*)(wb + P.lds_frames * 128), wmesh, (float*)(wmesh + P.lds_mesh * 64), lane};
-    const DScene& S = P.sc;
-    const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const LevStore<LK> lev{(MRT_GLOBAL_AS v4f*)P.lev, P.lev_rows, (uint32_t)slot,
-                           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)(MRT_LDS_AS uint32_t*)(wmesh + (P.lds_mesh + P.lds_save) * 64))};
-    // set bits of a wave mask below this lane (v_mbcnt: no per-lane 64-bit mask kept live)
-    auto rank_below = [](uint64_t m) -> uint32_t {
-        return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    };
-
-    // main.cpp:180/235 stop on !G_isRunning: a launch of a cancelled render does no work (mrt_render
-    // splits a cancellable render into several launches)
-    if (__hip_atomic_load(P.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return;
-    bool active = false;
-    uint32_t idx = 0;
-    PathState ps;
-    // every wave's first claim is static (wave w: paths [w*B, (w+1)*B)); the work counter hands
-    // out what follows, so a launch does not open with one atomic per wave on one address
-    // (short launches only -- P.static_first, set by the host when a wave gets fewer than 64
-    // claims: there the opening atomics are a visible share; in long launches the static batch of
-    // a wave that starts late in a pipelined step delays that launch's end)
-    const uint64_t static_paths = P.static_first ? (uint64_t)gridDim.x * (blockDim.x >> 6) * MRT_BATCH : 0;
-    uint64_t pool_next = P.static_first ? ((uint64_t)blockIdx.x * (blockDim.x >> 6) + wave) * MRT_BATCH : 0;  // wave-uniform
-    uint64_t pool_end = P.static_first ? pool_next + MRT_BATCH : 0;
-    bool exhausted = P.static_first && pool_next >= P.n_paths;
-    uint32_t done_rays = 0;
-    PhaseClock ph{};
-#ifdef MRT_PHASES
-    ph.t = __builtin_amdgcn_s_memtime();
-#endif
-    // mesh variants keep one constructor per branch: the shared-constructor loop spills there
-    // (bunny -4%, teapot -5%; Cornell +1.8%, book2 0)
-    constexpr bool kShared = (F & FT_MESH) == 0;
-    if constexpr (kShared) {
-    // One iteration: (1) every lane with a ray traces one segment; a path that ends is folded and
-    // stored; (2) lanes without a path take new ones (camera ray arguments); (3) ONE make_ray for
-    // every lane with a next ray -- camera and scattered rays alike, instead of one constructor per
-    // branch at partial lane occupancy; (4) diffuse scatters finish their pdfs on the new ray.
-    PendRay pr;
-    for (;;) {
-        bool want_ray = false;
-        if (active) {
-            f3 L;
-            const bool ended = trace_split<F, LK>(S, ps, P.max_bounces, lev, Ls, &L, &pr, ph);
-            PH_MARK(ph, 2);
-            if (ended) {
-                L = fold_levels(lev, ps.nlev, L);
-                PH_MARK(ph, 5);
-                float* dst = P.rad + (size_t)idx * 3;
-                dst[0] = L.x;
-                dst[1] = L.y;
-                dst[2] = L.z;
-                if (P.path_rays) P.path_rays[idx] = ps.rays;
-                done_rays += ps.rays;
-                active = false;
-            } else {
-                want_ray = true;
-            }
-        }
-        PH_MARK(ph, 3);
-        const uint64_t need = __ballot(!active);
-        if (need && !exhausted) {
-            const uint32_t c = (uint32_t)__popcll(need);
-            const uint32_t have = (uint32_t)(pool_end - pool_next);
-            // near the end of the launch, claims shrink so the last ones finish together
-            const uint32_t batch = pool_end + P.tail_zone >= P.n_paths ? MRT_TAIL_BATCH : MRT_BATCH;
-            uint64_t nb = 0;
-            if (have < c) {
-                if (lane == 0) {
-                    nb = static_paths + atomicAdd(P.counter, (unsigned long long)batch);
-                    // every 32nd claim: a system-scope store to host memory, read by mrt_progress
-                    // without any GPU queue (a device-to-host copy could wait behind this launch)
-                    if (P.hprog && ((nb / MRT_BATCH) & 31u) == 0)
-                        __hip_atomic_store(P.hprog, nb + batch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                }
-                nb = __shfl(nb, 0);
-            }
-            PH_MARK(ph, 0);
-            if (!active) {
-                const uint32_t rank = rank_below(need);
-                const uint64_t i = rank < have ? pool_next + rank : nb + (rank - have);
-                if (i < P.n_paths) {
-                    idx = (uint32_t)i;
-                    // idx = sl * npix + lp; the double estimate is off by at most one either way
-                    uint32_t sl = (uint32_t)((double)idx * P.inv_npix);
-                    uint32_t lp = idx - sl * P.npix;
-                    if ((int32_t)lp < 0) { sl--; lp += P.npix; }
-                    if (lp >= P.npix) { sl++; lp -= P.npix; }
-                    const uint32_t s = P.s0 + sl;
-                    const uint2 xy = P.pixels[lp];
-                    const uint32_t x = xy.x, y = xy.y;
-                    const uint32_t pix = x + y * P.width;
-                    const float2 dd = P.sdist[s];  // ((i + 0.5) / sq, (j + 0.5) / sq), s = i*sq + j
-                    // (x + dx) / W with RN(1/W) from the host: numerator >= 1/(2 sq) >= 2^-17, W <= 2^24
-                    const float nu = (float)x + dd.x, nv = (float)y + dd.y;
-                    float u = div_core(nu, (float)P.width, P.inv_w), v = div_core(nv, (float)P.height, P.inv_h);
-                    if (!P.fast_uv) {  // a real (uniform) branch: the barrier keeps it from being if-converted
-                        asm volatile("" ::: "memory");
-                        u = nu / (float)P.width;
-                        v = nv / (float)P.height;
-                    }
-                    const uint64_t path_id = (uint64_t)pix * P.ns + s;
-                    pcg_seed(ps.rng, splitmix64(P.seed ^ path_id), path_id);
-                    camera_ray_args(S, ps.rng, u, v, &pr.o, &pr.dir, &pr.time);
-                    pr.inside = 0;
-                    pr.kind = 0;
-                    want_ray = true;
-                    ps.depth = 0;
-                    ps.nlev = 0;
-                    ps.rays = 0;
-                    active = true;
-                }
-            }
-            PH_MARK(ph, 4);
-            if (have < c) {
-                pool_next = nb + (c - have);
-                pool_end = nb + batch;
-                if (nb >= P.n_paths) exhausted = true;
-            } else {
-                pool_next += c;
-            }
-            if (pool_next >= P.n_paths) exhausted = true;
-        }
-        if (!__any(active)) break;
-        PH_MARK(ph, 0);
-        if (want_ray) {
-            ps.r = make_ray(pr.o, pr.dir, pr.time, pr.inside);
-            if (pr.kind) finish_scatter<F, LK>(S, ps, lev, pr);
-        }
-        PH_MARK(ph, 7);
-    }
-    } else {
-    for (;;) {
-        const uint64_t need = __ballot(!active);
-        if (need && !exhausted) {
-            const uint32_t c = (uint32_t)__popcll(need);
-            const uint32_t have = (uint32_t)(pool_end - pool_next);
-            // near the end of the launch, claims shrink so the last ones finish together
-            const uint32_t batch = pool_end + P.tail_zone >= P.n_paths ? MRT_TAIL_BATCH : MRT_BATCH;
-            uint64_t nb = 0;
-            if (have < c) {
-                if (lane == 0) {
-                    nb = static_paths + atomicAdd(P.counter, (unsigned long long)batch);
-                    // every 32nd claim: a system-scope store to host memory, read by mrt_progress
-                    // without any GPU queue (a device-to-host copy could wait behind this launch)
-                    if (P.hprog && ((nb / MRT_BATCH) & 31u) == 0)
-                        __hip_atomic_store(P.hprog, nb + batch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                }
-                nb = __shfl(nb, 0);
-            }
-            PH_MARK(ph, 0);
-            if (!active) {
-                const uint32_t rank = rank_below(need);
-                const uint64_t i = rank < have ? pool_next + rank : nb + (rank - have);
-                if (i < P.n_paths) {
-                    idx = (uint32_t)i;
-                    // idx = sl * npix + lp; the double estimate is off by at most one either way
-                    uint32_t sl = (uint32_t)((double)idx * P.inv_npix);
-                    uint32_t lp = idx - sl * P.npix;
-                    if ((int32_t)lp < 0) { sl--; lp += P.npix; }
-                    if (lp >= P.npix) { sl++; lp -= P.npix; }
-                    const uint32_t s = P.s0 + sl;
-                    const uint2 xy = P.pixels[lp];
-                    const uint32_t x = xy.x, y = xy.y;
-                    const uint32_t pix = x + y * P.width;
-                    const float2 dd = P.sdist[s];  // ((i + 0.5) / sq, (j + 0.5) / sq), s = i*sq + j
-                    // (x + dx) / W with RN(1/W) from the host: numerator >= 1/(2 sq) >= 2^-17, W <= 2^24
-                    const float nu = (float)x + dd.x, nv = (float)y + dd.y;
-                    float u = div_core(nu, (float)P.width, P.inv_w), v = div_core(nv, (float)P.height, P.inv_h);
-                    if (!P.fast_uv) {  // a real (uniform) branch: the barrier keeps it from being if-converted
-                        asm volatile("" ::: "memory");
-                        u = nu / (float)P.width;
-                        v = nv / (float)P.height;
-                    }
-                    const uint64_t path_id = (uint64_t)pix * P.ns + s;
-                    pcg_seed(ps.rng, splitmix64(P.seed ^ path_id), path_id);
-                    ps.r = camera_ray(S, ps.rng, u, v);
-                    ps.depth = 0;
-                    ps.nlev = 0;
-                    ps.rays = 0;
-                    active = true;
-                }
-            }
-            PH_MARK(ph, 4);
-            if (have < c) {
-                pool_next = nb + (c - have);
-                pool_end = nb + batch;
-                if (nb >= P.n_paths) exhausted = true;
-            } else {
-                pool_next += c;
-            }
-            if (pool_next >= P.n_paths) exhausted = true;
-        }
-        if (!__any(active)) break;
-        PH_MARK(ph, 0);
-        if (active) {
-            f3 L;
-            const bool ended = trace_segment<F, LK>(S, ps, P.max_bounces, lev, Ls, &L, ph);
-            PH_MARK(ph, 2);
-            if (ended) {
-                L = fold_levels(lev, ps.nlev, L);
-                PH_MARK(ph, 5);
-                float* dst = P.rad + (size_t)idx * 3;
-#ifdef MRT_EXP_NOSTORE
-                if (L.x == 12345.0f)
-#endif
-                {
-                dst[0] = L.x;
-                dst[1] = L.y;
-                dst[2] = L.z;
-                }
-                if (P.path_rays) P.path_rays[idx] = ps.rays;
-                done_rays += ps.rays;
-                active = false;
-            }
-        }
-        PH_MARK(ph, 3);
-    }
-}
-#ifdef MRT_PHASES
-    if (lane == 0)
-        for (int i = 0; i < 8; i++) atomicAdd(&g_phases[i], (unsigned long long)ph.a[i]);
-#endif
-    // one 64-bit add per wave
-    uint64_t my = done_rays;
-    for (int off = 32; off > 0; off >>= 1) my += __shfl_xor(my, off);
-    if (lane == 0 && my) atomicAdd(P.rays, (unsigned long long)my);
-}
-
-// kernel variants by scene features (the first instantiated superset is launched); FT_LIN
-// variants need the scene's linear hit program (mrt_lin.h), FT_ALL runs any graph
-static constexpr uint32_t kVariants[] = {FT_LIN | FT_INST | MRT_SIG_BITS(SIG_CORNELL),
-                                         FT_LIN | FT_MESH | FT_METAL | MRT_SIG_BITS(SIG_ROOM_MESH),
-                                         FT_LIN | FT_INST,
-                                         FT_LIN | FT_MESH | FT_METAL,
-                                         FT_LIN | FT_BVHW | FT_TEX | FT_METAL | FT_MOVING | FT_SKY | FT_UV,
-                                         FT_LIN | FT_ALL,
-                                         FT_ALL};
-static constexpr uint32_t kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
-typedef void (*path_kernel_t)(PathParams);
-static path_kernel_t kernel_for(uint32_t v) {
-    switch (v) {
-    case 0: return mrt_path_kernel<kVariants[0]>;
-    case 1: return mrt_path_kernel<kVariants[1]>;
-    case 2: return mrt_path_kernel<kVariants[2]>;
-    case 3: return mrt_path_kernel<kVariants[3]>;
-    case 4: return mrt_path_kernel<kVariants[4]>;
-    case 5: return mrt_path_kernel<kVariants[5]>;
-    default: return mrt_path_kernel<kVariants[6]>;
-    }
-}
-static constexpr uint32_t kLevK[] = {PathLevLds<kVariants[0]>::K, PathLevLds<kVariants[1]>::K, PathLevLds<kVariants[2]>::K,
-                                     PathLevLds<kVariants[3]>::K, PathLevLds<kVariants[4]>::K, PathLevLds<kVariants[5]>::K,
-                                     PathLevLds<kVariants[6]>::K};
 // first variant covering the scene's features: its own program shape first, then the interpreter
 static uint32_t pick_variant(uint32_t features) {
     const uint32_t feat = features & 0xFFFFu, sig = MRT_SIG_OF(features);
@@ -510,6 +150,14 @@ extern "C" mrt_status mrt_tonemap_device(const float* d_rgb, uint32_t n, const f
 // --------------------------------------------------------------------------------------------
 // host side
 // --------------------------------------------------------------------------------------------
+// one numerics build of the scene's path kernel (exact / fast): kernel, grid, registers
+struct PathLaunch {
+    path_kernel_t fn = nullptr;
+    int grid = 0;
+    size_t lds_bytes = 0;
+    uint32_t vgprs = 0;
+};
+
 struct mrt_scene {
     int device = 0;
     DScene S{};
@@ -527,31 +175,39 @@ struct mrt_scene {
     uint32_t* d_path_rays = nullptr;
     float4* d_acc = nullptr;
     float4* d_lev = nullptr;
+    float4* d_out = nullptr;         // mrt_render's device framebuffer (local-pixel order)
     uint32_t lev_rows = 0;
-    uint64_t* d_counter = nullptr;   // 64 B scratch: [0] unused, [2] ray total of mrt_render
+    uint64_t* d_counter = nullptr;   // 64 B scratch: [0] unused, [2] ray total of mrt_render, [4] cancel flag
     uint64_t* d_counters = nullptr;  // one work counter per chunk launch (progress reads them)
     size_t cnt_cap = 0;
     std::vector<uint64_t> chunk_paths;
-    hipStream_t pstream = nullptr;   // non-blocking stream for progress reads
+    hipStream_t pstream = nullptr;   // non-blocking stream for the cancel-flag copy
     // host-coherent pinned memory: per-launch snapshots of the work counters, stored by the path
     // kernel itself (mrt_progress reads them with no GPU work), and the cancel flag's source
     uint64_t* h_prog = nullptr;
     size_t h_prog_cap = 0;
     std::vector<uint64_t> h_seen;  // largest snapshot read per launch (waves store out of order)
     int* h_one = nullptr;
-    hipEvent_t ev_reset = nullptr;   // recorded once this render's counters are zeroed
     std::atomic<uint32_t> n_chunks{0};  // launches of the current render (0 until all are enqueued)
+    // mrt_progress may run on another host thread: it and every change to the launch bookkeeping
+    // above (h_prog, h_seen, ev, chunk_paths) hold this lock
+    std::mutex prog_mu;
+    // recorded at the end of every mrt_render_device on the caller's stream: workspace changes
+    // (relayout uploads, reallocation) wait for it, so a render still running on another stream
+    // never sees its buffers rewritten or freed
+    hipEvent_t ev_done = nullptr;
+    bool ev_done_pending = false;
     unsigned long long* d_rays = nullptr;
-    int grid = 0;
     uint32_t features = 0, variant = 0;
     uint32_t lds_frames = 0, lds_rays = 0, lds_mesh = 0, lds_save = 0;
-    size_t lds_bytes = 0;
+    PathLaunch pl[2];            // [0] exact contract, [1] tolerance contract (MRT_RF_FAST)
+    int max_grid = 0;
     std::vector<hipEvent_t> ev;  // [2*k]: start/stop of path-kernel launch k of the last render
     uint32_t n_launch = 0;
-    size_t rad_cap = 0, acc_cap = 0, lev_cap = 0, px_cap = 0, pr_cap = 0, sd_cap = 0;
+    size_t rad_cap = 0, acc_cap = 0, lev_cap = 0, px_cap = 0, pr_cap = 0, sd_cap = 0, out_cap = 0;
     uint64_t last_paths = 0;
+    uint32_t last_numerics = 0;
     uint32_t prog_ops = 0;  // linear hit program length (0: generic machine)
-    uint32_t vgprs = 0;
 };
 
 static mrt_status dev_alloc(mrt_scene* s, void** p, size_t bytes) {
@@ -979,24 +635,36 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     s->lds_rays = lin_kernel ? 0 : (uint32_t)gc.max_rays;
     s->lds_mesh = (uint32_t)gc.max_mesh;
     s->lds_save = (lin_kernel && (kVariants[s->variant] & FT_INST)) ? 15u : 0u;
-    s->lds_bytes = (size_t)kWavesPerWG * 64 * 4 * (s->lds_frames * 2 + s->lds_rays * 11 + s->lds_mesh + s->lds_save + kLevK[s->variant] * 4);
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
-    if (s->lds_bytes > (size_t)prop.sharedMemPerBlock) { mrt_scene_free(s); return mrt_internal_fail(MRT_ERR_INVALID, "scene graph too deep for the LDS stacks"); }
     // resident workgroups per CU: one 256-thread group = one wave per SIMD (a 64-thread group =
-    // a quarter of that); VGPRs (512 per SIMD
-    // lane, granule 8) and LDS (160 KiB per CU) bound it.  (The runtime occupancy query
-    // under-counts gfx950 register budgets, so it is computed from the kernel's attributes.)
-    hipFuncAttributes fa{};
-    HIPCHK(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(kernel_for(s->variant))));
-    const int vg = std::max(8, (fa.numRegs + 7) & ~7);
-    int nb = std::min(8, 512 / vg) * (int)(4 / kWavesPerWG);  // waves per SIMD x groups per wave slot
-    if (s->lds_bytes) nb = std::min<int>(nb, (int)((160u * 1024u) / s->lds_bytes));
-    if (nb < 1) nb = 1;
-    s->vgprs = (uint32_t)fa.numRegs;
-    if (const char* e = getenv("MRT_BLOCKS_PER_CU"))  // experiment hook
-        if (*e) nb = std::max(1, atoi(e));
-    s->grid = prop.multiProcessorCount * nb;
+    // a quarter of that); VGPRs (512 per SIMD lane, granule 8) and LDS (160 KiB per CU) bound it.
+    // (The runtime occupancy query under-counts gfx950 register budgets, so it is computed from
+    // the kernel's attributes.)  Per numerics build: their register counts differ.
+    const KernelTable* tabs[2] = {&kernel_table_exact(), &kernel_table_fast()};
+    for (int k = 0; k < 2; k++) {
+        PathLaunch& L = s->pl[k];
+        L.fn = tabs[k]->kernel[s->variant];
+        L.lds_bytes = (size_t)kWavesPerWG * 64 * 4 *
+                      (s->lds_frames * 2 + s->lds_rays * 11 + s->lds_mesh + s->lds_save + tabs[k]->lev_k[s->variant] * 4);
+        if (L.lds_bytes > (size_t)prop.sharedMemPerBlock) {
+            mrt_scene_free(s);
+            return mrt_internal_fail(MRT_ERR_INVALID, "scene graph too deep for the LDS stacks");
+        }
+        hipFuncAttributes fa{};
+        HIPCHK(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(L.fn)));
+        const int vg = std::max(8, (fa.numRegs + 7) & ~7);
+        int nb = std::min(8, 512 / vg) * (int)(4 / kWavesPerWG);  // waves per SIMD x groups per wave slot
+        if (L.lds_bytes) nb = std::min<int>(nb, (int)((160u * 1024u) / L.lds_bytes));
+        if (nb < 1) nb = 1;
+        L.vgprs = (uint32_t)fa.numRegs;
+#ifdef MRT_EXPERIMENTS
+        if (const char* e = getenv("MRT_BLOCKS_PER_CU"))  // experiment hook
+            if (*e) nb = std::max(1, atoi(e));
+#endif
+        L.grid = prop.multiProcessorCount * nb;
+        s->max_grid = std::max(s->max_grid, L.grid);
+    }
     *out = s;
     return MRT_OK;
 }
@@ -1004,13 +672,15 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
 extern "C" void mrt_scene_free(mrt_scene* s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
+    if (s->ev_done_pending) (void)hipEventSynchronize(s->ev_done);
     for (void* p : s->allocs) (void)hipFree(p);
     for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
     if (s->pstream) (void)hipStreamDestroy(s->pstream);
     if (s->h_prog) (void)hipHostFree(s->h_prog);
     if (s->h_one) (void)hipHostFree(s->h_one);
-    if (s->ev_reset) (void)hipEventDestroy(s->ev_reset);
-    for (void* p : {(void*)s->d_counters, (void*)s->d_pixels, (void*)s->d_sdist, (void*)s->d_rad, (void*)s->d_path_rays, (void*)s->d_acc, (void*)s->d_lev})
+    if (s->ev_done) (void)hipEventDestroy(s->ev_done);
+    for (void* p : {(void*)s->d_counters, (void*)s->d_pixels, (void*)s->d_sdist, (void*)s->d_rad, (void*)s->d_path_rays, (void*)s->d_acc,
+                    (void*)s->d_lev, (void*)s->d_out})
         if (p) (void)hipFree(p);
     delete s;
 }
@@ -1024,8 +694,23 @@ static uint32_t auto_chunk(uint32_t npix, uint32_t ns) {
     return (uint32_t)std::min<size_t>(c, ns);
 }
 
-static mrt_status grow(void** p, size_t* cap, size_t bytes) {
+static bool same_layout(const mrt_render_desc& a, const mrt_render_desc& b) {
+    return a.width == b.width && a.height == b.height && a.tile_size == b.tile_size && a.rank == b.rank && a.world == b.world;
+}
+
+// Before the workspace is rewritten or reallocated: wait for the last enqueued render of this
+// context (it may still run on a caller stream that the synchronous uploads do not order against).
+static mrt_status quiesce(mrt_scene* s) {
+    if (s->ev_done_pending) {
+        HIPCHK(hipEventSynchronize(s->ev_done));
+        s->ev_done_pending = false;
+    }
+    return MRT_OK;
+}
+static mrt_status grow(mrt_scene* s, void** p, size_t* cap, size_t bytes) {
     if (*cap >= bytes && *p) return MRT_OK;
+    mrt_status st = quiesce(s);
+    if (st) return st;
     if (*p) (void)hipFree(*p);
     *p = nullptr;
     *cap = 0;
@@ -1033,10 +718,6 @@ static mrt_status grow(void** p, size_t* cap, size_t bytes) {
     if (e != hipSuccess) return mrt_internal_fail(MRT_ERR_OOM, "workspace allocation failed");
     *cap = bytes;
     return MRT_OK;
-}
-
-static bool same_layout(const mrt_render_desc& a, const mrt_render_desc& b) {
-    return a.width == b.width && a.height == b.height && a.tile_size == b.tile_size && a.rank == b.rank && a.world == b.world;
 }
 
 extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
@@ -1048,11 +729,12 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
     uint32_t ns = d->sqrt_samples * d->sqrt_samples;
     if (relayout) {
         std::vector<uint32_t> px = mrt_internal_local_pixels(d);
-        s->npix = (uint32_t)px.size();
         std::vector<uint2> xy(px.size());
         for (size_t i = 0; i < px.size(); i++) xy[i] = make_uint2(px[i] % d->width, px[i] / d->width);
-        if ((st = grow((void**)&s->d_pixels, &s->px_cap, xy.size() * 8))) return st;
+        if ((st = quiesce(s))) return st;
+        if ((st = grow(s, (void**)&s->d_pixels, &s->px_cap, xy.size() * 8))) return st;
         HIPCHK(hipMemcpy(s->d_pixels, xy.data(), xy.size() * 8, hipMemcpyHostToDevice));
+        s->npix = (uint32_t)px.size();
     }
     if (s->sdist_sq != d->sqrt_samples) {  // sample grid of main.cpp:319-332, in float like the reference
         const uint32_t sq = d->sqrt_samples;
@@ -1060,42 +742,50 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
         for (uint32_t i = 0; i < sq; i++)
             for (uint32_t j = 0; j < sq; j++)
                 sd[(size_t)i * sq + j] = make_float2(((float)i + 0.5f) / (float)sq, ((float)j + 0.5f) / (float)sq);
-        if ((st = grow((void**)&s->d_sdist, &s->sd_cap, sd.size() * 8))) return st;
+        if ((st = quiesce(s))) return st;
+        if ((st = grow(s, (void**)&s->d_sdist, &s->sd_cap, sd.size() * 8))) return st;
         HIPCHK(hipMemcpy(s->d_sdist, sd.data(), sd.size() * 8, hipMemcpyHostToDevice));
         s->sdist_sq = sq;
     }
-    s->chunk = d->chunk_samples ? std::min(d->chunk_samples, ns) : auto_chunk(s->npix, ns);
-    s->chunk = (uint32_t)std::min<uint64_t>(s->chunk, 0xFFFFFFFFull / std::max<uint32_t>(s->npix, 1));  // 32-bit path index
-    if (s->chunk == 0) return mrt_internal_fail(MRT_ERR_INVALID, "image too large for one launch");
-    if (d->flags & MRT_RF_PATH_DEBUG) s->chunk = ns;  // debug keeps every path
+    uint32_t chunk = d->chunk_samples ? std::min(d->chunk_samples, ns) : auto_chunk(s->npix, ns);
+    chunk = (uint32_t)std::min<uint64_t>(chunk, 0xFFFFFFFFull / std::max<uint32_t>(s->npix, 1));  // 32-bit path index
+    if (chunk == 0) return mrt_internal_fail(MRT_ERR_INVALID, "image too large for one launch");
+    if (d->flags & MRT_RF_PATH_DEBUG) chunk = ns;  // debug keeps every path
+    if (chunk != s->chunk && (st = quiesce(s))) return st;  // the fold of a running render reads `chunk` rows
+    s->chunk = chunk;
     size_t paths = (size_t)s->npix * s->chunk;
-    if ((st = grow((void**)&s->d_rad, &s->rad_cap, paths * 12))) return st;
-    if ((st = grow((void**)&s->d_acc, &s->acc_cap, (size_t)s->npix * 16))) return st;
+    if ((st = grow(s, (void**)&s->d_rad, &s->rad_cap, paths * 12))) return st;
+    if ((st = grow(s, (void**)&s->d_acc, &s->acc_cap, (size_t)s->npix * 16))) return st;
+    if ((st = grow(s, (void**)&s->d_out, &s->out_cap, (size_t)s->npix * 16 + 16))) return st;
     if (d->flags & MRT_RF_PATH_DEBUG)
-        if ((st = grow((void**)&s->d_path_rays, &s->pr_cap, paths * 4))) return st;
+        if ((st = grow(s, (void**)&s->d_path_rays, &s->pr_cap, paths * 4))) return st;
     s->lev_rows = std::max<uint32_t>(d->max_bounces, 1);
-    if ((st = grow((void**)&s->d_lev, &s->lev_cap, (size_t)s->lev_rows * s->grid * MRT_PATH_WG * 16))) return st;
+    if ((st = grow(s, (void**)&s->d_lev, &s->lev_cap, (size_t)s->lev_rows * s->max_grid * MRT_PATH_WG * 16))) return st;
     uint32_t launches = (ns + s->chunk - 1) / s->chunk;
-    if ((st = grow((void**)&s->d_counters, &s->cnt_cap, (size_t)launches * 8))) return st;
+    if ((st = grow(s, (void**)&s->d_counters, &s->cnt_cap, (size_t)launches * 8))) return st;
     if (!s->pstream) HIPCHK(hipStreamCreateWithFlags(&s->pstream, hipStreamNonBlocking));
-    if (s->h_prog_cap < (size_t)launches) {
-        if (s->h_prog) (void)hipHostFree(s->h_prog);
-        s->h_prog = nullptr;
-        s->h_prog_cap = 0;
-        HIPCHK(hipHostMalloc((void**)&s->h_prog, (size_t)launches * 8, hipHostMallocPortable | hipHostMallocCoherent));
-        s->h_prog_cap = launches;
+    if (!s->ev_done) HIPCHK(hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming));
+    {
+        std::lock_guard<std::mutex> lk(s->prog_mu);
+        if (s->h_prog_cap < (size_t)launches) {
+            if ((st = quiesce(s))) return st;
+            if (s->h_prog) (void)hipHostFree(s->h_prog);
+            s->h_prog = nullptr;
+            s->h_prog_cap = 0;
+            HIPCHK(hipHostMalloc((void**)&s->h_prog, (size_t)launches * 8, hipHostMallocPortable | hipHostMallocCoherent));
+            s->h_prog_cap = launches;
+        }
+        if (s->h_seen.size() < (size_t)launches) s->h_seen.resize(launches, 0);
+        if (s->chunk_paths.size() < launches) s->chunk_paths.resize(launches, 0);
+        while (s->ev.size() < 2 * (size_t)launches) {
+            hipEvent_t e;
+            HIPCHK(hipEventCreate(&e));
+            s->ev.push_back(e);
+        }
     }
-    if (s->h_seen.size() < (size_t)launches) s->h_seen.resize(launches, 0);
     if (!s->h_one) {
         HIPCHK(hipHostMalloc((void**)&s->h_one, sizeof(int), hipHostMallocPortable));
         *s->h_one = 1;
-    }
-    if (!s->ev_reset) HIPCHK(hipEventCreateWithFlags(&s->ev_reset, hipEventDisableTiming));
-    if (s->chunk_paths.size() < launches) s->chunk_paths.resize(launches, 0);
-    while (s->ev.size() < 2 * (size_t)launches) {
-        hipEvent_t e;
-        HIPCHK(hipEventCreate(&e));
-        s->ev.push_back(e);
     }
     s->wdesc = *d;
     s->have_ws = true;
@@ -1103,22 +793,27 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
 }
 
 extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, float* d_local, uint64_t* d_rays, void* stream) {
+    if (!s || !d || !d_local) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_render_device: null");
+    s->n_chunks.store(0, std::memory_order_release);  // progress: a new render, not started
     mrt_status st = mrt_prepare(s, d);
     if (st) return st;
+    const PathLaunch& PL = s->pl[(d->flags & MRT_RF_FAST) ? 1 : 0];
     hipStream_t q = (hipStream_t)stream;
     uint32_t ns = d->sqrt_samples * d->sqrt_samples;
     HIPCHK(hipMemsetAsync(s->d_acc, 0, (size_t)s->npix * 16, q));
     const uint32_t launches = (ns + s->chunk - 1) / s->chunk;
-    s->n_chunks = 0;
     HIPCHK(hipMemsetAsync(s->d_counters, 0, (size_t)launches * 8, q));
     HIPCHK(hipMemsetAsync(s->d_counter + 4, 0, 8, q));  // cancel flag
-    HIPCHK(hipEventRecord(s->ev_reset, q));
-    for (uint32_t k = 0; k < launches; k++) {
-        s->chunk_paths[k] = (uint64_t)s->npix * (std::min(ns, (k + 1) * s->chunk) - k * s->chunk);
-        __atomic_store_n(&s->h_prog[k], (uint64_t)0, __ATOMIC_RELAXED);
-        __atomic_store_n(&s->h_seen[k], (uint64_t)0, __ATOMIC_RELAXED);
+    {
+        std::lock_guard<std::mutex> lk(s->prog_mu);
+        for (uint32_t k = 0; k < launches; k++) {
+            s->chunk_paths[k] = (uint64_t)s->npix * (std::min(ns, (k + 1) * s->chunk) - k * s->chunk);
+            __atomic_store_n(&s->h_prog[k], (uint64_t)0, __ATOMIC_RELAXED);
+            s->h_seen[k] = 0;
+        }
     }
     s->n_launch = 0;
+    s->last_numerics = (d->flags & MRT_RF_FAST) ? 1u : 0u;
     for (uint32_t s0 = 0; s0 < ns; s0 += s->chunk) {
         uint32_t s1 = std::min(ns, s0 + s->chunk);
         PathParams P{};
@@ -1140,8 +835,8 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.ns = ns;
         P.s0 = s0;
         P.n_paths = s->npix * (s1 - s0);
-        P.tail_zone = (uint32_t)std::min<uint64_t>((uint64_t)s->grid * kWavesPerWG * 2 * MRT_BATCH, P.n_paths);  // ~2 big claims per wave
-        P.static_first = (uint64_t)P.n_paths < (uint64_t)s->grid * kWavesPerWG * MRT_BATCH * 64u;
+        P.tail_zone = (uint32_t)std::min<uint64_t>((uint64_t)PL.grid * kWavesPerWG * 2 * MRT_BATCH, P.n_paths);  // ~2 big claims per wave
+        P.static_first = (uint64_t)P.n_paths < (uint64_t)PL.grid * kWavesPerWG * MRT_BATCH * 64u;
         P.seed = d->seed;
         P.max_bounces = d->max_bounces;
         P.rad = s->d_rad;
@@ -1153,7 +848,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.lev = s->d_lev;
         P.lev_rows = s->lev_rows;
         HIPCHK(hipEventRecord(s->ev[2 * s->n_launch], q));
-        hipLaunchKernelGGL(kernel_for(s->variant), dim3(s->grid), dim3(MRT_PATH_WG), s->lds_bytes, q, P);
+        hipLaunchKernelGGL(PL.fn, dim3(PL.grid), dim3(MRT_PATH_WG), PL.lds_bytes, q, P);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(s->ev[2 * s->n_launch + 1], q));
         s->n_launch++;
@@ -1162,52 +857,48 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         HIPCHK(hipGetLastError());
         s->last_paths = P.n_paths;
     }
-    s->n_chunks = launches;  // progress reads start once every launch and its events are enqueued
     uint32_t blocks = (s->npix + 255) / 256;
     hipLaunchKernelGGL(mrt_final_kernel, dim3(blocks), dim3(256), 0, q, s->d_acc, (float4*)d_local, s->npix, ns, d->mode, d->max_luminance);
     HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(s->ev_done, q));
+    s->ev_done_pending = true;
+    s->n_chunks.store(launches, std::memory_order_release);  // progress reads start once every launch and its events are enqueued
     return MRT_OK;
 }
 
 extern "C" mrt_status mrt_render(mrt_scene* s, const mrt_render_desc* d, float* rgb_out, uint64_t* rays_out, const volatile int* cancel) {
     if (!s || !d || !rgb_out) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_render: null");
-    mrt_status st = mrt_prepare(s, d);
-    if (st) return st;
+    s->n_chunks.store(0, std::memory_order_release);
     if (cancel && *cancel) return mrt_internal_fail(MRT_ERR_CANCELLED, "cancelled");
     mrt_render_desc dc = *d;  // a cancellable render runs as >= 16 launches; cancel lands between them
     const uint32_t ns = d->sqrt_samples * d->sqrt_samples;
     if (cancel && dc.chunk_samples == 0 && !(dc.flags & MRT_RF_PATH_DEBUG)) dc.chunk_samples = std::max(1u, ns / 16);
     d = &dc;
-    if ((st = mrt_prepare(s, d))) return st;
-    float* d_out = nullptr;
-    HIPCHK(hipMalloc(&d_out, (size_t)s->npix * 16 + 16));
+    mrt_status st = mrt_prepare(s, d);
+    if (st) return st;
     HIPCHK(hipMemset(s->d_rays, 0, 8));
-    st = mrt_render_device(s, d, d_out, (uint64_t*)s->d_rays, nullptr);
-    if (st) {
-        (void)hipFree(d_out);
-        return st;
-    }
+    if ((st = mrt_render_device(s, d, (float*)s->d_out, (uint64_t*)s->d_rays, nullptr))) return st;
     // wait, forwarding the caller's cancel flag to the device flag the path kernel polls
     bool cancelled = false;
-    for (;;) {
-        const hipError_t q = hipStreamQuery(nullptr);
-        if (q == hipSuccess) break;
-        if (q != hipErrorNotReady) {
-            (void)hipFree(d_out);
-            return mrt_internal_fail(MRT_ERR_HIP, hipGetErrorString(q));
+    if (!cancel) {
+        HIPCHK(hipEventSynchronize(s->ev_done));
+    } else {
+        for (;;) {
+            const hipError_t q = hipEventQuery(s->ev_done);
+            if (q == hipSuccess) break;
+            if (q != hipErrorNotReady) return mrt_internal_fail(MRT_ERR_HIP, hipGetErrorString(q));
+            if (*cancel && !cancelled) {
+                HIPCHK(hipMemcpyAsync(s->d_counter + 4, s->h_one, sizeof(int), hipMemcpyHostToDevice, s->pstream));
+                HIPCHK(hipStreamSynchronize(s->pstream));
+                cancelled = true;
+            }
+            usleep(200);
         }
-        if (cancel && *cancel && !cancelled) {
-            HIPCHK(hipMemcpyAsync(s->d_counter + 4, s->h_one, sizeof(int), hipMemcpyHostToDevice, s->pstream));
-            HIPCHK(hipStreamSynchronize(s->pstream));
-            cancelled = true;
-        }
-        usleep(200);
     }
+    s->ev_done_pending = false;
     std::vector<float> local((size_t)s->npix * 4);
     std::vector<uint32_t> px = mrt_internal_local_pixels(d);
-    hipError_t e = hipMemcpy(local.data(), d_out, local.size() * 4, hipMemcpyDeviceToHost);
-    (void)hipFree(d_out);
-    if (e != hipSuccess) return mrt_internal_fail(MRT_ERR_HIP, hipGetErrorString(e));
+    HIPCHK(hipMemcpy(local.data(), s->d_out, local.size() * 4, hipMemcpyDeviceToHost));
     for (size_t i = 0; i < px.size(); i++) memcpy(rgb_out + (size_t)px[i] * 4, &local[i * 4], 16);
     uint64_t rays = 0;
     HIPCHK(hipMemcpy(&rays, s->d_rays, 8, hipMemcpyDeviceToHost));
@@ -1232,7 +923,8 @@ extern "C" mrt_status mrt_render_debug(mrt_scene* s, float* path_rgb, uint32_t* 
 extern "C" mrt_status mrt_progress(mrt_scene* s, float* pct) {
     if (!s || !pct) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_progress: null");
     *pct = 0.0f;
-    const size_t n = s->n_chunks;
+    std::lock_guard<std::mutex> lk(s->prog_mu);
+    const size_t n = s->n_chunks.load(std::memory_order_acquire);
     if (n == 0 || !s->h_prog || s->h_prog_cap < n || s->ev.size() < 2 * n || s->h_seen.size() < n) return MRT_OK;  // not started
     double done = 0, total = 0;
     for (size_t k = 0; k < n; k++) {
@@ -1242,8 +934,8 @@ extern "C" mrt_status mrt_progress(mrt_scene* s, float* pct) {
         } else if (hipEventQuery(s->ev[2 * k]) == hipSuccess) {
             // snapshots from different waves land out of order: report the largest seen so far
             uint64_t c = __atomic_load_n(&s->h_prog[k], __ATOMIC_RELAXED);
-            c = std::max(c, __atomic_load_n(&s->h_seen[k], __ATOMIC_RELAXED));
-            __atomic_store_n(&s->h_seen[k], c, __ATOMIC_RELAXED);
+            c = std::max(c, s->h_seen[k]);
+            s->h_seen[k] = c;
             done += (double)std::min<uint64_t>(c, s->chunk_paths[k]);
         }
     }
@@ -1255,10 +947,11 @@ extern "C" mrt_status mrt_scene_kernel_info(const mrt_scene* s, mrt_kernel_info*
     if (!s || !out) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_scene_kernel_info: null");
     out->features = s->features;
     out->kernel_features = kVariants[s->variant];
-    out->lds_bytes = (uint32_t)s->lds_bytes;
-    out->grid = (uint32_t)s->grid;
+    const PathLaunch& L = s->pl[s->last_numerics];
+    out->lds_bytes = (uint32_t)L.lds_bytes;
+    out->grid = (uint32_t)L.grid;
     out->prog_ops = s->prog_ops;
-    out->vgprs = s->vgprs;
+    out->vgprs = L.vgprs;
     return MRT_OK;
 }
 

@@ -49,6 +49,19 @@ def test_parse_argv_matches_reference_defaults_and_ranges(mrt):
     # out-of-range values are ignored with a warning (ReadParameter, cmdline_parser.cpp:51-54)
     p = mrt.ParseArgv(["mrt", "-scene", "12", "-mode", "2", "-width", "0", "-depth"])
     assert (p.scene_select, p.threading_mode, p.buffer_width, p.max_bounces) == (8, 1, 500, 32)
+    # -threads keeps the reference's meaning (CPU worker threads); GPUs and numerics have their own flags
+    p = mrt.ParseArgv(["mrt", "-threads", "3", "-gpus", "2", "-numerics", "exact"])
+    assert (p.num_threads, p.gpus, p.numerics) == (3, 2, 0)
+    p = mrt.ParseArgv(["mrt", "-numerics", "bogus"])
+    assert (p.num_threads, p.gpus, p.numerics) == (0, 0, 1)
+
+
+def test_default_render_desc_carries_numerics(mrt):
+    for num, flag in ((0, 0), (1, mrt._lib.RF_FAST)):
+        p = mrt.ParseArgv(["mrt", "-scene", "5", "-samples", "17", "-numerics", str(num)])
+        d = mrt._lib.MrtRenderDesc()
+        mrt.lib().mrt_default_render_desc(ctypes.byref(p), ctypes.byref(d))
+        assert (d.sqrt_samples, d.flags & mrt._lib.RF_FAST) == (4, flag)
 
 
 def reference_tiles(W, H, ts):

@@ -3,7 +3,7 @@
 # -> /tmp/isa_<tag>.s ; prints per path-kernel variant: VGPRs, scratch bytes, instructions.
 tag=$1; shift
 d=$(mktemp -d)
-( cd $d && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -Wno-unused-function \
+( cd $d && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-fast-math -ffp-contract=off -fno-slp-vectorize -Wno-unused-function \
     -mllvm -disable-promote-alloca-to-vector -mllvm -structurizecfg-skip-uniform-regions "$@" --save-temps -c /root/repo/miniraytracer_amd/csrc/mrt_render.hip -o r.o 2>/dev/null \
   && cp mrt_render-hip-amdgcn-amd-amdhsa-gfx950.s /tmp/isa_$tag.s )
 rm -rf $d

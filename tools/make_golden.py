@@ -13,7 +13,7 @@ Fixtures (all small; data only -- inputs and expected outputs):
   tonemap_<id>.npz        the reference display loop's input (linear buffer) and Drago/ARGB32 output
   shipped_stream_5*.npz   stream-matched render by the reference AS SHIPPED (FMA contraction, glibc
                           libm): the tolerance fixture of the per-pixel RMSE < 1e-3 criterion
-                          (SURVEY 8(d) parity 2).  Full C2 (500x500, 1024 spp): rows 200-299, 25x25
+                          (SURVEY 8(d) parity 2).  Full C2 (500x500, 1024 spp): the whole image, rows 200-299, 25x25
                           block means, channel means, ray count; and whole small images of scenes 5, 8, 9, 7
                           (SHIPPED_SMALL).
                           `--only-shipped-stream` regenerates just these two.
@@ -79,7 +79,7 @@ def shipped_stream(tmp):
     meta = json.loads(run(SHIPPED, ["--h-mode", "stream", "-width", 500, "-height", 500, "-samples", 1024, "-depth", 32,
                                     "--h-threads", 8, "--h-out", img, "-scene", 5]))
     im = read_pfm(img, 500, 500)
-    np.savez_compressed(os.path.join(OUT, "shipped_stream_5.npz"), band=im[200:300].copy(), band_rows=np.array([200, 300]),
+    np.savez_compressed(os.path.join(OUT, "shipped_stream_5.npz"), image=im, band=im[200:300].copy(), band_rows=np.array([200, 300]),
                         block_mean=im.reshape(20, 25, 20, 25, 3).mean(axis=(1, 3), dtype=np.float64),
                         mean=im.reshape(-1, 3).mean(axis=0, dtype=np.float64), rays=np.array([meta["rays"]], dtype=np.int64),
                         meta=np.array([5, 500, 500, 1024, 32], dtype=np.int64))

@@ -2,64 +2,117 @@
 """Summarise a tools/profile.sh run (gpurun_out/prof) into profiles/:
 
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
-  profiles/<tag>_pmc.json           per-launch counters of mrt_path_kernel + derived metrics
-  profiles/pmc_cornell_c2.json      HBM bytes per launch read by bench.py (roofline.traffic)
+  profiles/<tag>_pmc.json           per-launch counters of every mrt_path_kernel build (exact /
+                                    fast) + derived metrics, per-dispatch wave check
+  profiles/pmc_<name>.json          (--bench-file) what bench.py reads for roofline.traffic /
+                                    hbm_frac / valu_busy / valu_lane_util, keyed by workload config
 
 HBM bytes follow MI355X_MICROARCH.md "HBM": FETCH_SIZE / WRITE_SIZE are in KiB and come from
 separate passes; on gfx950 FETCH_SIZE reports half the bytes of wide coalesced reads, so it is
-doubled before adding WRITE_SIZE.
+doubled before adding WRITE_SIZE.  VALU busy = 2 cycles per wave64 VALU instruction (SIMD-32) over
+the SIMD cycles of the dispatch, the clock taken from GRBM_GUI_ACTIVE (summed over the 8 XCDs,
+MI355X_MICROARCH.md "DVFS give-back"): an issue-slot estimate (transcendental / f64 instructions
+occupy more than 2 cycles, so it is a lower bound).  Lane utilisation = SQ_THREAD_CYCLES_VALU /
+(64 SQ_ACTIVE_INST_VALU).
+
+Usage: pmc_summary.py <tag> [--prof DIR] [--bench-file NAME --config "S W H SPP DEPTH"]
 """
-import csv
+import argparse
 import collections
+import csv
 import json
 import os
 import shutil
-import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+N_SIMD = 1024  # 256 CUs x 4 SIMDs
 
 
-def per_launch(path, kernel="mrt_path_kernel"):
-    rows = list(csv.DictReader(open(path)))
-    agg, ids, meta = collections.defaultdict(float), set(), {}
-    for r in rows:
-        if kernel in r["Kernel_Name"]:
-            agg[r["Counter_Name"]] += float(r["Counter_Value"])
-            ids.add(r["Dispatch_Id"])
-            meta = {k: r[k] for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size", "VGPR_Count", "SGPR_Count")}
-    n = max(len(ids), 1)
-    return {k: v / n for k, v in agg.items()}, n, meta
+def kernel_key(name):
+    base = name.split("(")[0]
+    return "mrt_path_kernel_fast" if "mrt_path_kernel_fast" in base else ("mrt_path_kernel" if "mrt_path_kernel" in base else base)
+
+
+def per_dispatch(path):
+    """{dispatch id: (kernel key, {counter: value}, meta)} of one counter-collection CSV."""
+    out = {}
+    for r in csv.DictReader(open(path)):
+        d = out.setdefault(r["Dispatch_Id"], [kernel_key(r["Kernel_Name"]), collections.defaultdict(float), {}])
+        d[1][r["Counter_Name"]] += float(r["Counter_Value"])
+        d[2] = {k: r.get(k) for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size", "VGPR_Count",
+                                      "SGPR_Count", "Accum_VGPR_Count")}
+    return out
+
+
+def mean_by_kernel(disp):
+    agg, n, meta = collections.defaultdict(lambda: collections.defaultdict(float)), collections.Counter(), {}
+    for k, c, m in disp.values():
+        n[k] += 1
+        meta[k] = m
+        for name, v in c.items():
+            agg[k][name] += v
+    return {k: {name: v / n[k] for name, v in agg[k].items()} for k in agg}, n, meta
 
 
 def main():
-    tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
-    prof = os.path.join(ROOT, "gpurun_out", "prof")
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("--prof", default=os.path.join(ROOT, "gpurun_out", "prof"))
+    ap.add_argument("--bench-file", default=None)
+    ap.add_argument("--config", default="5 500 500 1024 32")
+    a = ap.parse_args()
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
-    shutil.copy(os.path.join(prof, "trace", "run_kernel_stats.csv"), os.path.join(out, f"{tag}_kernel_stats.csv"))
-    fetch, n, meta = per_launch(os.path.join(prof, "fetch", "run_counter_collection.csv"))
-    write, _, _ = per_launch(os.path.join(prof, "write", "run_counter_collection.csv"))
-    res = {"kernel": "mrt_path_kernel", "launches": n, "dispatch": meta,
-           "FETCH_SIZE_KiB": fetch.get("FETCH_SIZE"), "WRITE_SIZE_KiB": write.get("WRITE_SIZE")}
-    hbm = 2 * fetch["FETCH_SIZE"] * 1024 + write["WRITE_SIZE"] * 1024
-    res["hbm_bytes_per_launch"] = hbm
-    sqp = os.path.join(prof, "sq", "run_counter_collection.csv")
-    if os.path.exists(sqp):
-        sq, _, _ = per_launch(sqp)
-        res["sq"] = sq
-        if sq.get("SQ_ACTIVE_INST_VALU"):
-            res["valu_lane_utilization"] = sq["SQ_THREAD_CYCLES_VALU"] / (64.0 * sq["SQ_ACTIVE_INST_VALU"])
-        if sq.get("SQ_WAVE_CYCLES"):
-            res["wait_any_fraction"] = sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"]
-    for r in csv.DictReader(open(os.path.join(prof, "trace", "run_kernel_stats.csv"))):
-        if "mrt_path_kernel" in r["Name"]:
-            res["avg_kernel_ns"] = float(r["AverageNs"])
-            res["hbm_GBps"] = hbm / float(r["AverageNs"])
-    json.dump(res, open(os.path.join(out, f"{tag}_pmc.json"), "w"), indent=1)
-    cfg = [int(x) for x in os.environ.get("PMC_CONFIG", "5 500 500 1024 32").split()]
-    json.dump({"config": cfg, "hbm_bytes_per_launch": hbm, "source": f"profiles/{tag}_pmc.json"},
-              open(os.path.join(out, "pmc_cornell_c2.json"), "w"))
-    print(json.dumps(res, indent=1))
+    stats = os.path.join(a.prof, "trace", "run_kernel_stats.csv")
+    shutil.copy(stats, os.path.join(out, f"{a.tag}_kernel_stats.csv"))
+    avg_ns = {}
+    for r in csv.DictReader(open(stats)):
+        avg_ns.setdefault(kernel_key(r["Name"]), float(r["AverageNs"]))
+    fetch, n_f, meta = mean_by_kernel(per_dispatch(os.path.join(a.prof, "fetch", "run_counter_collection.csv")))
+    write, _, _ = mean_by_kernel(per_dispatch(os.path.join(a.prof, "write", "run_counter_collection.csv")))
+    sqp = os.path.join(a.prof, "sq", "run_counter_collection.csv")
+    sqd = per_dispatch(sqp) if os.path.exists(sqp) else {}
+    sq, _, _ = mean_by_kernel(sqd)
+    res = {"workload_config": [int(x) for x in a.config.split()], "kernels": {}, "sq_wave_check": []}
+    for did, (k, c, m) in sorted(sqd.items(), key=lambda t: int(t[0])):
+        try:
+            grid_waves = int(m["Grid_Size"]) // 64
+        except (TypeError, ValueError):
+            grid_waves = None
+        res["sq_wave_check"].append({"dispatch": int(did), "kernel": k, "SQ_WAVES": c.get("SQ_WAVES"), "grid_waves": grid_waves})
+    for k in fetch:
+        if not k.startswith("mrt_path_kernel"):
+            continue
+        e = {"launches": n_f[k], "dispatch": meta[k], "FETCH_SIZE_KiB": fetch[k].get("FETCH_SIZE"),
+             "WRITE_SIZE_KiB": write.get(k, {}).get("WRITE_SIZE")}
+        e["hbm_bytes_per_launch"] = 2 * e["FETCH_SIZE_KiB"] * 1024 + (e["WRITE_SIZE_KiB"] or 0) * 1024
+        if k in avg_ns:
+            e["avg_kernel_ns"] = avg_ns[k]
+            e["hbm_GBps"] = e["hbm_bytes_per_launch"] / avg_ns[k]
+            e["hbm_frac"] = e["hbm_GBps"] / 8000.0
+        s = sq.get(k)
+        if s:
+            e["sq"] = s
+            if s.get("SQ_ACTIVE_INST_VALU"):
+                e["valu_lane_util"] = s["SQ_THREAD_CYCLES_VALU"] / (64.0 * s["SQ_ACTIVE_INST_VALU"])
+            if s.get("SQ_WAVE_CYCLES"):
+                e["wait_any_fraction"] = s["SQ_WAIT_ANY"] / s["SQ_WAVE_CYCLES"]
+            if s.get("GRBM_GUI_ACTIVE"):
+                cycles = s["GRBM_GUI_ACTIVE"] / 8.0
+                e["gpu_cycles"] = cycles
+                e["valu_busy"] = 2.0 * s["SQ_INSTS_VALU"] / (N_SIMD * cycles)
+                if k in avg_ns:
+                    e["effective_clock_GHz"] = cycles / avg_ns[k]
+        res["kernels"][k] = e
+    json.dump(res, open(os.path.join(out, f"{a.tag}_pmc.json"), "w"), indent=1)
+    if a.bench_file:
+        by = {}
+        for k, e in res["kernels"].items():
+            num = "fast" if k.endswith("_fast") else "exact"
+            by[num] = {x: e.get(x) for x in ("hbm_bytes_per_launch", "valu_busy", "valu_lane_util", "avg_kernel_ns")}
+        json.dump({"config": res["workload_config"], "by_numerics": by, "source": f"profiles/{a.tag}_pmc.json"},
+                  open(os.path.join(out, a.bench_file), "w"), indent=1)
+    print(json.dumps(res, indent=1)[:6000])
 
 
 if __name__ == "__main__":
