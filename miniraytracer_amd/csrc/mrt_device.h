@@ -29,6 +29,31 @@
 #ifndef MRT_FAST
 #define MRT_FAST 0
 #endif
+// parts of the tolerance contract (all on with MRT_FAST; separable for experiments)
+#ifndef MRT_FAST_DIV
+#define MRT_FAST_DIV MRT_FAST    // reciprocal-based division
+#endif
+#ifndef MRT_FAST_SQRT
+#define MRT_FAST_SQRT MRT_FAST   // v_sqrt_f32
+#endif
+#ifndef MRT_FAST_NORM
+#define MRT_FAST_NORM MRT_FAST   // normalize by v_rsq_f32
+#endif
+#ifndef MRT_FAST_TRANS
+#define MRT_FAST_TRANS MRT_FAST  // f32 / hardware transcendentals
+#endif
+#ifndef MRT_FAST_GUARDS
+#define MRT_FAST_GUARDS MRT_FAST // no exactness range guards
+#endif
+// A rect hit's point is put ON the rect's plane (p[axis] = k).  Under the exact contract
+// o + RN(t*d) with t = RN((k - o)/d) lands on the plane almost always; with FMA contraction or a
+// reciprocal-based t it lands ~1e-5 off either side, and a grazing scattered ray from a point just
+// outside a face of an instanced box then re-hits that face at t > tmin (0.001): +0.1-0.2% rays on
+// the Cornell box (measured; DESIGN.md "Numerics contracts").  Snapping restores the exact
+// contract's geometry.
+#ifndef MRT_FAST_SNAP
+#define MRT_FAST_SNAP MRT_FAST
+#endif
 
 namespace mrtd {
 
@@ -41,7 +66,7 @@ __device__ __forceinline__ f3 sub(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, 
 __device__ __forceinline__ f3 mul(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
 __device__ __forceinline__ f3 mulf(f3 a, float f) { return f3{a.x * f, a.y * f, a.z * f}; }
 __device__ __forceinline__ f3 fmul(float f, f3 a) { return f3{f * a.x, f * a.y, f * a.z}; }
-#if MRT_FAST && defined(__HIP_DEVICE_COMPILE__)
+#if MRT_FAST_DIV && defined(__HIP_DEVICE_COMPILE__)
 __device__ __forceinline__ f3 divf(f3 a, float f) {
     const float y = __builtin_amdgcn_rcpf(f);
     return f3{a.x * y, a.y * y, a.z * y};
@@ -51,6 +76,16 @@ __device__ __forceinline__ f3 divf(f3 a, float f) { return f3{a.x / f, a.y / f, 
 #endif
 __device__ __forceinline__ float dot(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 __device__ __forceinline__ float sdot(f3 a) { return (a.x * a.x + a.y * a.y) + a.z * a.z; }
+// sphere::hit's quadratic (sphere.cpp:20-26): b = dot(oc, d), c = |oc|^2 - r^2, disc = b*b - c.
+// Never FMA-contracted, also in the tolerance-contract build (the CPU restatement built with
+// contraction loses 0.08% of book2's rays through this quadratic; DESIGN.md "Numerics contracts").
+__device__ __forceinline__ float sphere_disc(f3 oc, f3 d, float radius, float* bout) {
+#pragma clang fp contract(off)
+    const float b = (oc.x * d.x + oc.y * d.y) + oc.z * d.z;
+    const float c = ((oc.x * oc.x + oc.y * oc.y) + oc.z * oc.z) - radius * radius;
+    *bout = b;
+    return b * b - c;
+}
 // ---- exact f32 division on a short path (tools/numcheck/markstein_check.hip) ----------------------
 // IEEE a/b compiles to 11 VALU (div_scale x2, rcp, 6 fma, div_fmas, div_fixup).  With y = RN(1/b)
 // known, Markstein's correction q' = q + (a - b*q)*y (q = RN(a*y), residual exact by fma) IS the
@@ -62,7 +97,7 @@ __device__ __forceinline__ float sdot(f3 a) { return (a.x * a.x + a.y * a.y) + a
 // tests on their operands (a ray's `nice` flag, normalize's own test) and take the IEEE division in
 // a wave-uniform branch otherwise (never taken on real scenes).
 __device__ __forceinline__ float recip_nr(float b) {
-#if MRT_FAST && defined(__HIP_DEVICE_COMPILE__)
+#if MRT_FAST_DIV && defined(__HIP_DEVICE_COMPILE__)
     return __builtin_amdgcn_rcpf(b);
 #elif defined(__HIP_DEVICE_COMPILE__)
     const float y0 = __builtin_amdgcn_rcpf(b);
@@ -72,7 +107,7 @@ __device__ __forceinline__ float recip_nr(float b) {
 #endif
 }
 __device__ __forceinline__ float div_core(float a, float b, float y) {
-#if MRT_FAST
+#if MRT_FAST_DIV
     return a * y;
 #endif
     const float q = a * y;
@@ -97,7 +132,7 @@ __device__ __forceinline__ uint32_t mag2(float x) { return __float_as_uint(x) <<
 // tools/numcheck/sqrt_check.hip).  (RN32(v_sqrt_f64(x)) is NOT exact: v_sqrt_f64 misrounds 3.9% of
 // f32 inputs, tools/numcheck/divsqrt_check.hip.)
 __device__ __forceinline__ float sqrt_core(float x) {
-#if MRT_FAST && defined(__HIP_DEVICE_COMPILE__)
+#if MRT_FAST_SQRT && defined(__HIP_DEVICE_COMPILE__)
     return __builtin_amdgcn_sqrtf(x);
 #elif defined(__HIP_DEVICE_COMPILE__)
     const float s = __builtin_amdgcn_sqrtf(x);
@@ -110,7 +145,7 @@ __device__ __forceinline__ float sqrt_core(float x) {
 }
 __device__ __forceinline__ float sqrt_(float x) {
     float r = sqrt_core(x);
-    if (MRT_FAST) return r;
+    if (MRT_FAST_SQRT) return r;
     const bool ok = mag2(x) - 1u >= MRT_MAG2(-96) - 1u;  // |x| >= 2^-96 or x == +-0
     if (__builtin_expect(any_lane(!ok), 0)) r = ok ? r : __builtin_sqrtf(x);
     return r;
@@ -120,7 +155,7 @@ __device__ __forceinline__ float sqrt_(float x) {
 // or normal, and y is normal).
 __device__ __forceinline__ f3 normalize(f3 a) {
     const float dd = sdot(a);
-#if MRT_FAST && defined(__HIP_DEVICE_COMPILE__)
+#if MRT_FAST_NORM && defined(__HIP_DEVICE_COMPILE__)
     const float ry = __builtin_amdgcn_rsqf(dd);
     return f3{a.x * ry, a.y * ry, a.z * ry};
 #endif
@@ -142,7 +177,7 @@ __device__ __forceinline__ bool finite3(f3 a) { return isfinite(a.x) && isfinite
 static constexpr float PI_F = 3.14159265358979323846f;
 static constexpr float FLT_MAX_ = 3.402823466e+38f;
 
-#if MRT_FAST && defined(__HIP_DEVICE_COMPILE__)
+#if MRT_FAST_TRANS && defined(__HIP_DEVICE_COMPILE__)
 // tolerance contract: f32 library functions; sincos of a path angle in [0, 2 pi) by the hardware
 // v_sin/v_cos (argument in revolutions), log by v_log (log2)
 __device__ __forceinline__ float sin_(float x) { return sinf(x); }
@@ -253,7 +288,7 @@ struct Ray {
 // (k - o_a) / d_a may use div_core with inv (the difference of two such coordinates -- rect planes are
 // checked on upload, MRT_F_SLOWDIV -- is 0 or >= 2^-100, and the quotient stays normal).
 __device__ __forceinline__ bool ray_nice(f3 o, f3 d) {
-    if (MRT_FAST) return true;  // no exactness guards: every ray takes the hardware reciprocal
+    if (MRT_FAST_GUARDS) return true;  // no exactness guards: every ray takes the hardware reciprocal
     const bool dn = MRT_MAG_IN(d.x, -26, 1) & MRT_MAG_IN(d.y, -26, 1) & MRT_MAG_IN(d.z, -26, 1);
     const uint32_t mn = min(min(mag2(o.x) - 1u, mag2(o.y) - 1u), mag2(o.z) - 1u);  // 0 -> UINT_MAX
     const float mx = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));

@@ -17,7 +17,11 @@
 
 using namespace mrtd;
 
-#if MRT_FAST
+// which table this build provides (experiments may build the "fast" slot with other switches)
+#ifndef MRT_TABLE_FAST
+#define MRT_TABLE_FAST MRT_FAST
+#endif
+#if MRT_TABLE_FAST
 #define MRT_PATH_KERNEL mrt_path_kernel_fast
 #else
 #define MRT_PATH_KERNEL mrt_path_kernel
@@ -320,7 +324,7 @@ static constexpr path_kernel_t kfn() {
     return MRT_PATH_KERNEL<F>;
 }
 
-#if MRT_FAST
+#if MRT_TABLE_FAST
 const KernelTable& mrtd::kernel_table_fast() {
     static const KernelTable t = {
         "fast",

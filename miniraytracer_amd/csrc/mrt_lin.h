@@ -54,9 +54,8 @@ __device__ __forceinline__ bool lin_prim_t(const OP& o, const Ray& r, float tmin
             cen = add(cen, fmul((r.time - o.f[6]) / (o.f[7] - o.f[6]), sub(f3{o.f[3], o.f[4], o.f[5]}, cen)));
         const float radius = o.f[8];
         const f3 oc = sub(r.o, cen);
-        const float b = dot(oc, r.d);
-        const float c = sdot(oc) - radius * radius;
-        const float disc = b * b - c;
+        float b;
+        const float disc = sphere_disc(oc, r.d, radius, &b);
         const float sq = sqrt_(disc);
         const float t1 = (-b - sq), t2 = (-b + sq);
         const bool ok1 = (t1 < tmax) & (t1 > tmin);
@@ -75,7 +74,7 @@ __device__ __forceinline__ bool lin_prim_t(const OP& o, const Ray& r, float tmin
         // dot(dir, n) > 0 reduces to d_a * ns > 0 (the other products are zeros of finite values)
         float t = div_core(num, da, ia);
         bool back = da * ns > 0.0f;
-        const bool slow = !MRT_FAST && (op_flags(o) & MRT_F_SLOWDIV) != 0;  // uniform
+        const bool slow = !MRT_FAST_GUARDS && (op_flags(o) & MRT_F_SLOWDIV) != 0;  // uniform
         if (__builtin_expect(slow || any_lane(!r.nice), 0)) {  // the reference's forms
             const float dn = AX == 2 ? (r.d.x * 0.0f + r.d.y * 0.0f) + r.d.z * ns
                            : AX == 1 ? (r.d.x * 0.0f + r.d.y * ns) + r.d.z * 0.0f
@@ -113,12 +112,15 @@ __device__ __forceinline__ void lin_prim_rec_op(const MRT_CONST_AS LinOp& o, con
         float pb = 0, pc = 0;
         if constexpr (KIND == MRT_K_XY) {
             rec.n = f3{0, 0, ns};
+            if (MRT_FAST_SNAP) rec.p.z = o.f[4];
             if (needuv) { pb = r.o.x + t * r.d.x; pc = r.o.y + t * r.d.y; }
         } else if constexpr (KIND == MRT_K_XZ) {
             rec.n = f3{0, ns, 0};
+            if (MRT_FAST_SNAP) rec.p.y = o.f[4];
             if (needuv) { pb = r.o.x + t * r.d.x; pc = r.o.z + t * r.d.z; }
         } else {
             rec.n = f3{ns, 0, 0};
+            if (MRT_FAST_SNAP) rec.p.x = o.f[4];
             if (needuv) { pb = r.o.y + t * r.d.y; pc = r.o.z + t * r.d.z; }
         }
         if (needuv) {
@@ -160,12 +162,15 @@ __device__ __forceinline__ void lin_prim_rec(const DScene& S, uint32_t node, con
     float pb, pc;
     if (kind == MRT_K_XY) {
         rec.n = f3{0, 0, ns};
+        if (MRT_FAST_SNAP) rec.p.z = nf[4];
         if (needuv) { pb = r.o.x + t * r.d.x; pc = r.o.y + t * r.d.y; }
     } else if (kind == MRT_K_XZ) {
         rec.n = f3{0, ns, 0};
+        if (MRT_FAST_SNAP) rec.p.y = nf[4];
         if (needuv) { pb = r.o.x + t * r.d.x; pc = r.o.z + t * r.d.z; }
     } else {
         rec.n = f3{ns, 0, 0};
+        if (MRT_FAST_SNAP) rec.p.x = nf[4];
         if (needuv) { pb = r.o.y + t * r.d.y; pc = r.o.z + t * r.d.z; }
     }
     if (needuv) {

@@ -373,7 +373,7 @@ __device__ __forceinline__ bool trace_segment(const DScene& S, PathState& ps, ui
         // cosine / PI_F through div_core: PI_F and RN(1/PI_F) are normal, cosine <= 1
         constexpr float INV_PI = 1.0f / PI_F;
         float sv = div_core(cosine, PI_F, INV_PI);
-        if (!MRT_FAST && __builtin_expect(any_lane((cosine > 0) & (cosine < 0x1p-100f)), 0)) sv = cosine < 0x1p-100f ? cosine / PI_F : sv;
+        if (!MRT_FAST_GUARDS && __builtin_expect(any_lane((cosine > 0) & (cosine < 0x1p-100f)), 0)) sv = cosine < 0x1p-100f ? cosine / PI_F : sv;
         sval = cosine > 0 ? sv : 0;
         spdf = cosine < 0 ? 0 : cosine * (1.0f / PI_F);  // dot(rec.n, dir) == dot(dir, rec.n)
     } else {
@@ -508,7 +508,7 @@ __device__ __forceinline__ void finish_scatter(const DScene& S, PathState& ps, c
         const float cosine = dot(sc.d, pr.n);
         constexpr float INV_PI = 1.0f / PI_F;
         float sv = div_core(cosine, PI_F, INV_PI);
-        if (!MRT_FAST && __builtin_expect(any_lane((cosine > 0) & (cosine < 0x1p-100f)), 0)) sv = cosine < 0x1p-100f ? cosine / PI_F : sv;
+        if (!MRT_FAST_GUARDS && __builtin_expect(any_lane((cosine > 0) & (cosine < 0x1p-100f)), 0)) sv = cosine < 0x1p-100f ? cosine / PI_F : sv;
         sval = cosine > 0 ? sv : 0;
         spdf = cosine < 0 ? 0 : cosine * (1.0f / PI_F);
     } else {

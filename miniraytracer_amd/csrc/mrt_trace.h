@@ -184,9 +184,8 @@ __device__ __forceinline__ bool sphere_hit(const mrt_node& n, const Ray& r, floa
     f3 cen = sphere_center<F>(n, r.time);
     float radius = n.f[8];
     f3 oc = sub(r.o, cen);
-    float b = dot(oc, r.d);
-    float c = sdot(oc) - radius * radius;
-    float disc = b * b - c;
+    float b;
+    float disc = sphere_disc(oc, r.d, radius, &b);
     if (disc > 0) {
         float sq = sqrt_(disc);
         float t = (-b - sq);
@@ -235,6 +234,11 @@ __device__ __forceinline__ bool rect_hit(const mrt_node& n, const Ray& r, float 
         }
         rec.mat = n.mat;
         rec.p = eval(r, t);
+        if (MRT_FAST_SNAP) {  // tolerance contract: the hit point on the rect's plane (see mrt_device.h)
+            if (AX == 2) rec.p.z = n.f[4];
+            else if (AX == 1) rec.p.y = n.f[4];
+            else rec.p.x = n.f[4];
+        }
         rec.n = AX == 2 ? f3{0, 0, ns} : AX == 1 ? f3{0, ns, 0} : f3{ns, 0, 0};
     }
     return true;

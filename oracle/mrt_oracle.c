@@ -618,6 +618,20 @@ static ray get_ray(ctx* C, float s, float t) {
     return mkray(vadd(ld(c->origin), offset), dir, time, 0);
 }
 
+/* one path whose draws come from C->rng as it stands (the caller seeds it) */
+static V path_with(ctx* C, const oracle_desc* d, uint32_t x, uint32_t y, uint32_t s, uint32_t* rays) {
+    uint32_t sq = d->sqrt_samples;
+    uint32_t i = s / sq, j = s % sq;
+    float dx = (i + 0.5f) / (float)sq, dy = (j + 0.5f) / (float)sq; /* main.cpp:324-331 */
+    float u = (x + dx) / (float)d->width;
+    float vv = (y + dy) / (float)d->height;
+    ray r = get_ray(C, u, vv);
+    tstate T = {d->max_bounces, 0};
+    V c = trace(C, &T, &r, 0);
+    *rays = (uint32_t)T.rays;
+    return c;
+}
+
 static V one_path(const mrt_scene_view* v, const oracle_desc* d, uint32_t x, uint32_t y, uint32_t s, uint32_t* rays) {
     uint32_t sq = d->sqrt_samples, ns = sq * sq;
     uint32_t i = s / sq, j = s % sq;
@@ -719,6 +733,112 @@ uint64_t oracle_render(const mrt_scene_view* v, const oracle_desc* d, float* rgb
         if (nt > 1) pthread_join(th[i], NULL);
         rays += jobs[i].rays;
     }
+    return rays;
+}
+
+/* ---- the reference's own RNG order (-threads 1): one worker, one PCG stream ------------------
+ * work_queue tiles (work_queue.cpp:64-128): row-major tiles re-ordered along the inverted Hilbert
+ * curve over the next power of two, tiles outside the image skipped. */
+static void hil_d2xy(uint32_t n, uint32_t d, uint32_t* x, uint32_t* y) { /* work_queue.cpp:6-30 */
+    uint32_t rx, ry, s, t = d;
+    *x = *y = 0;
+    for (s = 1; s < n; s *= 2) {
+        rx = 1 & (t / 2);
+        ry = 1 & (t ^ rx);
+        if (ry == 0) {
+            if (rx == 1) {
+                *x = s - 1 - *x;
+                *y = s - 1 - *y;
+            }
+            uint32_t tmp = *x;
+            *x = *y;
+            *y = tmp;
+        }
+        *x += s * rx;
+        *y += s * ry;
+        t /= 4;
+    }
+}
+static uint32_t rev32(uint32_t v) { /* work_queue.cpp:33-45 */
+    v = ((v >> 1) & 0x55555555u) | ((v & 0x55555555u) << 1);
+    v = ((v >> 2) & 0x33333333u) | ((v & 0x33333333u) << 2);
+    v = ((v >> 4) & 0x0F0F0F0Fu) | ((v & 0x0F0F0F0Fu) << 4);
+    v = ((v >> 8) & 0x00FF00FFu) | ((v & 0x00FF00FFu) << 8);
+    return (v >> 16) | (v << 16);
+}
+typedef struct { uint32_t x0, x1, y0, y1; } otile;
+static uint32_t work_tiles(uint32_t W, uint32_t H, uint32_t ts, otile** out) {
+    uint32_t xc = (W + ts - 1) / ts, yc = (H + ts - 1) / ts, n = xc * yc, po2 = 1, lg = 0;
+    otile* rm = (otile*)malloc(sizeof(otile) * n);
+    otile* fin = (otile*)malloc(sizeof(otile) * n);
+    for (uint32_t y = 0; y < yc; y++)
+        for (uint32_t x = 0; x < xc; x++) {
+            otile t = {x * ts, x * ts + ts < W ? x * ts + ts : W, y * ts, y * ts + ts < H ? y * ts + ts : H};
+            rm[x + y * xc] = t;
+        }
+    uint32_t m = xc > yc ? xc : yc;
+    while (po2 < m) po2 *= 2; /* MRT::nextPo2 */
+    while ((1u << lg) < po2) lg++;
+    uint32_t idx = 0;
+    for (uint32_t d = 0; d < po2 * po2 && idx < n; d++) {
+        uint32_t x, y;
+        hil_d2xy(po2, d, &x, &y);
+        x = lg ? rev32(x) >> (32u - lg) : 0; /* INVERT (work_queue.cpp:104-108) */
+        y = lg ? rev32(y) >> (32u - lg) : 0;
+        if (x < xc && y < yc) fin[idx++] = rm[x + y * xc];
+    }
+    free(rm);
+    *out = fin;
+    return n;
+}
+
+uint64_t oracle_render_ref_order(const mrt_scene_view* v, const oracle_desc* d, uint32_t tile_size, uint64_t initstate, uint64_t initseq,
+                                 float* rgb) {
+    ctx C;
+    C.v = v;
+    pcg_srandom(&C.rng, initstate, initseq); /* Init_Thread_RNG(args.initstate, args.initseq), main.cpp:143/198 */
+    otile* tiles;
+    uint32_t nt = work_tiles(d->width, d->height, tile_size, &tiles);
+    uint32_t ns = d->sqrt_samples * d->sqrt_samples;
+    uint64_t rays = 0;
+    if (d->mode == 0) { /* draw() over work_queue_seq (main.cpp:138-188, work_queue.cpp:133-140) */
+        for (uint32_t k = 0; k < nt; k++)
+            for (uint32_t y = tiles[k].y0; y < tiles[k].y1; y++)
+                for (uint32_t x = tiles[k].x0; x < tiles[k].x1; x++) {
+                    V color = v3(0, 0, 0);
+                    for (uint32_t s = 0; s < ns; s++) {
+                        uint32_t rr;
+                        V smp = path_with(&C, d, x, y, s, &rr);
+                        rays += rr;
+                        if (!isfinite(smp.x) || !isfinite(smp.y) || !isfinite(smp.z)) smp = color;
+                        color = vadd(color, smp);
+                    }
+                    color = vdivf(color, (float)ns);
+                    float l = lum(color);
+                    if (l > d->max_luminance) color = vscale(d->max_luminance / l, color);
+                    float* o = rgb + ((size_t)x + (size_t)y * d->width) * 4;
+                    o[0] = color.x; o[1] = color.y; o[2] = color.z; o[3] = 0;
+                }
+    } else { /* draw2() over work_queue_dynamic: item c -> tile c % nt, sample c / nt (main.cpp:193-243, work_queue.cpp:157-166) */
+        for (uint64_t c = 0; c < (uint64_t)nt * ns; c++) {
+            const otile* t = &tiles[c % nt];
+            uint32_t s = (uint32_t)(c / nt);
+            for (uint32_t y = t->y0; y < t->y1; y++)
+                for (uint32_t x = t->x0; x < t->x1; x++) {
+                    float* o = rgb + ((size_t)x + (size_t)y * d->width) * 4;
+                    V old = v3(o[0], o[1], o[2]);
+                    uint32_t rr;
+                    V color = path_with(&C, d, x, y, s, &rr);
+                    rays += rr;
+                    if (!isfinite(color.x) || !isfinite(color.y) || !isfinite(color.z)) color = s > 0 ? old : v3(0, 0, 0);
+                    if (s > 0) color = vadd(old, vscale(1.0f / (s + 1.0f), vsub(color, old)));
+                    float l = lum(color);
+                    if (l > d->max_luminance) color = vscale(d->max_luminance / l, color);
+                    o[0] = color.x; o[1] = color.y; o[2] = color.z; o[3] = 0;
+                }
+        }
+    }
+    free(tiles);
     return rays;
 }
 

@@ -31,6 +31,14 @@ typedef struct oracle_desc {
  * radiance (W*H*ns*3, pixel-major [pixel][s]) and ray counts (W*H*ns).  Returns total rays. */
 uint64_t oracle_render(const mrt_scene_view* v, const oracle_desc* d, float* rgb, float* path_rgb, uint32_t* path_rays);
 
+/* The reference's own deterministic mode (-threads 1, main.cpp:347-382): ONE worker stream seeded
+ * (initstate, initseq) = the worker seeds main() draws after select_scene (main.cpp:357-361, see
+ * mrt_worker_seeds), tiles of tile_size in work_queue order; mode 0 = draw() over work_queue_seq
+ * (tile -> row -> pixel -> sample), mode 1 = draw2() over work_queue_dynamic (sample-major passes
+ * over the tiles).  rgb = W*H*4 floats (row 0 = bottom).  Returns G_rayCounter. */
+uint64_t oracle_render_ref_order(const mrt_scene_view* v, const oracle_desc* d, uint32_t tile_size, uint64_t initstate, uint64_t initseq,
+                                 float* rgb);
+
 /* One path (pixel, sample): radiance -> out[3]; returns its ray count. */
 uint32_t oracle_path(const mrt_scene_view* v, const oracle_desc* d, uint32_t x, uint32_t y, uint32_t s, float* out);
 

@@ -1,15 +1,23 @@
 #!/bin/bash
-# Experiment builds: exp/libmrt_<tag>.so from the current sources with extra device defines.
-#   tools/build_variant.sh <tag> "<extra hipcc flags>"
-# (exp/ is git-ignored; it travels to the GPU box for A/B runs with tools/_ab.sh / tools/_abs.sh)
+# Experiment builds: exp/libmrt_<tag>.so from the current sources, the tolerance-contract TU
+# (mrt_kernels.hip, MRT_FAST build) compiled with the given flags instead of the Makefile's
+# FASTFLAGS; the exact TU as in the Makefile unless EXACT_FLAGS is set.
+#   tools/build_variant.sh <tag> "<fast-TU hipcc flags>"
+# Load with MRT_EXPERIMENT_LIB=exp/libmrt_<tag>.so (miniraytracer_amd/_lib.py); exp/ is
+# git-ignored and travels to the GPU box with the tree.
 set -e
 cd "$(dirname "$0")/.."
 tag=$1; shift
 flags="$*"
-make -s build/obj/scene_builder.o build/obj/mrt_common.o
+make -s build/obj/scene_builder.o build/obj/mrt_common.o build/obj/mrt_render.o build/obj/mrt_kernels_exact.o
 mkdir -p exp/obj_$tag
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -w \
-    -mllvm -disable-promote-alloca-to-vector -mllvm -structurizecfg-skip-uniform-regions $flags -c miniraytracer_amd/csrc/mrt_render.hip -o exp/obj_$tag/mrt_render.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC exp/obj_$tag/mrt_render.o build/obj/scene_builder.o \
-    build/obj/mrt_common.o -ldl -o exp/libmrt_$tag.so
+BASE="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-fast-math -fno-slp-vectorize -w -mllvm -disable-promote-alloca-to-vector -mllvm -structurizecfg-skip-uniform-regions -DMRT_EXPERIMENTS"
+/opt/rocm/bin/hipcc $BASE -DMRT_TABLE_FAST=1 $flags -c miniraytracer_amd/csrc/mrt_kernels.hip -o exp/obj_$tag/mrt_kernels_fast.o
+EX=build/obj/mrt_kernels_exact.o
+if [ -n "${EXACT_FLAGS:-}" ]; then
+  /opt/rocm/bin/hipcc $BASE -ffp-contract=off -DMRT_FAST=0 $EXACT_FLAGS -c miniraytracer_amd/csrc/mrt_kernels.hip -o exp/obj_$tag/mrt_kernels_exact.o
+  EX=exp/obj_$tag/mrt_kernels_exact.o
+fi
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC build/obj/mrt_render.o $EX exp/obj_$tag/mrt_kernels_fast.o \
+    build/obj/scene_builder.o build/obj/mrt_common.o -ldl -o exp/libmrt_$tag.so
 echo "built exp/libmrt_$tag.so"
