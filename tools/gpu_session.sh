@@ -18,4 +18,5 @@ step() {  # name timeout cmd...
 [ "${SKIP_TESTS:-0}" = 1 ] || step gpu_tests 900 python -u -m pytest ${TESTS:-tests/} -x -v -m gpu --timeout 300 --timeout-method thread
 [ "${SKIP_BENCH:-0}" = 1 ] || step bench 600 python bench.py ${BENCH_ARGS:-}
 [ "${SKIP_PROF:-0}" = 1 ] || step prof 900 bash tools/profile.sh
+[ "${PROF_CFG:-0}" = 1 ] && step prof_cfg 1200 bash tools/prof_configs.sh
 exit 0
