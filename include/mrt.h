@@ -73,6 +73,11 @@ void mrt_free_string(char* s);
  * mrt_select_scene; used when the .obj itself is not shipped). */
 mrt_status mrt_pack_obj(const char* obj_path, const char* out_path);
 void mrt_scene_blob_free(mrt_scene_blob* blob);
+/* The (initstate, initseq) main() hands its worker threads (main.cpp:357-361): drawn from the main
+ * thread's PCG after select_scene consumed what it needs.  Only the reference's own deterministic
+ * mode (-threads 1) depends on them: the CPU backend's ref-order renders and the oracle's
+ * reference-RNG-order restatement use them; the GPU path keys its streams per path instead. */
+mrt_status mrt_worker_seeds(const mrt_scene_blob* blob, uint32_t n_threads, uint64_t* initstate, uint64_t* initseq);
 
 /* ---- device -------------------------------------------------------------------------------- */
 mrt_status mrt_init(int* device_count);

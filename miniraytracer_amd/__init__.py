@@ -60,6 +60,13 @@ class Scene:
         finally:
             lib().mrt_free_string(out)
 
+    def worker_seeds(self, n_threads):
+        """[(initstate, initseq)] main() gives its worker threads (main.cpp:357-361)."""
+        a = np.zeros(n_threads, dtype=np.uint64)
+        b = np.zeros(n_threads, dtype=np.uint64)
+        check(lib().mrt_worker_seeds(self._h, n_threads, a.ctypes.data, b.ctypes.data), "mrt_worker_seeds")
+        return [(int(x), int(y)) for x, y in zip(a, b)]
+
     def close(self):
         if self._h:
             lib().mrt_scene_blob_free(self._h)

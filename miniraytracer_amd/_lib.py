@@ -115,6 +115,8 @@ def lib():
     L.mrt_scene_kernel_info.restype = st
     L.mrt_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_uint32)]
     L.mrt_kernel_ms.restype = st
+    L.mrt_worker_seeds.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
+    L.mrt_worker_seeds.restype = st
     L.mrt_pack_obj.argtypes = [C.c_char_p, C.c_char_p]
     L.mrt_pack_obj.restype = st
     L.mrt_tonemap_argb.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
@@ -139,5 +141,5 @@ EXPORTS = [
     "mrt_scene_upload", "mrt_scene_free", "mrt_default_render_desc", "mrt_local_pixels",
     "mrt_render", "mrt_render_device", "mrt_prepare", "mrt_render_debug", "mrt_progress",
     "mrt_tonemap_argb", "mrt_strerror", "mrt_last_error", "mrt_kernel_ms", "mrt_pack_obj",
-    "mrt_scene_kernel_info", "mrt_lum_max_device", "mrt_tonemap_device",
+    "mrt_scene_kernel_info", "mrt_lum_max_device", "mrt_tonemap_device", "mrt_worker_seeds",
 ]

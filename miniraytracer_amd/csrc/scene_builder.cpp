@@ -891,6 +891,7 @@ struct mrt_scene_blob {
     std::vector<uint8_t> texels;
     float ranvec[256 * 4];
     int32_t perm[3 * 256];
+    Pcg main_rng;  // main()'s T_rng after select_scene: the worker seeds come from it (main.cpp:357-361)
 };
 
 static std::string default_asset_dir() {
@@ -920,6 +921,7 @@ extern "C" mrt_status mrt_select_scene(uint32_t scene, float aspect, const char*
     }
     if (B.err != MRT_OK) return mrt_internal_fail(B.err, B.errmsg.c_str());
     mrt_scene_blob* b = new mrt_scene_blob();
+    b->main_rng = rng;
     uint32_t root = emit(b->flat, S.objects);
     uint32_t biased = S.biased ? emit(b->flat, S.biased) : MRT_NONE;
     b->mats = std::move(B.mats);
@@ -954,6 +956,21 @@ extern "C" mrt_status mrt_scene_blob_view(const mrt_scene_blob* blob, mrt_scene_
 }
 
 extern "C" void mrt_scene_blob_free(mrt_scene_blob* blob) { delete blob; }
+
+// main.cpp:357-361: for each worker, initstate = rand32() << 32 | rand32(), then initseq the same
+// way, drawn from main()'s T_rng after scene generation (operands of | left to right, as clang
+// evaluates the reference's expression)
+extern "C" mrt_status mrt_worker_seeds(const mrt_scene_blob* blob, uint32_t n_threads, uint64_t* initstate, uint64_t* initseq) {
+    if (!blob || (n_threads && (!initstate || !initseq))) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_worker_seeds: null");
+    Pcg r = blob->main_rng;
+    for (uint32_t i = 0; i < n_threads; i++) {
+        uint64_t hi = pcg_next(r);
+        initstate[i] = (hi << 32) | pcg_next(r);
+        hi = pcg_next(r);
+        initseq[i] = (hi << 32) | pcg_next(r);
+    }
+    return MRT_OK;
+}
 
 // ---- JSON dump in the schema of oracle/ref/harness.cpp (--h-mode scene) ----
 static std::string Fb(float f) {

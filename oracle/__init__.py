@@ -42,6 +42,8 @@ def lib():
         L.oracle_path.restype = C.c_uint32
         L.oracle_hit.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_float, C.c_int, C.c_uint64, C.c_void_p]
         L.oracle_hit.restype = C.c_int
+        L.oracle_render_ref_order.argtypes = [C.c_void_p, C.POINTER(OracleDesc), C.c_uint32, C.c_uint64, C.c_uint64, C.c_void_p]
+        L.oracle_render_ref_order.restype = C.c_uint64
         L.oracle_pcg_stream.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p]
         L.oracle_samplers.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_void_p]
         _lib = L
@@ -63,6 +65,16 @@ def render(scene, d, paths=False):
     rays = lib().oracle_render(C.byref(scene.view), C.byref(d), img.ctypes.data,
                                prgb.ctypes.data if paths else None, prays.ctypes.data if paths else None)
     return img, rays, prgb, prays
+
+
+def render_ref_order(scene, d, tile_size=32):
+    """The reference's own deterministic mode (-threads 1): one worker stream seeded as main() seeds
+    worker 0 (main.cpp:357-361), work_queue tile order, draw() (mode 0) / draw2() (mode 1).
+    Returns (image [H, W, 4], rays)."""
+    img = np.zeros((d.height, d.width, 4), dtype=np.float32)
+    st, sq = scene.worker_seeds(1)[0]
+    rays = lib().oracle_render_ref_order(C.byref(scene.view), C.byref(d), tile_size, st, sq, img.ctypes.data)
+    return img, rays
 
 
 def hit(scene, o, d, time, inside, seed=0):

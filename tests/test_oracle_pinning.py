@@ -105,3 +105,30 @@ def test_restatement_within_tolerance_of_shipped_numerics(mrt, orc, sid):
     assert float(np.sqrt((d ** 2).mean())) < 1e-3
     assert np.abs(d.reshape(-1, 3).mean(axis=0)).max() < 1e-4
     assert abs(rays / float(g["rays"][0]) - 1) < 1e-3
+
+
+def test_worker_seeds_match_reference_main(mrt):
+    """main.cpp:357-361: the (initstate, initseq) main() draws for its workers after select_scene.
+    Scene 5 consumes no RNG while it is built, so these are the SURVEY 8(c) vector (clang's left-to-
+    right evaluation of `(uint64(rand32()) << 32) | rand32()`)."""
+    sc = mrt.select_scene(5, 1.0)
+    assert sc.worker_seeds(2) == [(6838637184523169570, 909894286423444019), (11866281134630579356, 5863659702987752277)]
+
+
+REFSEQ = [(s, md) for s in (0, 5, 7, 8) for md in (0, 1)]
+
+
+@pytest.mark.parametrize("sid,mode", REFSEQ)
+def test_oracle_reproduces_reference_threads1_mode(mrt, orc, sid, mode):
+    """The reference's OWN deterministic mode (-threads 1 -mode 0/1, fixtures refseq_<sid>_m<mode>
+    from the exact reference build): one worker PCG stream seeded as main() seeds it, tiles in
+    work_queue order, pixels row by row, samples (mode 0) or sample-major passes (mode 1).  The C
+    restatement's reference-RNG-order mode reproduces G_linearBackBuffer and G_rayCounter bit for
+    bit."""
+    g = np.load(os.path.join(GOLDEN, f"refseq_{sid}_m{mode}.npz"))
+    _, w, h, spp, depth, ts, md, rays = (int(x) for x in g["meta"])
+    assert md == mode
+    sc = mrt.select_scene(sid, w / h)
+    img, r = orc.render_ref_order(sc, orc.desc(w, h, spp, depth=depth, mode=mode), tile_size=ts)
+    assert r == rays
+    assert np.array_equal(img[..., :3].view(np.uint32), g["image"].view(np.uint32))

@@ -17,6 +17,9 @@ Fixtures (all small; data only -- inputs and expected outputs):
                           block means, channel means, ray count; and whole small images of scenes 5, 8, 9, 7
                           (SHIPPED_SMALL).
                           `--only-shipped-stream` regenerates just these two.
+  refseq_<id>_m<mode>.npz the exact reference build with -threads 1 (its own deterministic mode:
+                          one worker PCG stream, work_queue tile order), image + G_rayCounter
+                          (`--only-refseq`)
 """
 import gzip
 import json
@@ -92,7 +95,29 @@ def shipped_stream(tmp):
         print("shipped stream small", sid, meta)
 
 
+# the reference's own deterministic mode: -threads 1, one worker stream, work_queue tile order
+# (scene id, width, height, samples, depth, tile size); both -mode 0 (draw) and -mode 1 (draw2)
+REFSEQ_CASES = [(0, 60, 30, 16, 8, 16), (5, 48, 40, 16, 32, 16), (7, 40, 40, 4, 32, 16), (8, 40, 40, 9, 32, 16)]
+
+
+def refseq(tmp):
+    """refseq_<sid>_m<mode>.npz: the exact reference build run as shipped with -threads 1 (image =
+    G_linearBackBuffer, rays = G_rayCounter): pins the oracle's reference-RNG-order restatement."""
+    img = os.path.join(tmp, "r.pfm")
+    for sid, w, h, spp, depth, ts in REFSEQ_CASES:
+        for mode in (0, 1):
+            meta = json.loads(run(EXACT, ["-scene", sid, "-width", w, "-height", h, "-samples", spp, "-depth", depth,
+                                          "-tilesize", ts, "-threads", 1, "-mode", mode, "--h-out", img]))
+            np.savez_compressed(os.path.join(OUT, f"refseq_{sid}_m{mode}.npz"), image=read_pfm(img, w, h),
+                                meta=np.array([sid, w, h, spp, depth, ts, mode, meta["rays"]], dtype=np.int64))
+            print("refseq", sid, mode, meta)
+
+
 def main():
+    if "--only-refseq" in sys.argv:
+        with tempfile.TemporaryDirectory() as tmp:
+            refseq(tmp)
+        return
     if "--only-shipped-stream" in sys.argv:
         with tempfile.TemporaryDirectory() as tmp:
             shipped_stream(tmp)
@@ -153,6 +178,7 @@ def main():
             print("tonemap", sid, int(out.min()), int(out.max()))
 
         shipped_stream(tmp)
+        refseq(tmp)
 
         # 5. shipped reference (multithreaded, its own worker seeds): statistical parity fixture
         if os.path.exists(os.path.join(OUT, "shipped_5.npz")) and "--force" not in sys.argv:
