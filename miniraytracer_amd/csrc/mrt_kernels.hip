@@ -63,6 +63,14 @@ extern "C" int mrt_debug_phases(unsigned long long* out, int reset) {
     return 0;
 }
 #endif
+// resumable mesh walk (room + mesh kernels): the walk loop returns the wave to shading / new rays
+// once at most MRT_WALK_MIN lanes still walk and at least MRT_WALK_OTHER lanes have other work
+#ifndef MRT_WALK_MIN
+#define MRT_WALK_MIN 32u
+#endif
+#ifndef MRT_WALK_OTHER
+#define MRT_WALK_OTHER 16u
+#endif
 #if defined(MRT_EXPERIMENTS) && defined(MRT_WPE)  // experiment hook: override for every variant
 #define MRT_OCC(F) MRT_WPE
 #else
@@ -125,190 +133,206 @@ __global__ void __launch_bounds__(MRT_PATH_WG) __attribute__((amdgpu_waves_per_e
 #ifdef MRT_PHASES
     ph.t = __builtin_amdgcn_s_memtime();
 #endif
+    // Lanes without a path take the next path indices from the wave's pool (ballot + mbcnt
+    // compaction), the pool refilled by one atomic per claim (work_queue::getWork,
+    // work_queue.cpp:158-166).  start(u, v) begins a lane's path at camera coordinates (u, v) with
+    // its PCG stream seeded from the path key.
+    auto take_paths = [&](auto&& start) {
+        const uint64_t need = __ballot(!active);
+        if (!need || exhausted) return;
+        const uint32_t c = (uint32_t)__popcll(need);
+        const uint32_t have = (uint32_t)(pool_end - pool_next);
+        // near the end of the launch, claims shrink so the last ones finish together
+        const uint32_t batch = pool_end + P.tail_zone >= P.n_paths ? MRT_TAIL_BATCH : MRT_BATCH;
+        uint64_t nb = 0;
+        if (have < c) {
+            if (lane == 0) {
+                nb = static_paths + atomicAdd(P.counter, (unsigned long long)batch);
+                // every 32nd claim: a system-scope store to host memory, read by mrt_progress
+                // without any GPU queue (a device-to-host copy could wait behind this launch)
+                if (P.hprog && ((nb / MRT_BATCH) & 31u) == 0)
+                    __hip_atomic_store(P.hprog, nb + batch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            nb = __shfl(nb, 0);
+        }
+        PH_MARK(ph, 0);
+        if (!active) {
+            const uint32_t rank = rank_below(need);
+            const uint64_t i = rank < have ? pool_next + rank : nb + (rank - have);
+            if (i < P.n_paths) {
+                idx = (uint32_t)i;
+                // idx = sl * npix + lp; the double estimate is off by at most one either way
+                uint32_t sl = (uint32_t)((double)idx * P.inv_npix);
+                uint32_t lp = idx - sl * P.npix;
+                if ((int32_t)lp < 0) { sl--; lp += P.npix; }
+                if (lp >= P.npix) { sl++; lp -= P.npix; }
+                const uint32_t s = P.s0 + sl;
+                const uint2 xy = P.pixels[lp];
+                const uint32_t x = xy.x, y = xy.y;
+                const uint32_t pix = x + y * P.width;
+                const float2 dd = P.sdist[s];  // ((i + 0.5) / sq, (j + 0.5) / sq), s = i*sq + j
+                // (x + dx) / W with RN(1/W) from the host: numerator >= 1/(2 sq) >= 2^-17, W <= 2^24
+                const float nu = (float)x + dd.x, nv = (float)y + dd.y;
+                float u = div_core(nu, (float)P.width, P.inv_w), v = div_core(nv, (float)P.height, P.inv_h);
+                if (!P.fast_uv) {  // a real (uniform) branch: the barrier keeps it from being if-converted
+                    asm volatile("" ::: "memory");
+                    u = nu / (float)P.width;
+                    v = nv / (float)P.height;
+                }
+                const uint64_t path_id = (uint64_t)pix * P.ns + s;
+                pcg_seed(ps.rng, splitmix64(P.seed ^ path_id), path_id);
+                start(u, v);
+                ps.depth = 0;
+                ps.nlev = 0;
+                ps.rays = 0;
+                active = true;
+            }
+        }
+        PH_MARK(ph, 4);
+        if (have < c) {
+            pool_next = nb + (c - have);
+            pool_end = nb + batch;
+            if (nb >= P.n_paths) exhausted = true;
+        } else {
+            pool_next += c;
+        }
+        if (pool_next >= P.n_paths) exhausted = true;
+    };
+    // a finished path: the recursion's fold, radiance out (sample-major, coalesced), rays counted
+    auto finish_path = [&](f3 L) {
+        L = fold_levels(lev, ps.nlev, L);
+        PH_MARK(ph, 5);
+        float* dst = P.rad + (size_t)idx * 3;
+        dst[0] = L.x;
+        dst[1] = L.y;
+        dst[2] = L.z;
+        if (P.path_rays) P.path_rays[idx] = ps.rays;
+        done_rays += ps.rays;
+        active = false;
+    };
     // mesh variants keep one constructor per branch: the shared-constructor loop spills there
     // (bunny -4%, teapot -5%; Cornell +1.8%, book2 0)
     constexpr bool kShared = (F & FT_MESH) == 0;
+    constexpr bool kResume = MRT_SIG_OF(F) == SIG_ROOM_MESH;
     if constexpr (kShared) {
-    // One iteration: (1) every lane with a ray traces one segment; a path that ends is folded and
-    // stored; (2) lanes without a path take new ones (camera ray arguments); (3) ONE make_ray for
-    // every lane with a next ray -- camera and scattered rays alike, instead of one constructor per
-    // branch at partial lane occupancy; (4) diffuse scatters finish their pdfs on the new ray.
-    PendRay pr;
-    for (;;) {
-        bool want_ray = false;
-        if (active) {
-            f3 L;
-            const bool ended = trace_split<F, LK>(S, ps, P.max_bounces, lev, Ls, &L, &pr, ph);
-            PH_MARK(ph, 2);
-            if (ended) {
-                L = fold_levels(lev, ps.nlev, L);
-                PH_MARK(ph, 5);
-                float* dst = P.rad + (size_t)idx * 3;
-                dst[0] = L.x;
-                dst[1] = L.y;
-                dst[2] = L.z;
-                if (P.path_rays) P.path_rays[idx] = ps.rays;
-                done_rays += ps.rays;
-                active = false;
-            } else {
+        // One iteration: (1) every lane with a ray traces one segment; a path that ends is folded
+        // and stored; (2) lanes without a path take new ones (camera ray arguments); (3) ONE
+        // make_ray for every lane with a next ray -- camera and scattered rays alike, instead of one
+        // constructor per branch at partial lane occupancy; (4) diffuse scatters finish their pdfs
+        // on the new ray.
+        PendRay pr;
+        for (;;) {
+            bool want_ray = false;
+            if (active) {
+                f3 L;
+                const bool ended = trace_split<F, LK>(S, ps, P.max_bounces, lev, Ls, &L, &pr, ph);
+                PH_MARK(ph, 2);
+                if (ended) finish_path(L);
+                else want_ray = true;
+            }
+            PH_MARK(ph, 3);
+            take_paths([&](float u, float v) {
+                camera_ray_args(S, ps.rng, u, v, &pr.o, &pr.dir, &pr.time);
+                pr.inside = 0;
+                pr.kind = 0;
                 want_ray = true;
-            }
-        }
-        PH_MARK(ph, 3);
-        const uint64_t need = __ballot(!active);
-        if (need && !exhausted) {
-            const uint32_t c = (uint32_t)__popcll(need);
-            const uint32_t have = (uint32_t)(pool_end - pool_next);
-            // near the end of the launch, claims shrink so the last ones finish together
-            const uint32_t batch = pool_end + P.tail_zone >= P.n_paths ? MRT_TAIL_BATCH : MRT_BATCH;
-            uint64_t nb = 0;
-            if (have < c) {
-                if (lane == 0) {
-                    nb = static_paths + atomicAdd(P.counter, (unsigned long long)batch);
-                    // every 32nd claim: a system-scope store to host memory, read by mrt_progress
-                    // without any GPU queue (a device-to-host copy could wait behind this launch)
-                    if (P.hprog && ((nb / MRT_BATCH) & 31u) == 0)
-                        __hip_atomic_store(P.hprog, nb + batch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                }
-                nb = __shfl(nb, 0);
-            }
+            });
+            if (!__any(active)) break;
             PH_MARK(ph, 0);
-            if (!active) {
-                const uint32_t rank = rank_below(need);
-                const uint64_t i = rank < have ? pool_next + rank : nb + (rank - have);
-                if (i < P.n_paths) {
-                    idx = (uint32_t)i;
-                    // idx = sl * npix + lp; the double estimate is off by at most one either way
-                    uint32_t sl = (uint32_t)((double)idx * P.inv_npix);
-                    uint32_t lp = idx - sl * P.npix;
-                    if ((int32_t)lp < 0) { sl--; lp += P.npix; }
-                    if (lp >= P.npix) { sl++; lp -= P.npix; }
-                    const uint32_t s = P.s0 + sl;
-                    const uint2 xy = P.pixels[lp];
-                    const uint32_t x = xy.x, y = xy.y;
-                    const uint32_t pix = x + y * P.width;
-                    const float2 dd = P.sdist[s];  // ((i + 0.5) / sq, (j + 0.5) / sq), s = i*sq + j
-                    // (x + dx) / W with RN(1/W) from the host: numerator >= 1/(2 sq) >= 2^-17, W <= 2^24
-                    const float nu = (float)x + dd.x, nv = (float)y + dd.y;
-                    float u = div_core(nu, (float)P.width, P.inv_w), v = div_core(nv, (float)P.height, P.inv_h);
-                    if (!P.fast_uv) {  // a real (uniform) branch: the barrier keeps it from being if-converted
-                        asm volatile("" ::: "memory");
-                        u = nu / (float)P.width;
-                        v = nv / (float)P.height;
-                    }
-                    const uint64_t path_id = (uint64_t)pix * P.ns + s;
-                    pcg_seed(ps.rng, splitmix64(P.seed ^ path_id), path_id);
-                    camera_ray_args(S, ps.rng, u, v, &pr.o, &pr.dir, &pr.time);
-                    pr.inside = 0;
-                    pr.kind = 0;
-                    want_ray = true;
-                    ps.depth = 0;
-                    ps.nlev = 0;
-                    ps.rays = 0;
-                    active = true;
+            if (want_ray) {
+                ps.r = make_ray(pr.o, pr.dir, pr.time, pr.inside);
+                if (pr.kind) finish_scatter<F, LK>(S, ps, lev, pr);
+            }
+            PH_MARK(ph, 7);
+        }
+    } else if constexpr (kResume) {
+        // Cornell room + one pod_bvh mesh (scenes 8 / 9): the mesh walk is RESUMABLE.  Lanes walk
+        // the BVH for different numbers of steps, so a walk run to completion inside one segment
+        // leaves most lanes of the wave idle while the longest walks finish (lane utilisation
+        // 0.13-0.17 measured).  Here a lane's walk state (node ref, stack depth, its LDS stack, the
+        // walls' closest hit) persists across iterations; the walk loop hands the wave back once
+        // few lanes still walk and enough others can shade or start new rays, and the stragglers
+        // resume next iteration beside fresh rays (Aila & Laine 2009 "dynamic ray fetch", per
+        // lane).  Every lane runs the same operations in the same order as mesh_hit: bit-exact.
+        constexpr uint32_t PH_BEGIN = 1, PH_WALK = 2, PH_DONE = 3;
+        using W = SigWalk<F, SIG_ROOM_MESH>;
+        constexpr uint32_t kMeshPC = 7;  // LIST, 6 rects, MESH, LIST_END (mrt_sig.h kSigs)
+        static_assert(kSigs[SIG_ROOM_MESH].op[kMeshPC] == LOP_MESH, "room + mesh program shape");
+        const MRT_CONST_AS LinOp* prog = const_ptr(S.prog);
+        uint32_t phase = 0, ref = 0, msp = 0;
+        SigState w;
+        w.closest = FLT_MAX_;
+        w.hnode = MRT_NONE;
+        w.hinst = MRT_NONE;
+        w.hdone = false;
+        HitRec rec;
+        for (;;) {
+            take_paths([&](float u, float v) {
+                ps.r = camera_ray(S, ps.rng, u, v);
+                phase = PH_BEGIN;
+            });
+            if (!__any(active)) break;
+            PH_MARK(ph, 0);
+            if (phase == PH_BEGIN) {  // the room's walls (scene_hit_sig's ops 0..6), then the mesh root box
+                ps.rays++;
+                w.cur = ps.r;
+                w.closest = FLT_MAX_;
+                w.hnode = MRT_NONE;
+                w.hinst = MRT_NONE;
+                w.hdone = false;
+                const MRT_CONST_AS LinOp& lo = prog[0];
+                const bool in = !(LOP_FLAGS(lo) & MRT_F_HASBOX) || lin_box(lo, w.cur, 0.001f, w.closest);
+                W::template run<1, kMeshPC>(S, prog, 0.001f, w, in, rec, Ls);
+                const mrt_node mn = ld_node(const_ptr(S.nodes) + prog[kMeshPC].node);
+                const MRT_CONST_AS mrt_mesh_node& rt = const_ptr(S.mnodes)[mn.a];
+                const bool enter = in && aabb_hit(f3{rt.bmin[0], rt.bmin[1], rt.bmin[2]}, f3{rt.bmax[0], rt.bmax[1], rt.bmax[2]}, ps.r,
+                                                  0.001f, w.closest);
+                ref = mn.b;
+                msp = 0;
+                phase = enter ? PH_WALK : PH_DONE;
+            }
+            PH_MARK(ph, 1);
+            // at least one step per iteration for every walking lane (no lane starves), then more
+            // while enough lanes walk or too few have anything else to do
+            while (__any(phase == PH_WALK)) {
+                if (phase == PH_WALK) {
+                    const mrt_node mn = ld_node(const_ptr(S.nodes) + prog[kMeshPC].node);
+                    const uint32_t st = mesh_step(S, mn, ps.r, 0.001f, w.closest, rec, Ls, ref, msp, w.hdone);
+                    if (st == 1u) w.hnode = kMeshPC;  // w.closest = the hit's t, w.hdone set
+                    phase = st != 0u ? PH_DONE : PH_WALK;
+                }
+                if ((uint32_t)__popcll(__ballot(phase == PH_WALK)) <= MRT_WALK_MIN &&
+                    (uint32_t)__popcll(__ballot(phase == PH_DONE || (!active && !exhausted))) >= MRT_WALK_OTHER)
+                    break;  // others can shade / start rays: done lanes, or idle lanes with paths left
+            }
+            PH_MARK(ph, 6);
+            if (phase == PH_DONE) {
+                if (!w.hdone && w.hnode != MRT_NONE) W::template derive<0>(prog, w, ps.r, ps.r, rec);
+                f3 L;
+                const bool ended = shade_hit<F, LK>(S, ps, P.max_bounces, lev, w.hnode != MRT_NONE, rec, &L, ph);
+                PH_MARK(ph, 2);
+                phase = PH_BEGIN;
+                if (ended) {
+                    finish_path(L);
+                    phase = 0;
                 }
             }
-            PH_MARK(ph, 4);
-            if (have < c) {
-                pool_next = nb + (c - have);
-                pool_end = nb + batch;
-                if (nb >= P.n_paths) exhausted = true;
-            } else {
-                pool_next += c;
-            }
-            if (pool_next >= P.n_paths) exhausted = true;
+            PH_MARK(ph, 3);
         }
-        if (!__any(active)) break;
-        PH_MARK(ph, 0);
-        if (want_ray) {
-            ps.r = make_ray(pr.o, pr.dir, pr.time, pr.inside);
-            if (pr.kind) finish_scatter<F, LK>(S, ps, lev, pr);
-        }
-        PH_MARK(ph, 7);
-    }
     } else {
-    for (;;) {
-        const uint64_t need = __ballot(!active);
-        if (need && !exhausted) {
-            const uint32_t c = (uint32_t)__popcll(need);
-            const uint32_t have = (uint32_t)(pool_end - pool_next);
-            // near the end of the launch, claims shrink so the last ones finish together
-            const uint32_t batch = pool_end + P.tail_zone >= P.n_paths ? MRT_TAIL_BATCH : MRT_BATCH;
-            uint64_t nb = 0;
-            if (have < c) {
-                if (lane == 0) {
-                    nb = static_paths + atomicAdd(P.counter, (unsigned long long)batch);
-                    // every 32nd claim: a system-scope store to host memory, read by mrt_progress
-                    // without any GPU queue (a device-to-host copy could wait behind this launch)
-                    if (P.hprog && ((nb / MRT_BATCH) & 31u) == 0)
-                        __hip_atomic_store(P.hprog, nb + batch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                }
-                nb = __shfl(nb, 0);
-            }
+        for (;;) {
+            take_paths([&](float u, float v) { ps.r = camera_ray(S, ps.rng, u, v); });
+            if (!__any(active)) break;
             PH_MARK(ph, 0);
-            if (!active) {
-                const uint32_t rank = rank_below(need);
-                const uint64_t i = rank < have ? pool_next + rank : nb + (rank - have);
-                if (i < P.n_paths) {
-                    idx = (uint32_t)i;
-                    // idx = sl * npix + lp; the double estimate is off by at most one either way
-                    uint32_t sl = (uint32_t)((double)idx * P.inv_npix);
-                    uint32_t lp = idx - sl * P.npix;
-                    if ((int32_t)lp < 0) { sl--; lp += P.npix; }
-                    if (lp >= P.npix) { sl++; lp -= P.npix; }
-                    const uint32_t s = P.s0 + sl;
-                    const uint2 xy = P.pixels[lp];
-                    const uint32_t x = xy.x, y = xy.y;
-                    const uint32_t pix = x + y * P.width;
-                    const float2 dd = P.sdist[s];  // ((i + 0.5) / sq, (j + 0.5) / sq), s = i*sq + j
-                    // (x + dx) / W with RN(1/W) from the host: numerator >= 1/(2 sq) >= 2^-17, W <= 2^24
-                    const float nu = (float)x + dd.x, nv = (float)y + dd.y;
-                    float u = div_core(nu, (float)P.width, P.inv_w), v = div_core(nv, (float)P.height, P.inv_h);
-                    if (!P.fast_uv) {  // a real (uniform) branch: the barrier keeps it from being if-converted
-                        asm volatile("" ::: "memory");
-                        u = nu / (float)P.width;
-                        v = nv / (float)P.height;
-                    }
-                    const uint64_t path_id = (uint64_t)pix * P.ns + s;
-                    pcg_seed(ps.rng, splitmix64(P.seed ^ path_id), path_id);
-                    ps.r = camera_ray(S, ps.rng, u, v);
-                    ps.depth = 0;
-                    ps.nlev = 0;
-                    ps.rays = 0;
-                    active = true;
-                }
+            if (active) {
+                f3 L;
+                const bool ended = trace_segment<F, LK>(S, ps, P.max_bounces, lev, Ls, &L, ph);
+                PH_MARK(ph, 2);
+                if (ended) finish_path(L);
             }
-            PH_MARK(ph, 4);
-            if (have < c) {
-                pool_next = nb + (c - have);
-                pool_end = nb + batch;
-                if (nb >= P.n_paths) exhausted = true;
-            } else {
-                pool_next += c;
-            }
-            if (pool_next >= P.n_paths) exhausted = true;
+            PH_MARK(ph, 3);
         }
-        if (!__any(active)) break;
-        PH_MARK(ph, 0);
-        if (active) {
-            f3 L;
-            const bool ended = trace_segment<F, LK>(S, ps, P.max_bounces, lev, Ls, &L, ph);
-            PH_MARK(ph, 2);
-            if (ended) {
-                L = fold_levels(lev, ps.nlev, L);
-                PH_MARK(ph, 5);
-                float* dst = P.rad + (size_t)idx * 3;
-                dst[0] = L.x;
-                dst[1] = L.y;
-                dst[2] = L.z;
-                if (P.path_rays) P.path_rays[idx] = ps.rays;
-                done_rays += ps.rays;
-                active = false;
-            }
-        }
-        PH_MARK(ph, 3);
     }
-}
 #ifdef MRT_PHASES
     if (lane == 0)
         for (int i = 0; i < 8; i++) atomicAdd(&g_phases[i], (unsigned long long)ph.a[i]);

@@ -273,18 +273,13 @@ __device__ __forceinline__ void camera_ray_args(const DScene& S, Pcg& rng, float
     *o = add(origin, offset);
 }
 
-// One segment.  Returns true when the path has ended; its radiance is then in *L.
+// The rest of one segment once scene_object::hit has answered for ps.r: emission, the bounce
+// limit, material::scatter and the next ray.  Returns true when the path has ended; its radiance
+// is then in *L.
 template <uint32_t F, uint32_t LK>
-__device__ __forceinline__ bool trace_segment(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev,
-                                              const LStack& Ls, f3* L, PhaseClock& ph) {
-    ps.rays++;
-    HitRec rec;
+__device__ __forceinline__ bool shade_hit(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev, bool hit,
+                                          const HitRec& rec, f3* L, PhaseClock& ph) {
     Ray& r = ps.r;
-    bool hit;
-    if constexpr (MRT_SIG_OF(F) != SIG_NONE) hit = scene_hit_sig<F>(S, r, 0.001f, rec, Ls);
-    else if constexpr ((F & FT_LIN) != 0) hit = scene_hit_lin<F>(S, r, 0.001f, rec, Ls, ps.rng);
-    else hit = scene_hit<F>(S, r, 0.001f, rec, ps.rng, Ls);
-    PH_MARK(ph, 1);
     if (!hit) {
         if ((F & FT_SKY) && S.sky) {  // main.cpp:113-115
             float tt = 0.5f * (r.d.y + 1.0f);
@@ -386,6 +381,20 @@ __device__ __forceinline__ bool trace_segment(const DScene& S, PathState& ps, ui
     ps.nlev = (ps.nlev + 1) | (quiet_level(lv) ? 0u : LEV_LOUD);
     r = sc;
     return false;
+}
+
+// One segment.  Returns true when the path has ended; its radiance is then in *L.
+template <uint32_t F, uint32_t LK>
+__device__ __forceinline__ bool trace_segment(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev,
+                                              const LStack& Ls, f3* L, PhaseClock& ph) {
+    ps.rays++;
+    HitRec rec;
+    bool hit;
+    if constexpr (MRT_SIG_OF(F) != SIG_NONE) hit = scene_hit_sig<F>(S, ps.r, 0.001f, rec, Ls);
+    else if constexpr ((F & FT_LIN) != 0) hit = scene_hit_lin<F>(S, ps.r, 0.001f, rec, Ls, ps.rng);
+    else hit = scene_hit<F>(S, ps.r, 0.001f, rec, ps.rng, Ls);
+    PH_MARK(ph, 1);
+    return shade_hit<F, LK>(S, ps, max_bounces, lev, hit, rec, L, ph);
 }
 
 // The next ray of a lane, built by make_ray once per iteration for all lanes at once (camera

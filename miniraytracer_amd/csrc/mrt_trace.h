@@ -375,6 +375,62 @@ __device__ __forceinline__ bool mesh_hit(const DScene& S, const mrt_node& n, con
 #endif
 }
 
+// One step of mesh_hit's walk for a lane whose state persists between calls (ref, msp and its LDS
+// stack; inside a leaf: the triangles left in ref, the leaf's running closest in tt, the best
+// triangle so far in rec.mat / rec.u / rec.v, `in_hit` set once one hit).  A step is an inner
+// node's two boxes or ONE triangle of a leaf, so lanes in leaves of different sizes (up to 25
+// triangles) and lanes at inner nodes cost about the same per step.  Returns 0: keep walking,
+// 1: hit (rec complete, tt = its t; the walk is over: first-hit early-out), 2: no hit.  Every lane
+// performs mesh_hit's operations in mesh_hit's order: the results are bit-identical.
+__device__ __forceinline__ uint32_t mesh_step(const DScene& S, const mrt_node& n, const Ray& r, float tmin, float& tt, HitRec& rec,
+                                              const LStack& L, uint32_t& ref, uint32_t& msp, bool& in_hit) {
+    if (ref & MESH_LEAF) {
+        const uint32_t first = ref & 0xFFFFFFu, cnt = (ref >> 24) & 0x7Fu;
+        float t, uu, vv;
+        if (cnt > 0 && tri_hit(S, first, r, tmin, tt, &t, &uu, &vv)) {
+            in_hit = true;
+            tt = t;
+            rec.mat = first;
+            rec.u = uu;
+            rec.v = vv;
+        }
+        if (cnt > 1) {
+            ref = MESH_LEAF | ((cnt - 1) << 24) | (first + 1);
+            return 0u;
+        }
+        if (in_hit) {  // mesh_leaf's record of the leaf's closest triangle
+            const uint32_t best = rec.mat;
+            const float bu = rec.u, bv = rec.v;
+            const float4* q = S.tri_nrm + (size_t)best * 3;
+            f3 nm = ld3(q[0]), nu = ld3(q[1]), nv = ld3(q[2]);
+            rec.t = tt;
+            rec.p = eval(r, tt);
+            rec.n = normalize(add(add(mulf(nm, (1 - bu) - bv), mulf(nu, bu)), mulf(nv, bv)));
+            rec.mat = n.mat;
+            return 1u;
+        }
+    } else {
+        const WideNode W = load_wide(S.mwide + ref);
+        const bool hl = aabb_hit(W.lmin, W.lmax, r, tmin, tt);
+        const bool hr = aabb_hit(W.rmin, W.rmax, r, tmin, tt);
+        const bool left_first = (W.order & r.mask) != 0;
+        const uint32_t cref = left_first ? W.lref : W.rref, fref = left_first ? W.rref : W.lref;
+        const bool hc = left_first ? hl : hr, hf = left_first ? hr : hl;
+        if (hc) {
+            if (hf) L.mesh[(msp++) * 64 + L.lane] = fref;
+            ref = cref;
+            return 0u;
+        }
+        if (hf) {
+            ref = fref;
+            return 0u;
+        }
+    }
+    if (msp == 0) return 2u;
+    ref = L.mesh[(--msp) * 64 + L.lane];
+    return 0u;
+}
+
 template <uint32_t F>
 __device__ __forceinline__ bool leaf_prim_hit(const mrt_node& n, uint32_t kind, const Ray& r, float tmin, float tmax, HitRec& rec, bool full) {
     switch (kind) {
