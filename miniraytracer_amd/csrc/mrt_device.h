@@ -363,7 +363,7 @@ __device__ __forceinline__ f3 ld3(const MRT_CONST_AS float* p) { return f3{p[0],
 // Phase clock (experiment builds with -DMRT_PHASES): wave-uniform s_memtime deltas per phase.
 #ifdef MRT_PHASES
 struct PhaseClock {
-    uint64_t t, a[8];
+    uint64_t t, a[12];  // 0-7: path loop phases; 8-11: inside scene_hit_lin (lists/instances, prims, volumes, BVHs)
 };
 #define PH_MARK(pc, i)                                      \
     do {                                                    \

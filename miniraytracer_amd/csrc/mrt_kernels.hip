@@ -53,11 +53,11 @@ template <uint32_t F> struct PathOcc {
     static constexpr int W = kWide ? MRT_WPE_WIDE : ((F & FT_MESH) != 0 ? MRT_WPE_MESH : MRT_WPE_LIN);
 };
 #if defined(MRT_EXPERIMENTS) && defined(MRT_PHASES) && !MRT_FAST
-__device__ unsigned long long g_phases[8];
+__device__ unsigned long long g_phases[12];
 extern "C" int mrt_debug_phases(unsigned long long* out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phases), sizeof(g_phases)) != hipSuccess) return 1;
     if (reset) {
-        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long z[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_phases), z, sizeof(z)) != hipSuccess) return 1;
     }
     return 0;
@@ -335,7 +335,7 @@ __global__ void __launch_bounds__(MRT_PATH_WG) __attribute__((amdgpu_waves_per_e
     }
 #ifdef MRT_PHASES
     if (lane == 0)
-        for (int i = 0; i < 8; i++) atomicAdd(&g_phases[i], (unsigned long long)ph.a[i]);
+        for (int i = 0; i < 12; i++) atomicAdd(&g_phases[i], (unsigned long long)ph.a[i]);
 #endif
     // one 64-bit add per wave
     uint64_t my = done_rays;

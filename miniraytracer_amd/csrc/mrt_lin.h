@@ -253,7 +253,7 @@ __device__ __forceinline__ void lin_untransform(const OP& io, HitRec& rec) {
 // LDS per lane (L.save): [0..8] the query ray, [9..14] origin/direction of the instance ray of
 // the closest hit (written at the instance's END op when that hit lies inside it).
 template <uint32_t F>
-__device__ __forceinline__ bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, const LStack& L, Pcg& rng) {
+__device__ __forceinline__ bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, const LStack& L, Pcg& rng, PhaseClock& ph) {
     constexpr bool INST = (F & FT_INST) != 0;
     if (INST) lin_save_ray(L, r);
     Ray cur = r;
@@ -284,6 +284,7 @@ __device__ __forceinline__ bool scene_hit_lin(const DScene& S, Ray& r, float tmi
             hnode = h ? o.node : hnode;
             hinst = h ? inst : hinst;
             hdone = h ? false : hdone;
+            PH_MARK(ph, 9);
         } else if ((F & FT_MESH) && op == LOP_MESH) {
             if (on && mesh_hit<true>(S, ld_node(const_ptr(S.nodes) + o.node), cur, tmin, closest, rec, true, L)) {
                 closest = rec.t;
@@ -330,6 +331,7 @@ __device__ __forceinline__ bool scene_hit_lin(const DScene& S, Ray& r, float tmi
                 }
             }
             pc++;  // past the boundary op
+            PH_MARK(ph, 10);
         } else if ((F & FT_BVHW) && op == LOP_BVHW) {
             if (on && bvhw_hit<F>(S, S.nodes[o.node], cur, tmin, closest, rec, true, L)) {
                 closest = rec.t;
@@ -337,6 +339,7 @@ __device__ __forceinline__ bool scene_hit_lin(const DScene& S, Ray& r, float tmi
                 hinst = inst;
                 hdone = true;
             }
+            PH_MARK(ph, 11);
         } else if (op == LOP_LIST) {  // object_list::hit box reject (scene_object.h:83)
             bool in = on;
             if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, cur, tmin, closest);
@@ -375,6 +378,7 @@ __device__ __forceinline__ bool scene_hit_lin(const DScene& S, Ray& r, float tmi
         } else if (op == LOP_LIST_END) {
             lvl--;
         }
+        PH_MARK(ph, 8);
     }
     if (INST) r = lin_load_ray(L);
     if (hnode == MRT_NONE) return false;

@@ -467,6 +467,7 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     // bvh_node subtrees whose leaves are primitives / object_lists of primitives (and of boxes of
     // primitives) -> wide nodes; the subtree root becomes an MRT_K_BVHW node (a = root ref)
     std::vector<BvhWide> bwide;
+    std::vector<mrt_node> bprims;  // leaf primitive runs of the wide subtrees
     int bvhw_depth = 0;
     std::vector<uint8_t> absorbed(nodes.size(), 0);  // bvh_nodes now inside a wide subtree
     {
@@ -505,9 +506,35 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
             if (kind_of(i) != MRT_K_BVH) return leaf_ok(i);
             return ok(nodes[i].a, guard + 1) && ok(nodes[i].b, guard + 1);
         };
+        // a leaf's primitives as one contiguous run of node records (bprims): a primitive leaf is a
+        // run of one; an object_list leaf is its children in order, a nested object_list as a LIST
+        // record (its box, b = the count of its own children that follow) before its children.  The
+        // walk then fetches a leaf's records at independent addresses instead of through the
+        // children[] -> node chain (two dependent loads per primitive).
+        bool leaves_ok = true;
+        auto emit_leaf = [&](uint32_t i) -> uint32_t {
+            const uint32_t first = (uint32_t)bprims.size();
+            if (is_leaf_prim(i)) {
+                bprims.push_back(nodes[i]);
+            } else {
+                const mrt_node& l = nodes[i];
+                for (uint32_t c = 0; c < l.b; c++) {
+                    const uint32_t ci = v->children[l.a + c];
+                    if (is_leaf_prim(ci)) { bprims.push_back(nodes[ci]); continue; }
+                    const mrt_node& g = nodes[ci];
+                    mrt_node m = g;
+                    m.b = g.b;
+                    bprims.push_back(m);
+                    for (uint32_t j = 0; j < g.b; j++) bprims.push_back(nodes[v->children[g.a + j]]);
+                }
+            }
+            const uint32_t cnt = (uint32_t)bprims.size() - first;
+            if (cnt > BVHW_MAX_RUN || first > BVHW_FIRST_MASK) leaves_ok = false;
+            return BVHW_LEAF | (cnt << 24) | (first & BVHW_FIRST_MASK);
+        };
         std::function<uint32_t(uint32_t, int)> build = [&](uint32_t i, int depth) -> uint32_t {
             bvhw_depth = std::max(bvhw_depth, depth);
-            if (kind_of(i) != MRT_K_BVH) return BVHW_LEAF | i;
+            if (kind_of(i) != MRT_K_BVH) return emit_leaf(i);
             absorbed[i] = 1;
             const uint32_t w = (uint32_t)bwide.size();
             bwide.push_back(BvhWide{});
@@ -537,6 +564,7 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
                     r.kind = (r.kind & ~0xFFu) | MRT_K_BVHW;
                     r.a = root;
                 }
+        if (!leaves_ok) return mrt_internal_fail(MRT_ERR_INVALID, "bvh_node leaf outside the device encoding (> 127 primitives or > 2^24 leaf records)");
     }
     GraphCheck gc{nodes, v};
     gc.bvhw_depth = bvhw_depth;
@@ -561,6 +589,7 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     UP(v->mesh_nodes, v->n_mesh_nodes, &S.mnodes);
     UP(wide.data(), wide.size(), &S.mwide);
     UP(bwide.data(), bwide.size(), &S.bwide);
+    UP(bprims.data(), bprims.size(), &S.bprims);
     UP((const float4*)v->tri_geo, (size_t)v->n_tris * 3, &S.tri_geo);
     UP((const float4*)v->tri_nrm, (size_t)v->n_tris * 3, &S.tri_nrm);
     std::vector<DMat> dmats(v->n_materials);

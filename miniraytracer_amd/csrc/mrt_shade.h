@@ -391,7 +391,7 @@ __device__ __forceinline__ bool trace_segment(const DScene& S, PathState& ps, ui
     HitRec rec;
     bool hit;
     if constexpr (MRT_SIG_OF(F) != SIG_NONE) hit = scene_hit_sig<F>(S, ps.r, 0.001f, rec, Ls);
-    else if constexpr ((F & FT_LIN) != 0) hit = scene_hit_lin<F>(S, ps.r, 0.001f, rec, Ls, ps.rng);
+    else if constexpr ((F & FT_LIN) != 0) hit = scene_hit_lin<F>(S, ps.r, 0.001f, rec, Ls, ps.rng, ph);
     else hit = scene_hit<F>(S, ps.r, 0.001f, rec, ps.rng, Ls);
     PH_MARK(ph, 1);
     return shade_hit<F, LK>(S, ps, max_bounces, lev, hit, rec, L, ph);
@@ -418,7 +418,7 @@ __device__ __forceinline__ bool trace_split(const DScene& S, PathState& ps, uint
     Ray& r = ps.r;
     bool hit;
     if constexpr (MRT_SIG_OF(F) != SIG_NONE) hit = scene_hit_sig<F>(S, r, 0.001f, rec, Ls);
-    else if constexpr ((F & FT_LIN) != 0) hit = scene_hit_lin<F>(S, r, 0.001f, rec, Ls, ps.rng);
+    else if constexpr ((F & FT_LIN) != 0) hit = scene_hit_lin<F>(S, r, 0.001f, rec, Ls, ps.rng, ph);
     else hit = scene_hit<F>(S, r, 0.001f, rec, ps.rng, Ls);
     PH_MARK(ph, 1);
     if (!hit) {

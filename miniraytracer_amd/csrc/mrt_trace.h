@@ -34,8 +34,9 @@ struct DMat {
 
 // bvh_node (scene_object.h:138-244) subtree as wide nodes: both children's boxes inline.  flags:
 // bit 0 / 1 = the left / right child has a box (bvh_node, object_list with hasBox); primitives
-// are hit() directly.  Child ref: inner -> index into the wide array; leaf -> BVHW_LEAF | node
-// index of the primitive or object_list.
+// are hit() directly.  Child ref: inner -> index into the wide array; leaf -> BVHW_LEAF |
+// count << 24 | first: a run of `count` node records in DScene::bprims (the leaf primitive, or an
+// object_list leaf's children in order, nested object_lists as a LIST record before their children).
 struct BvhWide {
     float lmin[3];
     uint32_t lref;
@@ -47,6 +48,8 @@ struct BvhWide {
     uint32_t flags;
 };
 #define BVHW_LEAF 0x80000000u
+#define BVHW_MAX_RUN 0x7Fu
+#define BVHW_FIRST_MASK 0xFFFFFFu
 
 // A wide node (MeshWide / BvhWide: both children's boxes, refs, order, flags) fetched whole: four
 // 16-byte loads issued together, so one memory round trip per node visit.  (Read field by field,
@@ -106,6 +109,7 @@ struct DScene {
     const mrt_mesh_node* __restrict__ mnodes;
     const MeshWide* __restrict__ mwide;
     const BvhWide* __restrict__ bwide;
+    const mrt_node* __restrict__ bprims;  // leaf primitive runs of the wide subtrees
     const float4* __restrict__ tri_geo;
     const float4* __restrict__ tri_nrm;
     const DMat* __restrict__ mats;
@@ -443,27 +447,27 @@ __device__ __forceinline__ bool leaf_prim_hit(const mrt_node& n, uint32_t kind, 
 
 // a bvh_node leaf: a primitive, or an object_list (its box already tested by the parent) of
 // primitives and object_lists of primitives (box, box.h:6-30) -- object_list::hit semantics,
-// the running closest narrowing across children (scene_object.h:79-103)
+// the running closest narrowing across children (scene_object.h:79-103).  The leaf is a run of
+// node records (BVHW_LEAF ref); a nested list's record carries its box and child count.
 template <uint32_t F>
-__device__ __forceinline__ bool bvhw_leaf(const DScene& S, uint32_t node, const Ray& r, float tmin, float tmax, HitRec& rec, bool full) {
-    const mrt_node n = ld_node_v(S.nodes + node);
-    const uint32_t k = MRT_NODE_KIND(n);
-    if (k != MRT_K_LIST) return leaf_prim_hit<F>(n, k, r, tmin, tmax, rec, full);
+__device__ __forceinline__ bool bvhw_leaf(const DScene& S, uint32_t ref, const Ray& r, float tmin, float tmax, HitRec& rec, bool full) {
+    const uint32_t first = ref & BVHW_FIRST_MASK, cnt = (ref >> 24) & BVHW_MAX_RUN;
+    const mrt_node* run = S.bprims + first;
+    if (cnt == 1) {  // a primitive leaf (or a list of one): hit() with the bvh_node's (tmin, tmax)
+        const mrt_node n = ld_node_v(run);
+        const uint32_t k = MRT_NODE_KIND(n);
+        return k != MRT_K_LIST && leaf_prim_hit<F>(n, k, r, tmin, tmax, rec, full);
+    }
     float closest = tmax;
     bool hit = false;
-    for (uint32_t i = 0; i < n.b; i++) {
-        const mrt_node c = ld_node_v(S.nodes + S.children[n.a + i]);
+    for (uint32_t i = 0; i < cnt; i++) {
+        const mrt_node c = ld_node_v(run + i);
         const uint32_t ck = MRT_NODE_KIND(c);
         if (ck == MRT_K_LIST) {
-            if ((MRT_NODE_FLAGS(c) & MRT_F_HASBOX) && !aabb_hit(c.f, c.f + 3, r, tmin, closest)) continue;
-            for (uint32_t j = 0; j < c.b; j++) {
-                const mrt_node g = ld_node_v(S.nodes + S.children[c.a + j]);
-                if (leaf_prim_hit<F>(g, MRT_NODE_KIND(g), r, tmin, closest, rec, full)) {
-                    hit = true;
-                    closest = rec.t;
-                }
-            }
-        } else if (leaf_prim_hit<F>(c, ck, r, tmin, closest, rec, full)) {
+            if ((MRT_NODE_FLAGS(c) & MRT_F_HASBOX) && !aabb_hit(c.f, c.f + 3, r, tmin, closest)) i += c.b;
+            continue;
+        }
+        if (leaf_prim_hit<F>(c, ck, r, tmin, closest, rec, full)) {
             hit = true;
             closest = rec.t;
         }
@@ -504,14 +508,14 @@ __device__ __forceinline__ bool bvhw_hit(const DScene& S, const mrt_node& n, con
                 ref = L.mesh[(--sp) * 64 + L.lane];
             }
         }
-        if (bvhw_leaf<F>(S, ref & ~BVHW_LEAF, r, tmin, tmax, rec, full)) return true;
+        if (bvhw_leaf<F>(S, ref, r, tmin, tmax, rec, full)) return true;
         if (sp == 0) return false;
         ref = L.mesh[(--sp) * 64 + L.lane];
     }
 #else
     for (;;) {
         if (ref & BVHW_LEAF) {
-            if (bvhw_leaf<F>(S, ref & ~BVHW_LEAF, r, tmin, tmax, rec, full)) return true;
+            if (bvhw_leaf<F>(S, ref, r, tmin, tmax, rec, full)) return true;
         } else {
             const WideNode W = load_wide(S.bwide + ref);
             const bool hl = !(W.flags & 1u) || aabb_hit(W.lmin, W.lmax, r, tmin, tmax);

@@ -11,13 +11,13 @@ sc = m.select_scene(scene, w / h)
 r = m.Renderer(sc, 0)
 d = m.render_desc(w, h, spp)
 r.render(d)
-NPH = int(__import__('os').environ.get('NPH', '4'))
+NPH = int(__import__("os").environ.get("NPH", "12"))
 out = (C.c_ulonglong * NPH)()
 lib().mrt_debug_phases(out, 1)
 img, rays = r.render(d)
 lib().mrt_debug_phases(out, 1)
 v = np.array(list(out), dtype=np.float64)
-names = ["loop+pool", "scene_hit", "shade:pdf+lev", "write+bottom", "new path", "fold", "shade:mat+dir", "-"][:NPH]
+names = ["loop+pool", "hit:record", "shade:pdf+lev", "write+bottom", "new path", "fold", "shade:mat+dir", "-", "hit:list/inst", "hit:prim", "hit:volume", "hit:bvh"][:NPH]
 print(f"scene {scene} {w}x{h}x{spp}: rays {rays}")
 for n, x in zip(names, v):
     print(f"  {n:12s} {100 * x / v.sum():6.2f}%")
