@@ -313,7 +313,7 @@ def main():
                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
                     "kernel": "mrt_path_kernel" + ("_fast" if args.numerics == "fast" else ""),
                     "kernel_ms": round(k_ms, 3), "bytes_per_ray": b_ray,
-                    **{k: rnd.kernel_info()[k] for k in ("grid", "lds_bytes", "vgprs")}}
+                    **{k: rnd.kernel_info()[k] for k in ("grid", "wg", "lds_bytes", "vgprs", "tree_nodes")}}
         roofline.update(roofline_counters(args, k_ms))
 
     # the other numerics contract, same protocol (reported beside the headline, never as `value`)

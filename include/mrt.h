@@ -127,9 +127,10 @@ mrt_status mrt_progress(mrt_scene* s, float* pct);
 mrt_status mrt_kernel_ms(mrt_scene* s, float* path_ms, uint32_t* launches);
 
 /* Which path kernel the scene runs: feature bits of the scene (FT_* of mrt_trace.h; bit 11 =
- * linear hit program, DESIGN.md "Kernels"), dynamic LDS bytes per workgroup and grid size. */
+ * linear hit program, DESIGN.md "Kernels"), dynamic LDS bytes per workgroup, grid size in
+ * workgroups, threads per workgroup and the BVH nodes each workgroup keeps in LDS. */
 typedef struct mrt_kernel_info {
-    uint32_t features, kernel_features, lds_bytes, grid, prog_ops, vgprs;
+    uint32_t features, kernel_features, lds_bytes, grid, prog_ops, vgprs, wg, tree_nodes;
 } mrt_kernel_info;
 mrt_status mrt_scene_kernel_info(const mrt_scene* s, mrt_kernel_info* out);
 

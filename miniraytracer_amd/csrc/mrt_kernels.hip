@@ -95,7 +95,7 @@ template <uint32_t F> struct PathLevLds {
                                                                        : 0u;
 };
 template <uint32_t F>
-__global__ void __launch_bounds__(MRT_PATH_WG) __attribute__((amdgpu_waves_per_eu(MRT_OCC(F)))) MRT_PATH_KERNEL(PathParams P) {
+__global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per_eu(MRT_OCC(F)))) MRT_PATH_KERNEL(PathParams P) {
     constexpr uint32_t LK = PathLevLds<F>::K;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t lane = threadIdx.x & 63u;
@@ -103,7 +103,16 @@ __global__ void __launch_bounds__(MRT_PATH_WG) __attribute__((amdgpu_waves_per_e
     const uint32_t words = (P.lds_frames * 2 + P.lds_rays * 11 + P.lds_mesh + P.lds_save + LK * 4) * 64;
     uint32_t* wb = lds + wave * words;
     uint32_t* const wmesh = wb + P.lds_frames * 128 + P.lds_rays * 704;
-    const LStack Ls{wb, (float*)(wb + P.lds_frames * 128), wmesh, (float*)(wmesh + P.lds_mesh * 64), lane};
+    float4* tree = nullptr;
+    if constexpr (TreeOf<F>::on) {
+        // the workgroup's copy of the top wide nodes (after every wave's own region), filled once
+        // before any wave starts a path; no other barrier follows in this persistent kernel
+        tree = reinterpret_cast<float4*>(lds + (TreeOf<F>::wg / 64u) * words);
+        for (uint32_t i = threadIdx.x; i < P.tree_n * 4u; i += blockDim.x) tree[i] = P.tree_src[i];
+        __syncthreads();
+    }
+    const LStack Ls{wb, (float*)(wb + P.lds_frames * 128), wmesh, (float*)(wmesh + P.lds_mesh * 64), lane, tree,
+                    TreeOf<F>::on ? P.tree_n : 0u};
     const DScene& S = P.sc;
     const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const LevStore<LK> lev{(MRT_GLOBAL_AS v4f*)P.lev, P.lev_rows, (uint32_t)slot,
@@ -360,7 +369,11 @@ const KernelTable& mrtd::kernel_table_exact() {
         {kfn<kVariants[0]>(), kfn<kVariants[1]>(), kfn<kVariants[2]>(), kfn<kVariants[3]>(), kfn<kVariants[4]>(),
          kfn<kVariants[5]>(), kfn<kVariants[6]>()},
         {PathLevLds<kVariants[0]>::K, PathLevLds<kVariants[1]>::K, PathLevLds<kVariants[2]>::K, PathLevLds<kVariants[3]>::K,
-         PathLevLds<kVariants[4]>::K, PathLevLds<kVariants[5]>::K, PathLevLds<kVariants[6]>::K}};
+         PathLevLds<kVariants[4]>::K, PathLevLds<kVariants[5]>::K, PathLevLds<kVariants[6]>::K},
+        {TreeOf<kVariants[0]>::wg, TreeOf<kVariants[1]>::wg, TreeOf<kVariants[2]>::wg, TreeOf<kVariants[3]>::wg,
+         TreeOf<kVariants[4]>::wg, TreeOf<kVariants[5]>::wg, TreeOf<kVariants[6]>::wg},
+        {TreeOf<kVariants[0]>::on, TreeOf<kVariants[1]>::on, TreeOf<kVariants[2]>::on, TreeOf<kVariants[3]>::on,
+         TreeOf<kVariants[4]>::on, TreeOf<kVariants[5]>::on, TreeOf<kVariants[6]>::on}};
     static_assert(kNumVariants == 7, "one table entry per variant");
     return t;
 }

@@ -32,16 +32,16 @@ struct PathParams {
     float4* __restrict__ lev;             // fold levels, lane-major: [slot][lev_rows]
     uint32_t lev_rows;                    // levels per lane (max_bounces, at least 1)
     uint32_t lds_frames, lds_rays, lds_mesh, lds_save;  // LDS stack slots / words per lane
+    const float4* tree_src;               // TreeOf<F>::on kernels: BvhWide nodes copied to LDS at start
+    uint32_t tree_n;                      // how many (the first tree_n of the breadth-first array)
 };
 
 typedef void (*path_kernel_t)(PathParams);
 
-// threads per path-kernel workgroup (each wave owns its own LDS slice; a smaller group frees its
-// CU slot as soon as its own waves finish, which matters in a launch's tail)
-#ifndef MRT_PATH_WG
-#define MRT_PATH_WG 64
-#endif
-static constexpr uint32_t kWavesPerWG = MRT_PATH_WG / 64;
+// threads per path-kernel workgroup: TreeOf<F>::wg (mrt_trace.h).  One-wave groups by default
+// (each wave owns its own LDS slice; a small group frees its CU slot as soon as its wave finishes,
+// which matters in a launch's tail); the bvh_node kernels run one 16-wave group per CU that
+// shares a treelet of hot BVH nodes.
 #ifndef MRT_BATCH
 #define MRT_BATCH 256u  // paths a wave claims per atomic on the work counter (one hot address)
 #endif
@@ -68,6 +68,8 @@ struct KernelTable {
     const char* numerics;  // "exact" | "fast"
     path_kernel_t kernel[kNumVariants];
     uint32_t lev_k[kNumVariants];
+    uint32_t wg[kNumVariants];    // threads per workgroup
+    uint32_t tree[kNumVariants];  // 1: the kernel reads the top BvhWide nodes from an LDS treelet
 };
 const KernelTable& kernel_table_exact();
 const KernelTable& kernel_table_fast();

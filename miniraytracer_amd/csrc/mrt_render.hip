@@ -156,7 +156,37 @@ struct PathLaunch {
     int grid = 0;
     size_t lds_bytes = 0;
     uint32_t vgprs = 0;
+    uint32_t wg = 64;     // threads per workgroup
+    uint32_t tree_n = 0;  // BvhWide nodes kept in each workgroup's LDS (treelet kernels)
 };
+
+// Wide nodes renumbered breadth-first over all roots together (level 0 of every tree, then level
+// 1, ...), so the first K nodes of the array are the top levels of the scene's BVHs -- what a
+// treelet of K nodes holds.  Only the labels change: every walk visits the same nodes.
+template <typename W>
+static void bfs_order(std::vector<W>& wide, std::vector<uint32_t*> roots, uint32_t leaf_bit) {
+    const uint32_t n = (uint32_t)wide.size();
+    std::vector<uint32_t> nid(n, MRT_NONE), order;
+    order.reserve(n);
+    for (uint32_t* r : roots)
+        if (!(*r & leaf_bit) && *r < n && nid[*r] == MRT_NONE) { nid[*r] = (uint32_t)order.size(); order.push_back(*r); }
+    for (size_t q = 0; q < order.size(); q++) {
+        const W& w = wide[order[q]];
+        for (uint32_t c : {w.lref, w.rref})
+            if (!(c & leaf_bit) && c < n && nid[c] == MRT_NONE) { nid[c] = (uint32_t)order.size(); order.push_back(c); }
+    }
+    for (uint32_t i = 0; i < n; i++)  // unreachable nodes keep a slot at the end
+        if (nid[i] == MRT_NONE) { nid[i] = (uint32_t)order.size(); order.push_back(i); }
+    auto remap = [&](uint32_t c) { return (c & leaf_bit) || c >= n ? c : nid[c]; };
+    std::vector<W> out(n);
+    for (uint32_t k = 0; k < n; k++) {
+        out[k] = wide[order[k]];
+        out[k].lref = remap(out[k].lref);
+        out[k].rref = remap(out[k].rref);
+    }
+    wide.swap(out);
+    for (uint32_t* r : roots) *r = remap(*r);
+}
 
 struct mrt_scene {
     int device = 0;
@@ -201,7 +231,7 @@ struct mrt_scene {
     uint32_t features = 0, variant = 0;
     uint32_t lds_frames = 0, lds_rays = 0, lds_mesh = 0, lds_save = 0;
     PathLaunch pl[2];            // [0] exact contract, [1] tolerance contract (MRT_RF_FAST)
-    int max_grid = 0;
+    size_t max_threads = 0;  // largest path-kernel grid in threads (per-lane level rows)
     std::vector<hipEvent_t> ev;  // [2*k]: start/stop of path-kernel launch k of the last render
     uint32_t n_launch = 0;
     size_t rad_cap = 0, acc_cap = 0, lev_cap = 0, px_cap = 0, pr_cap = 0, sd_cap = 0, out_cap = 0;
@@ -566,6 +596,12 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
                 }
         if (!leaves_ok) return mrt_internal_fail(MRT_ERR_INVALID, "bvh_node leaf outside the device encoding (> 127 primitives or > 2^24 leaf records)");
     }
+    {  // treelet kernels cache the first nodes of the wide array: the top levels
+        std::vector<uint32_t*> broots;
+        for (mrt_node& n : nodes)
+            if ((n.kind & 0xFF) == MRT_K_BVHW) broots.push_back(&n.a);
+        bfs_order(bwide, broots, BVHW_LEAF);
+    }
     GraphCheck gc{nodes, v};
     gc.bvhw_depth = bvhw_depth;
     gc.walk(v->root, 0, 0, false, 0);
@@ -674,7 +710,9 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     for (int k = 0; k < 2; k++) {
         PathLaunch& L = s->pl[k];
         L.fn = tabs[k]->kernel[s->variant];
-        L.lds_bytes = (size_t)kWavesPerWG * 64 * 4 *
+        L.wg = tabs[k]->wg[s->variant];
+        const uint32_t waves_per_wg = L.wg / 64u;
+        L.lds_bytes = (size_t)waves_per_wg * 64 * 4 *
                       (s->lds_frames * 2 + s->lds_rays * 11 + s->lds_mesh + s->lds_save + tabs[k]->lev_k[s->variant] * 4);
         if (L.lds_bytes > (size_t)prop.sharedMemPerBlock) {
             mrt_scene_free(s);
@@ -683,16 +721,28 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
         hipFuncAttributes fa{};
         HIPCHK(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(L.fn)));
         const int vg = std::max(8, (fa.numRegs + 7) & ~7);
-        int nb = std::min(8, 512 / vg) * (int)(4 / kWavesPerWG);  // waves per SIMD x groups per wave slot
+        int nb = std::min(8, 512 / vg) * 4 / (int)waves_per_wg;  // waves per CU / waves per group
+        if (nb < 1) nb = 1;
         if (L.lds_bytes) nb = std::min<int>(nb, (int)((160u * 1024u) / L.lds_bytes));
         if (nb < 1) nb = 1;
+        if (tabs[k]->tree[s->variant]) {
+            // the LDS the resident groups leave free, split among them: the treelet of each group
+            const size_t per = std::min<size_t>((160u * 1024u) / nb, (size_t)prop.sharedMemPerBlock);
+            uint32_t cap = per > L.lds_bytes ? (uint32_t)((per - L.lds_bytes) / 64u) : 0u;
+#ifdef MRT_EXPERIMENTS
+            if (const char* e = getenv("MRT_TREELET_NODES"))  // sweep hook
+                if (*e) cap = std::min<uint32_t>(cap, (uint32_t)atoi(e));
+#endif
+            L.tree_n = std::min(cap, (uint32_t)bwide.size());
+            L.lds_bytes += (size_t)L.tree_n * 64u;
+        }
         L.vgprs = (uint32_t)fa.numRegs;
 #ifdef MRT_EXPERIMENTS
         if (const char* e = getenv("MRT_BLOCKS_PER_CU"))  // experiment hook
             if (*e) nb = std::max(1, atoi(e));
 #endif
         L.grid = prop.multiProcessorCount * nb;
-        s->max_grid = std::max(s->max_grid, L.grid);
+        s->max_threads = std::max(s->max_threads, (size_t)L.grid * L.wg);
     }
     *out = s;
     return MRT_OK;
@@ -789,7 +839,7 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
     if (d->flags & MRT_RF_PATH_DEBUG)
         if ((st = grow(s, (void**)&s->d_path_rays, &s->pr_cap, paths * 4))) return st;
     s->lev_rows = std::max<uint32_t>(d->max_bounces, 1);
-    if ((st = grow(s, (void**)&s->d_lev, &s->lev_cap, (size_t)s->lev_rows * s->max_grid * MRT_PATH_WG * 16))) return st;
+    if ((st = grow(s, (void**)&s->d_lev, &s->lev_cap, (size_t)s->lev_rows * s->max_threads * 16))) return st;
     uint32_t launches = (ns + s->chunk - 1) / s->chunk;
     if ((st = grow(s, (void**)&s->d_counters, &s->cnt_cap, (size_t)launches * 8))) return st;
     if (!s->pstream) HIPCHK(hipStreamCreateWithFlags(&s->pstream, hipStreamNonBlocking));
@@ -851,6 +901,8 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.lds_rays = s->lds_rays;
         P.lds_mesh = s->lds_mesh;
         P.lds_save = s->lds_save;
+        P.tree_src = reinterpret_cast<const float4*>(s->S.bwide);
+        P.tree_n = PL.tree_n;
         P.pixels = s->d_pixels;
         P.sdist = s->d_sdist;
         P.npix = s->npix;
@@ -864,8 +916,8 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.ns = ns;
         P.s0 = s0;
         P.n_paths = s->npix * (s1 - s0);
-        P.tail_zone = (uint32_t)std::min<uint64_t>((uint64_t)PL.grid * kWavesPerWG * 2 * MRT_BATCH, P.n_paths);  // ~2 big claims per wave
-        P.static_first = (uint64_t)P.n_paths < (uint64_t)PL.grid * kWavesPerWG * MRT_BATCH * 64u;
+        P.tail_zone = (uint32_t)std::min<uint64_t>((uint64_t)PL.grid * (PL.wg / 64u) * 2 * MRT_BATCH, P.n_paths);  // ~2 big claims per wave
+        P.static_first = (uint64_t)P.n_paths < (uint64_t)PL.grid * (PL.wg / 64u) * MRT_BATCH * 64u;
         P.seed = d->seed;
         P.max_bounces = d->max_bounces;
         P.rad = s->d_rad;
@@ -877,7 +929,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.lev = s->d_lev;
         P.lev_rows = s->lev_rows;
         HIPCHK(hipEventRecord(s->ev[2 * s->n_launch], q));
-        hipLaunchKernelGGL(PL.fn, dim3(PL.grid), dim3(MRT_PATH_WG), PL.lds_bytes, q, P);
+        hipLaunchKernelGGL(PL.fn, dim3(PL.grid), dim3(PL.wg), PL.lds_bytes, q, P);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(s->ev[2 * s->n_launch + 1], q));
         s->n_launch++;
@@ -981,6 +1033,8 @@ extern "C" mrt_status mrt_scene_kernel_info(const mrt_scene* s, mrt_kernel_info*
     out->grid = (uint32_t)L.grid;
     out->prog_ops = s->prog_ops;
     out->vgprs = L.vgprs;
+    out->wg = L.wg;
+    out->tree_nodes = L.tree_n;
     return MRT_OK;
 }
 

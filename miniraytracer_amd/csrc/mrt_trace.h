@@ -76,6 +76,23 @@ __device__ __forceinline__ WideNode load_wide(const W* p) {
     return n;
 }
 
+// The same from any address space: with a treelet (MRT_TREELET) the top wide nodes of the scene's
+// BVHs are copied into the workgroup's LDS at kernel start, and a node ref below the treelet size
+// reads there -- one flat load per 16 B that the hardware routes to LDS or memory per lane.
+__device__ __forceinline__ WideNode load_wide_q(const float4* q) {
+    const float4 a = q[0], b = q[1], c = q[2], d = q[3];
+    WideNode n;
+    n.lmin = f3{a.x, a.y, a.z};
+    n.lref = __float_as_uint(a.w);
+    n.lmax = f3{b.x, b.y, b.z};
+    n.rref = __float_as_uint(b.w);
+    n.rmin = f3{c.x, c.y, c.z};
+    n.order = __float_as_uint(c.w);
+    n.rmax = f3{d.x, d.y, d.z};
+    n.flags = __float_as_uint(d.w);
+    return n;
+}
+
 // a node record read through the constant address space (scalar loads at a uniform address)
 __device__ __forceinline__ mrt_node ld_node(const MRT_CONST_AS mrt_node* p) {
     mrt_node n;
@@ -158,7 +175,40 @@ struct LStack {
     uint32_t* mesh;    // 1 word per slot
     float* save;       // 9 words: query ray parked by the linear program (mrt_lin.h)
     uint32_t lane;
+    const float4* tree;  // the workgroup's LDS copy of BvhWide nodes [0, tree_b) (TreeOf<F>::on kernels)
+    uint32_t tree_b;
 };
+
+// Hot BVH nodes in LDS (north star): kernels of the bvh_node scenes run one 16-wave workgroup
+// per CU, and that group keeps the top levels of the scene's bvh_node subtrees (breadth-first
+// wide-node numbering: the first tree_b nodes) in the LDS its waves' stacks leave free.  Measured
+// on MI355X (DESIGN.md "Hot nodes in LDS"): random spheres +14%, book2 +3.6%; for the pod_bvh
+// kernels (7 waves per SIMD, no LDS to spare at one-wave groups) bigger groups cost more than the
+// treelet gained, so they keep one-wave groups and no treelet.
+#ifndef MRT_TREELET
+#define MRT_TREELET 1
+#endif
+#ifndef MRT_TREE_WG
+#define MRT_TREE_WG 1024
+#endif
+template <uint32_t F>
+struct TreeOf {
+    // the kernels of bvh_node scenes (wide-node walks); the same test as PathOcc::kWide
+    static constexpr bool on = MRT_TREELET && (F & FT_BVHW) != 0 &&
+                               ((F & (FT_BVHW | FT_TEX | FT_VOLUME)) != 0 || !(F & FT_LIN));
+    static constexpr uint32_t wg = on ? MRT_TREE_WG : 64u;  // threads per path-kernel workgroup
+};
+// wide node `ref` of a BvhWide / MeshWide array: from the LDS treelet when it holds it
+template <bool TREE, typename W>
+__device__ __forceinline__ WideNode wide_at(const W* base, uint32_t ref, const LStack& L) {
+    if constexpr (TREE) {
+        const float4* q = ref < L.tree_b ? L.tree + (size_t)ref * 4 : reinterpret_cast<const float4*>(base + ref);
+        return load_wide_q(q);
+    } else {
+        (void)L;
+        return load_wide(base + ref);
+    }
+}
 
 template <uint32_t F>
 __device__ __forceinline__ bool is_prim(uint32_t kind) {
@@ -332,7 +382,7 @@ __device__ __forceinline__ bool mesh_hit(const DScene& S, const mrt_node& n, con
     // on the teapot (C3) than the one-step-per-iteration walk below, so kept as an experiment.
     for (;;) {
         while (!(ref & MESH_LEAF)) {
-            const WideNode W = load_wide(S.mwide + ref);
+            const WideNode W = wide_at<false>(S.mwide, ref, L);
             const bool hl = aabb_hit(W.lmin, W.lmax, r, tmin, tmax);
             const bool hr = aabb_hit(W.rmin, W.rmax, r, tmin, tmax);
             const bool left_first = (W.order & r.mask) != 0;
@@ -357,7 +407,7 @@ __device__ __forceinline__ bool mesh_hit(const DScene& S, const mrt_node& n, con
         if (ref & MESH_LEAF) {
             if (mesh_leaf(S, ref, n, r, tmin, tmax, rec, full)) return true;
         } else {
-            const WideNode W = load_wide(S.mwide + ref);
+            const WideNode W = wide_at<false>(S.mwide, ref, L);
             const bool hl = aabb_hit(W.lmin, W.lmax, r, tmin, tmax);
             const bool hr = aabb_hit(W.rmin, W.rmax, r, tmin, tmax);
             const bool left_first = (W.order & r.mask) != 0;
@@ -414,7 +464,7 @@ __device__ __forceinline__ uint32_t mesh_step(const DScene& S, const mrt_node& n
             return 1u;
         }
     } else {
-        const WideNode W = load_wide(S.mwide + ref);
+        const WideNode W = wide_at<false>(S.mwide, ref, L);
         const bool hl = aabb_hit(W.lmin, W.lmax, r, tmin, tt);
         const bool hr = aabb_hit(W.rmin, W.rmax, r, tmin, tt);
         const bool left_first = (W.order & r.mask) != 0;
@@ -492,7 +542,7 @@ __device__ __forceinline__ bool bvhw_hit(const DScene& S, const mrt_node& n, con
     // visits the same nodes in the same order as the reference's recursion: results unchanged.
     for (;;) {
         while (!(ref & BVHW_LEAF)) {
-            const WideNode W = load_wide(S.bwide + ref);
+            const WideNode W = wide_at<TreeOf<F>::on>(S.bwide, ref, L);
             const bool hl = !(W.flags & 1u) || aabb_hit(W.lmin, W.lmax, r, tmin, tmax);
             const bool hr = !(W.flags & 2u) || aabb_hit(W.rmin, W.rmax, r, tmin, tmax);
             const bool left_first = (W.order & r.mask) != 0;
@@ -517,7 +567,7 @@ __device__ __forceinline__ bool bvhw_hit(const DScene& S, const mrt_node& n, con
         if (ref & BVHW_LEAF) {
             if (bvhw_leaf<F>(S, ref, r, tmin, tmax, rec, full)) return true;
         } else {
-            const WideNode W = load_wide(S.bwide + ref);
+            const WideNode W = wide_at<TreeOf<F>::on>(S.bwide, ref, L);
             const bool hl = !(W.flags & 1u) || aabb_hit(W.lmin, W.lmax, r, tmin, tmax);
             const bool hr = !(W.flags & 2u) || aabb_hit(W.rmin, W.rmax, r, tmin, tmax);
             const bool left_first = (W.order & r.mask) != 0;

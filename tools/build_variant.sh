@@ -18,6 +18,11 @@ if [ -n "${EXACT_FLAGS:-}" ]; then
   /opt/rocm/bin/hipcc $BASE -ffp-contract=off -DMRT_FAST=0 $EXACT_FLAGS -c miniraytracer_amd/csrc/mrt_kernels.hip -o exp/obj_$tag/mrt_kernels_exact.o
   EX=exp/obj_$tag/mrt_kernels_exact.o
 fi
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC build/obj/mrt_render.o $EX exp/obj_$tag/mrt_kernels_fast.o \
+RO=build/obj/mrt_render.o
+if [ -n "${HOST_FLAGS:-}" ]; then  # host TU too (e.g. -DMRT_PATH_WG=..., which both sides must agree on)
+  /opt/rocm/bin/hipcc $BASE -ffp-contract=off $HOST_FLAGS -c miniraytracer_amd/csrc/mrt_render.hip -o exp/obj_$tag/mrt_render.o
+  RO=exp/obj_$tag/mrt_render.o
+fi
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $RO $EX exp/obj_$tag/mrt_kernels_fast.o \
     build/obj/scene_builder.o build/obj/mrt_common.o -ldl -o exp/libmrt_$tag.so
 echo "built exp/libmrt_$tag.so"

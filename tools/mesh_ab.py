@@ -30,7 +30,9 @@ for c in CASES.split():
         out[f"s{sid}_{num}_grays"] = round(rays / min(ms) / 1e6, 3)
         out[f"s{sid}_{num}_rays"] = int(rays)
         out[f"s{sid}_{num}_sum"] = float(img[..., :3].astype(np.float64).sum())
-    out[f"s{sid}_vgprs"] = r.kernel_info()["vgprs"]
+    ki = r.kernel_info()
+    out[f"s{sid}_vgprs"] = ki["vgprs"]
+    out[f"s{sid}_tree"] = f"wg{ki['wg']}:t{ki['tree_nodes']}:lds{ki['lds_bytes']}:g{ki['grid']}"
 print(json.dumps(out))
 '''
 
