@@ -54,6 +54,14 @@
 #ifndef MRT_FAST_SNAP
 #define MRT_FAST_SNAP MRT_FAST
 #endif
+// The recursion's return path (L = emitted + a*L/pdf, main.cpp:84-104) evaluated FORWARD: a
+// running throughput T = (T*a)/pdf per bounce, L = T*emitted at the path's end, instead of storing
+// every bounce's (a, pdf) and folding them deepest-first.  Same factors, another association (a
+// rounding difference per bounce), so tolerance contract only; it needs no per-bounce level
+// storage (LDS / HBM) and no fold loop.
+#ifndef MRT_FWD_FOLD
+#define MRT_FWD_FOLD MRT_FAST
+#endif
 
 namespace mrtd {
 

@@ -43,7 +43,7 @@ using namespace mrtd;
 #define MRT_WPE_WIDE 4
 #endif
 #ifndef MRT_WPE_LIN
-#define MRT_WPE_LIN 6
+#define MRT_WPE_LIN (MRT_FWD_FOLD ? 7 : 6)  // forward fold: no LDS levels, 72 VGPRs (C2 +1%)
 #endif
 #ifndef MRT_WPE_MESH
 #define MRT_WPE_MESH 7
@@ -89,7 +89,8 @@ extern "C" int mrt_debug_phases(unsigned long long* out, int reset) {
 #define MRT_LEVK_MESH 0u
 #endif
 template <uint32_t F> struct PathLevLds {
-    static constexpr uint32_t K = ((F & 0xFFFFu) == (FT_LIN | FT_INST)) ? MRT_LEVK_CORNELL
+    static constexpr uint32_t K = MRT_FWD_FOLD ? 0u  // no stored levels
+                                  : ((F & 0xFFFFu) == (FT_LIN | FT_INST)) ? MRT_LEVK_CORNELL
                                   : PathOcc<F>::kWide                  ? MRT_LEVK_WIDE
                                   : ((F & FT_MESH) != 0)               ? MRT_LEVK_MESH
                                                                        : 0u;
@@ -193,6 +194,9 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                 start(u, v);
                 ps.depth = 0;
                 ps.nlev = 0;
+#if MRT_FWD_FOLD
+                ps.T = f3{1.0f, 1.0f, 1.0f};
+#endif
                 ps.rays = 0;
                 active = true;
             }
@@ -209,7 +213,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
     };
     // a finished path: the recursion's fold, radiance out (sample-major, coalesced), rays counted
     auto finish_path = [&](f3 L) {
-        L = fold_levels(lev, ps.nlev, L);
+        L = end_path(ps, lev, L);
         PH_MARK(ph, 5);
         float* dst = P.rad + (size_t)idx * 3;
         dst[0] = L.x;

@@ -190,6 +190,9 @@ struct PathState {
     uint32_t depth;  // bounces so far (trace depth)
     uint32_t nlev;   // stored fold levels | LEV_LOUD once a level could turn a black result non-zero
     uint32_t rays;   // trace() calls of this path
+#if MRT_FWD_FOLD
+    f3 T;            // throughput of the bounces so far (forward fold)
+#endif
 };
 static constexpr uint32_t LEV_LOUD = 0x80000000u;
 
@@ -240,6 +243,20 @@ __device__ __forceinline__ bool quiet_level(float4 v) {
     const bool fin = isfinite(v.x) && isfinite(v.y) && isfinite(v.z);
     if (v.w < 0.0f) return fin & (((__float_as_uint(v.x) | __float_as_uint(v.y) | __float_as_uint(v.z)) >> 31) == 0);
     return fin & (v.w > 0.0f) & isfinite(v.w);
+}
+
+// One bounce's level (a, pdf; pdf < 0: metal, L = a*L): stored for the deepest-first fold, or
+// (forward fold) multiplied into the path's throughput.
+template <uint32_t LK>
+__device__ __forceinline__ void push_level(PathState& ps, const LevStore<LK>& lev, float4 lv) {
+#if MRT_FWD_FOLD
+    (void)lev;
+    if (lv.w < 0.0f) ps.T = f3{ps.T.x * lv.x, ps.T.y * lv.y, ps.T.z * lv.z};
+    else ps.T = f3{(ps.T.x * lv.x) / lv.w, (ps.T.y * lv.y) / lv.w, (ps.T.z * lv.z) / lv.w};
+#else
+    lev.put(ps.nlev & ~LEV_LOUD, lv);
+    ps.nlev = (ps.nlev + 1) | (quiet_level(lv) ? 0u : LEV_LOUD);
+#endif
 }
 
 // camera::get_ray (camera.h:38-44)
@@ -306,8 +323,7 @@ __device__ __forceinline__ bool shade_hit(const DScene& S, PathState& ps, uint32
         f3 nd = add(reflected, fmul(1 - M.p, rs));
         f3 att = mat_color<F>(S, M, rec);
         const float4 lv = make_float4(att.x, att.y, att.z, -1.0f);
-        lev.put(ps.nlev & ~LEV_LOUD, lv);
-        ps.nlev = (ps.nlev + 1) | (quiet_level(lv) ? 0u : LEV_LOUD);
+        push_level(ps, lev, lv);
         r = make_ray(rec.p, nd, r.time, 0);
         return false;
     }
@@ -377,8 +393,7 @@ __device__ __forceinline__ bool shade_hit(const DScene& S, PathState& ps, uint32
     }
     const float pdf_v = S.biased != MRT_NONE ? 0.5f * (biased_pdf_value<F>(S, rec.p, sc.d, r.time) + sval) : sval;
     const float4 lv = make_float4(att.x * spdf, att.y * spdf, att.z * spdf, pdf_v);
-    lev.put(ps.nlev & ~LEV_LOUD, lv);
-    ps.nlev = (ps.nlev + 1) | (quiet_level(lv) ? 0u : LEV_LOUD);
+    push_level(ps, lev, lv);
     r = sc;
     return false;
 }
@@ -451,8 +466,7 @@ __device__ __forceinline__ bool trace_split(const DScene& S, PathState& ps, uint
         pr->dir = add(reflected, fmul(1 - M.p, rs));
         f3 att = mat_color<F>(S, M, rec);
         const float4 lv = make_float4(att.x, att.y, att.z, -1.0f);
-        lev.put(ps.nlev & ~LEV_LOUD, lv);
-        ps.nlev = (ps.nlev + 1) | (quiet_level(lv) ? 0u : LEV_LOUD);
+        push_level(ps, lev, lv);
         return false;
     }
     if (M.kind == MRT_M_DIELECTRIC) {  // dielectric::scatter (material.h:121-175)
@@ -526,8 +540,7 @@ __device__ __forceinline__ void finish_scatter(const DScene& S, PathState& ps, c
     }
     const float pdf_v = S.biased != MRT_NONE ? 0.5f * (biased_pdf_value<F>(S, sc.o, sc.d, sc.time) + sval) : sval;
     const float4 lv = make_float4(pr.att.x * spdf, pr.att.y * spdf, pr.att.z * spdf, pdf_v);
-    lev.put(ps.nlev & ~LEV_LOUD, lv);
-    ps.nlev = (ps.nlev + 1) | (quiet_level(lv) ? 0u : LEV_LOUD);
+    push_level(ps, lev, lv);
 }
 
 // the recursion's return path, deepest level first; the lane's levels are contiguous, so they
@@ -558,6 +571,16 @@ __device__ __forceinline__ f3 fold_levels(const LevStore<LK>& lev, uint32_t nlev
 #endif
     for (; d >= 0; d--) L = fold_level(lev.get((uint32_t)d), L);
     return L;
+}
+// a path's radiance from its end's emitted (or sky / black) L
+template <uint32_t LK>
+__device__ __forceinline__ f3 end_path(const PathState& ps, const LevStore<LK>& lev, f3 L) {
+#if MRT_FWD_FOLD
+    (void)lev;
+    return f3{ps.T.x * L.x, ps.T.y * L.y, ps.T.z * L.z};
+#else
+    return fold_levels(lev, ps.nlev, L);
+#endif
 }
 
 }  // namespace mrtd
