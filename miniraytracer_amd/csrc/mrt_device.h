@@ -321,6 +321,40 @@ __device__ __forceinline__ Ray make_ray(f3 o, f3 dir, float time, int inside) {
     r.inv = ray_inv(r.d, r.nice);
     return r;
 }
+// A ray whose direction argument is already of unit length up to rounding (a ray's normalized
+// direction, rotated or reused): the exact contract runs the constructor as the reference does;
+// the tolerance contract skips the renormalization (a change of at most an ulp or two).
+#ifndef MRT_FAST_UNIT
+#define MRT_FAST_UNIT MRT_FAST
+#endif
+__device__ __forceinline__ Ray make_ray_unit(f3 o, f3 dir, float time, int inside) {
+#if MRT_FAST_UNIT
+    Ray r;
+    r.o = o;
+    r.d = dir;
+    r.time = time;
+    r.inside = inside;
+    uint32_t X = __float_as_uint(dir.x) >> 31, Y = __float_as_uint(dir.y) >> 31, Z = __float_as_uint(dir.z) >> 31;
+    r.mask = 1u << (Z | (Y << 1) | (X << 2));
+    r.nice = ray_nice(r.o, r.d);
+    r.inv = ray_inv(r.d, r.nice);
+    return r;
+#else
+    return make_ray(o, dir, time, inside);
+#endif
+}
+// translate::hit's moved ray (scene_object.cpp:11): the same direction, a new origin
+__device__ __forceinline__ Ray moved_ray(const Ray& r0, f3 o) {
+#if MRT_FAST_UNIT
+    Ray r = r0;  // direction, its reciprocal and mask reused as they are
+    r.o = o;
+    r.inside = 0;
+    r.nice = ray_nice(r.o, r.d);
+    return r;
+#else
+    return make_ray(o, r0.d, r0.time, 0);
+#endif
+}
 __device__ __forceinline__ f3 eval(const Ray& r, float t) { return add(r.o, fmul(t, r.d)); }
 
 // aabb::hit, active SSE branch (aabb.h:49-76)

@@ -52,7 +52,7 @@ template <uint32_t F> struct PathOcc {
     static constexpr bool kWide = (F & (FT_BVHW | FT_TEX | FT_VOLUME)) != 0 || !(F & FT_LIN);
     static constexpr int W = kWide ? MRT_WPE_WIDE : ((F & FT_MESH) != 0 ? MRT_WPE_MESH : MRT_WPE_LIN);
 };
-#if defined(MRT_EXPERIMENTS) && defined(MRT_PHASES) && !MRT_FAST
+#if defined(MRT_EXPERIMENTS) && defined(MRT_PHASES)  // build ONE of the two TUs with it
 __device__ unsigned long long g_phases[12];
 extern "C" int mrt_debug_phases(unsigned long long* out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phases), sizeof(g_phases)) != hipSuccess) return 1;
@@ -216,9 +216,15 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
         L = end_path(ps, lev, L);
         PH_MARK(ph, 5);
         float* dst = P.rad + (size_t)idx * 3;
+#if defined(MRT_EXPERIMENTS) && defined(MRT_EXP_NOSTORE)  // experiment: what the radiance store costs
+        if (__float_as_uint(L.x) == 0x7fc00123u) {
+#endif
         dst[0] = L.x;
         dst[1] = L.y;
         dst[2] = L.z;
+#if defined(MRT_EXPERIMENTS) && defined(MRT_EXP_NOSTORE)
+        }
+#endif
         if (P.path_rays) P.path_rays[idx] = ps.rays;
         done_rays += ps.rays;
         active = false;

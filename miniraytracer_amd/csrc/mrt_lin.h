@@ -351,7 +351,7 @@ __device__ __forceinline__ bool scene_hit_lin(const DScene& S, Ray& r, float tmi
             bool in = on;
             const Ray r0 = lin_load_ray(L);
             if (kind == MRT_K_TRROTY) {  // translate::hit then rotate_y::hit (scene_object.cpp:9-18, 70-98)
-                cur = make_ray(sub(r0.o, f3{o.f[8], o.f[9], o.f[10]}), r0.d, r0.time, 0);
+                cur = moved_ray(r0, sub(r0.o, f3{o.f[8], o.f[9], o.f[10]}));
                 if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, cur, tmin, closest);
             } else if (kind == MRT_K_ROTY) {
                 cur = r0;
@@ -365,7 +365,7 @@ __device__ __forceinline__ bool scene_hit_lin(const DScene& S, Ray& r, float tmi
                 continue;
             }
             if (kind == MRT_K_TRROTY || kind == MRT_K_ROTY) cur = rotate_ray(cur, o.f[6], o.f[7]);
-            else cur = make_ray(sub(r0.o, f3{o.f[0], o.f[1], o.f[2]}), r0.d, r0.time, 0);
+            else cur = moved_ray(r0, sub(r0.o, f3{o.f[0], o.f[1], o.f[2]}));
         } else if (INST && op == LOP_INST_END) {
             if (hinst == inst) {  // keep the instance-frame ray of the hit for the record
                 float* b = L.save + L.lane + 9 * 64;

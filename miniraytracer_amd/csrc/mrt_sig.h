@@ -118,7 +118,7 @@ struct SigWalk {
                 const Ray r0 = lin_load_ray(L);
                 bool in = on;
                 if constexpr (kind == MRT_K_TRROTY) {
-                    w.cur = make_ray(sub(r0.o, f3{o.f[8], o.f[9], o.f[10]}), r0.d, r0.time, 0);
+                    w.cur = moved_ray(r0, sub(r0.o, f3{o.f[8], o.f[9], o.f[10]}));
                     if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, w.cur, tmin, w.closest);
                 } else if constexpr (kind == MRT_K_ROTY) {
                     w.cur = r0;
@@ -126,7 +126,7 @@ struct SigWalk {
                 }
                 if (__any(in)) {
                     if constexpr (kind == MRT_K_TRROTY || kind == MRT_K_ROTY) w.cur = rotate_ray(w.cur, o.f[6], o.f[7]);
-                    else w.cur = make_ray(sub(r0.o, f3{o.f[0], o.f[1], o.f[2]}), r0.d, r0.time, 0);
+                    else w.cur = moved_ray(r0, sub(r0.o, f3{o.f[0], o.f[1], o.f[2]}));
                     run<PC + 1, skip>(S, prog, tmin, w, in, rec, L);
                     if (w.hinst == PC) {  // keep the instance-frame ray of the hit for the record
                         float* b = L.save + L.lane + 9 * 64;

@@ -631,7 +631,7 @@ __device__ __forceinline__ Ray rotate_ray(const Ray& ray, float s, float c) {
     o.z = c * ray.o.z + s * ray.o.x;
     d.x = c * ray.d.x - s * ray.d.z;
     d.z = c * ray.d.z + s * ray.d.x;
-    return make_ray(o, d, ray.time, 0);
+    return make_ray_unit(o, d, ray.time, 0);
 }
 // ... and the record back (scene_object.cpp:85-93)
 __device__ __forceinline__ void unrotate_rec(HitRec& rec, float s, float c) {
@@ -715,7 +715,7 @@ __device__ __forceinline__ bool scene_hit(const DScene& S, Ray ray, float tmin0,
         } else if ((F & FT_INST) && kind == MRT_K_TRROTY) {  // translate(rotate_y(x)) fused
             const float s = N.f[6], c = N.f[7];
             if (st == ST_ENTER) {
-                Ray moved = make_ray(sub(ray.o, ld3(N.f + 8)), ray.d, ray.time, 0);  // translate::hit
+                Ray moved = moved_ray(ray, sub(ray.o, ld3(N.f + 8)));  // translate::hit
                 if ((MRT_NODE_FLAGS(N) & MRT_F_HASBOX) && !aabb_hit(N.f, N.f + 3, moved, tmin, closest)) {
                     ret = false;
                     pop = true;
@@ -741,7 +741,7 @@ __device__ __forceinline__ bool scene_hit(const DScene& S, Ray ray, float tmin0,
                     pop = true;
                 } else {
                     push_ray(L, rsp++, ray);
-                    ray = roty ? rotate_ray(ray, N.f[6], N.f[7]) : make_ray(sub(ray.o, ld3(N.f)), ray.d, ray.time, 0);
+                    ray = roty ? rotate_ray(ray, N.f[6], N.f[7]) : moved_ray(ray, sub(ray.o, ld3(N.f)));
                     req = N.a;
                     tstate = ST_PH1;
                 }
