@@ -16,7 +16,7 @@ HIPDEV   = -mllvm -disable-promote-alloca-to-vector -mllvm -structurizecfg-skip-
 CSRC     = miniraytracer_amd/csrc
 OBJDIR   = build/obj
 
-LIB_OBJS = $(OBJDIR)/mrt_render.o $(OBJDIR)/mrt_kernels_exact.o $(OBJDIR)/mrt_kernels_fast.o $(OBJDIR)/scene_builder.o $(OBJDIR)/mrt_common.o
+LIB_OBJS = $(OBJDIR)/mrt_render.o $(OBJDIR)/mrt_kernels_exact.o $(OBJDIR)/mrt_kernels_fast.o $(OBJDIR)/mrt_cpu.o $(OBJDIR)/scene_builder.o $(OBJDIR)/mrt_common.o
 # the path kernels twice: exact contract (no contraction, IEEE division) and tolerance contract
 # (FMA contraction, reciprocal division, hardware rcp/sqrt/rsq, f32 transcendentals)
 FASTFLAGS = -DMRT_FAST=1 -ffp-contract=fast -freciprocal-math
@@ -31,6 +31,11 @@ $(OBJDIR)/mrt_kernels_exact.o: $(CSRC)/mrt_kernels.hip $(HDRS)
 $(OBJDIR)/mrt_kernels_fast.o: $(CSRC)/mrt_kernels.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(HIPDEV) $(FASTFLAGS) -c $< -o $@
+
+# the CPU backend: the same hot-path headers compiled for the host only (exact contract)
+$(OBJDIR)/mrt_cpu.o: $(CSRC)/mrt_cpu.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) --offload-host-only -c $< -o $@
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)

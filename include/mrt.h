@@ -53,6 +53,7 @@ typedef struct mrt_params {
     uint64_t seed;            /* path stream-key seed, default = the reference main seed */
     uint32_t gpus;            /* -gpus: GPUs to shard the work_queue tiles over (0 = every visible GPU) */
     uint32_t numerics;        /* -numerics: 0 exact contract, 1 tolerance contract (MRT_RF_FAST) */
+    uint32_t backend;         /* -backend: 0 GPU (default), 1 CPU (MRT_DEVICE_CPU, -threads workers, exact) */
 } mrt_params;
 
 void mrt_default_params(mrt_params* p);
@@ -82,6 +83,11 @@ mrt_status mrt_worker_seeds(const mrt_scene_blob* blob, uint32_t n_threads, uint
 /* ---- device -------------------------------------------------------------------------------- */
 mrt_status mrt_init(int* device_count);
 typedef struct mrt_scene mrt_scene;
+/* device: a HIP device index, or MRT_DEVICE_CPU for the CPU backend -- the same hot-path source
+ * compiled for the host (exact numerics contract; worker threads over the work_queue tiles like
+ * draw()/draw2(), main.cpp:347-382).  It is only ever chosen explicitly: with no gfx950 device the
+ * GPU entry points fail (MRT_ERR_NO_DEVICE), they never fall back to the CPU. */
+#define MRT_DEVICE_CPU (-1)
 mrt_status mrt_scene_upload(int device, const mrt_scene_view* view, mrt_scene** out);
 void mrt_scene_free(mrt_scene* scene);
 
@@ -96,6 +102,7 @@ typedef struct mrt_render_desc {
     uint32_t rank, world;    /* this call renders tiles k (inverted-Hilbert order) with k % world == rank */
     uint32_t chunk_samples;  /* samples per launch (0 = auto, bounded by HBM budget) */
     uint32_t flags;          /* MRT_RF_* */
+    uint32_t threads;        /* CPU backend: worker threads (0 = every core); the GPU backend ignores it */
 } mrt_render_desc;
 #define MRT_RF_PATH_DEBUG 0x1u /* also keep per-path radiance + ray counts (mrt_render_debug) */
 #define MRT_RF_FAST 0x2u       /* tolerance numerics contract: FMA contraction, hardware rcp/sqrt/rsq,
@@ -109,10 +116,12 @@ void mrt_default_render_desc(const mrt_params* p, mrt_render_desc* d);
  * G_linearBackBuffer main.cpp:58) in the order mrt_render_device writes them. */
 mrt_status mrt_local_pixels(const mrt_render_desc* d, uint32_t* n_out, uint32_t* pixels_out /* may be NULL */);
 
-/* Render into a host W*H*4 float buffer (x,y,z,0 per pixel; only owned pixels are written). */
+/* Render into a host W*H*4 float buffer (x,y,z,0 per pixel; only owned pixels are written).
+ * Both backends; on the CPU backend the call returns when the render is done (cancel is polled
+ * per tile, as G_isRunning at main.cpp:180). */
 mrt_status mrt_render(mrt_scene* s, const mrt_render_desc* d, float* rgb_out, uint64_t* rays_out,
                       const volatile int* cancel);
-/* Render into device memory: d_local = n_local*4 floats in mrt_local_pixels order.  Enqueued on
+/* GPU backend only.  Render into device memory: d_local = n_local*4 floats in mrt_local_pixels order.  Enqueued on
  * `stream` (hipStream_t or NULL); rays are accumulated into the device uint64 *d_rays; nothing is
  * synchronised and nothing is allocated when the scene's workspace already fits (capturable). */
 mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, float* d_local, uint64_t* d_rays, void* stream);

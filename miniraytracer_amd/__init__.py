@@ -90,7 +90,7 @@ NUMERICS = ("exact", "fast")
 
 
 def render_desc(width, height, samples, depth=32, max_luminance=1000.0, mode=0, seed=MAIN_SEED, tile_size=32,
-                rank=0, world=1, chunk_samples=0, flags=0, numerics="exact"):
+                rank=0, world=1, chunk_samples=0, flags=0, numerics="exact", threads=0):
     """Render description; `samples` is floored to a perfect square like main.cpp:319-320.
     numerics: "exact" (bit-for-bit the reference built exact) or "fast" (tolerance contract:
     per-pixel RMSE < 1e-3 vs the reference as shipped; MRT_RF_FAST)."""
@@ -100,7 +100,7 @@ def render_desc(width, height, samples, depth=32, max_luminance=1000.0, mode=0, 
         flags |= _lib.RF_FAST
     sq = int(np.sqrt(np.float32(samples)))
     return MrtRenderDesc(width, height, sq, depth, max_luminance, mode, seed, tile_size, rank, world,
-                         chunk_samples, flags)
+                         chunk_samples, flags, threads)
 
 
 def local_pixels(desc):
@@ -118,11 +118,18 @@ def device_count():
 
 
 class Renderer:
-    """A scene resident in HBM of one device."""
+    """A scene resident in HBM of one device -- or, with device="cpu" (MRT_DEVICE_CPU), held by the
+    CPU backend: the same hot-path code compiled for the host, exact numerics contract, worker
+    threads over the work_queue tiles (render_desc(threads=...)).  Only an explicit "cpu" selects
+    it; without a gfx950 device a GPU Renderer raises."""
 
     def __init__(self, scene, device=0):
-        n = C.c_int()
-        check(lib().mrt_init(C.byref(n)), "mrt_init")
+        if device == "cpu":
+            device = _lib.DEVICE_CPU
+        else:
+            n = C.c_int()
+            check(lib().mrt_init(C.byref(n)), "mrt_init")
+        self.device = device
         self._h = C.c_void_p()
         check(lib().mrt_scene_upload(device, C.byref(scene.view), C.byref(self._h)), "mrt_scene_upload")
         self.scene = scene

@@ -16,6 +16,7 @@ if os.environ.get("MRT_EXPERIMENT_LIB"):
 MRT_NONE = 0xFFFFFFFF
 RF_PATH_DEBUG = 0x1
 RF_FAST = 0x2  # tolerance numerics contract (include/mrt.h MRT_RF_FAST)
+DEVICE_CPU = -1  # mrt_scene_upload device of the CPU backend (include/mrt.h MRT_DEVICE_CPU)
 
 
 class MrtParams(C.Structure):
@@ -26,14 +27,15 @@ class MrtParams(C.Structure):
                 ("num_threads", C.c_uint32), ("max_bounces", C.c_uint32),
                 ("scene_select", C.c_uint32), ("threading_mode", C.c_uint32),
                 ("max_luminance", C.c_float), ("delay", C.c_uint32), ("seed", C.c_uint64),
-                ("gpus", C.c_uint32), ("numerics", C.c_uint32)]
+                ("gpus", C.c_uint32), ("numerics", C.c_uint32), ("backend", C.c_uint32)]
 
 
 class MrtRenderDesc(C.Structure):
     _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("sqrt_samples", C.c_uint32),
                 ("max_bounces", C.c_uint32), ("max_luminance", C.c_float), ("mode", C.c_uint32),
                 ("seed", C.c_uint64), ("tile_size", C.c_uint32), ("rank", C.c_uint32),
-                ("world", C.c_uint32), ("chunk_samples", C.c_uint32), ("flags", C.c_uint32)]
+                ("world", C.c_uint32), ("chunk_samples", C.c_uint32), ("flags", C.c_uint32),
+                ("threads", C.c_uint32)]
 
 
 class MrtCamera(C.Structure):

@@ -4,8 +4,9 @@
 // and writes the image (-o out.pfm: linear; -o out.ppm: Drago tone map, main.cpp:416-444).
 //
 // -gpus N shards the work_queue tiles over N GPUs (one host thread per device, tile k -> GPU
-// k % N); 0 = every visible GPU.  -threads keeps the reference's meaning (CPU worker threads) and
-// has nothing to do on the GPU backend.  -numerics exact|fast picks the arithmetic contract.
+// k % N); 0 = every visible GPU.  -backend cpu renders on the host instead (the CPU backend: the
+// same hot-path code compiled for the host, exact contract), with -threads worker threads as the
+// reference's -threads (0 = every core).  -numerics exact|fast picks the GPU's arithmetic contract.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -36,22 +37,25 @@ int main(int argc, char** argv) {
     mrt_scene_view view;
     mrt_scene_blob_view(blob, &view);
 
-    int ndev = 0;
-    if ((st = mrt_init(&ndev))) return fail("mrt_init", st);
-    int world = p.gpus ? (int)p.gpus : ndev;
-    if (world > ndev) {
-        fprintf(stderr, "-gpus %u: only %d GPU(s) visible\n", p.gpus, ndev);
-        return 1;
+    const bool cpu = p.backend == 1;
+    int ndev = 0, world = 1;
+    if (!cpu) {
+        if ((st = mrt_init(&ndev))) return fail("mrt_init", st);
+        world = p.gpus ? (int)p.gpus : ndev;
+        if (world > ndev) {
+            fprintf(stderr, "-gpus %u: only %d GPU(s) visible\n", p.gpus, ndev);
+            return 1;
+        }
     }
 
     std::vector<mrt_scene*> scenes(world, nullptr);
     std::vector<mrt_render_desc> descs(world);
     for (int r = 0; r < world; r++) {
-        if ((st = mrt_scene_upload(r, &view, &scenes[r]))) return fail("scene_upload", st);
+        if ((st = mrt_scene_upload(cpu ? MRT_DEVICE_CPU : r, &view, &scenes[r]))) return fail("scene_upload", st);
         mrt_default_render_desc(&p, &descs[r]);
         descs[r].rank = (uint32_t)r;
         descs[r].world = (uint32_t)world;
-        if ((st = mrt_prepare(scenes[r], &descs[r]))) return fail("prepare", st);
+        if (!cpu && (st = mrt_prepare(scenes[r], &descs[r]))) return fail("prepare", st);
     }
     std::vector<float> img((size_t)p.buffer_width * p.buffer_height * 4, 0.0f);
     std::vector<uint64_t> rays(world, 0);
@@ -67,8 +71,16 @@ int main(int argc, char** argv) {
         if (sts[r]) return fail("render", sts[r]);
     uint64_t total = 0;
     for (uint64_t x : rays) total += x;
-    printf("MiniRayTracer - Scene: %.0fms - Trace: %.2fs - %.3f Mrays/s | %.3f us/ray  [%d x MI355X, %u spp, %s numerics]\n", gen_ms,
-           secs, (total * 0.000001) / secs, (secs * 1000000.0) / (double)total, world, descs[0].sqrt_samples * descs[0].sqrt_samples,
+    char where[64];
+    if (cpu) {
+        mrt_kernel_info ki{};
+        mrt_scene_kernel_info(scenes[0], &ki);
+        snprintf(where, sizeof where, "CPU, %u threads", ki.grid);
+    } else {
+        snprintf(where, sizeof where, "%d x MI355X", world);
+    }
+    printf("MiniRayTracer - Scene: %.0fms - Trace: %.2fs - %.3f Mrays/s | %.3f us/ray  [%s, %u spp, %s numerics]\n", gen_ms,
+           secs, (total * 0.000001) / secs, (secs * 1000000.0) / (double)total, where, descs[0].sqrt_samples * descs[0].sqrt_samples,
            p.numerics ? "fast" : "exact");
     printf("rays %llu\n", (unsigned long long)total);
 

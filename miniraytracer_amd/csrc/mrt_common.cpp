@@ -65,6 +65,7 @@ extern "C" void mrt_default_params(mrt_params* p) {
     p->seed = 11350390909718046443ull;  // main.cpp:302
     p->gpus = 0;
     p->numerics = 1;  // tolerance contract (DESIGN.md "Numerics contracts"); -numerics exact for bit-exact
+    p->backend = 0;
 }
 
 // ReadParameter (cmdline_parser.cpp:41-62): first occurrence wins, value range-checked, a bad
@@ -126,6 +127,8 @@ extern "C" mrt_status mrt_parse_argv(int argc, char** argv, mrt_params* out) {
                "  -depth    \t<value>\t\tMaximum bounce depth per primary ray\n"
                "  -maxlum   \t<value>\t\tClamp maximum luminance (introduces bias)\n"
                "  -threads  \t<value>\t\tNumber of CPU threads (0 selects all; CPU backend only)\n"
+               "  -backend  \t[gpu, cpu]\tRender on the MI355X(s) (default) or on the host CPU\n"
+               "            \t\t\t(the same hot-path code, exact numerics, -threads workers)\n"
                "  -gpus     \t<value>\t\tNumber of GPUs to shard tiles over (0 selects all)\n"
                "  -numerics \t[exact, fast]\tArithmetic contract (exact: bit-for-bit the reference built\n"
                "            \t\t\twithout contraction; fast: per-pixel RMSE < 1e-3, default)\n"
@@ -158,6 +161,13 @@ extern "C" mrt_status mrt_parse_argv(int argc, char** argv, mrt_params* out) {
         else if (!strcmp(v, "fast") || !strcmp(v, "1")) p.numerics = 1;
         else printf("Warning: Invalid value for parameter '-numerics', must be exact or fast.\n");
     }
+    if (int i = check_param(argc, argv, "-backend")) {
+        const char* v = i + 1 < argc ? argv[i + 1] : "";
+        if (!strcmp(v, "gpu")) p.backend = 0;
+        else if (!strcmp(v, "cpu")) p.backend = 1;
+        else printf("Warning: Invalid value for parameter '-backend', must be gpu or cpu.\n");
+    }
+    if (p.backend == 1) p.numerics = 0;  // the CPU backend runs the exact contract
     if (out) *out = p;
     return MRT_OK;
 }
@@ -175,6 +185,7 @@ extern "C" void mrt_default_render_desc(const mrt_params* p, mrt_render_desc* d)
     d->rank = 0;
     d->world = 1;
     d->flags = p->numerics ? MRT_RF_FAST : 0u;
+    d->threads = p->num_threads;
 }
 
 // ---- work_queue tile order (work_queue.cpp:6-128) ----

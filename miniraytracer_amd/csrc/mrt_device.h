@@ -19,6 +19,27 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// One source, two backends: the hot-path functions below are compiled for gfx950 (the path
+// kernels, mrt_kernels.hip) and -- in the CPU backend's translation unit, which defines
+// MRT_HOST_BACKEND -- for the host as well (mrt_cpu.hip).  Device intrinsics sit behind
+// __HIP_DEVICE_COMPILE__ with IEEE host forms, so the exact contract gives the same bits on both.
+#ifdef MRT_HOST_BACKEND
+#define MRT_DATTR __host__ __device__
+#else
+#define MRT_DATTR __device__
+#endif
+#define MRT_DFN MRT_DATTR __forceinline__
+#if defined(MRT_HOST_BACKEND) && !defined(__HIP_DEVICE_COMPILE__)
+#include <cmath>
+#include <cstring>
+// host forms of the HIP device built-ins the hot path uses (overloads by target attribute)
+__host__ static inline unsigned int __float_as_uint(float x) { unsigned int u; memcpy(&u, &x, 4); return u; }
+__host__ static inline float __uint_as_float(unsigned int u) { float x; memcpy(&x, &u, 4); return x; }
+__host__ static inline int __float_as_int(float x) { int u; memcpy(&u, &x, 4); return u; }
+__host__ static inline float __int_as_float(int u) { float x; memcpy(&x, &u, 4); return x; }
+__host__ static inline bool isfinite(float x) { return std::isfinite(x); }
+__host__ static inline bool signbit(double x) { return std::signbit(x); }
+#endif
 #include "../../include/mrt_mathfn.h"
 #include "../../include/mrt_scene.h"
 
@@ -68,26 +89,26 @@ namespace mrtd {
 struct f3 {
     float x, y, z;
 };
-__device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
-__device__ __forceinline__ f3 add(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
-__device__ __forceinline__ f3 sub(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
-__device__ __forceinline__ f3 mul(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
-__device__ __forceinline__ f3 mulf(f3 a, float f) { return f3{a.x * f, a.y * f, a.z * f}; }
-__device__ __forceinline__ f3 fmul(float f, f3 a) { return f3{f * a.x, f * a.y, f * a.z}; }
+MRT_DFN f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+MRT_DFN f3 add(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+MRT_DFN f3 sub(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+MRT_DFN f3 mul(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+MRT_DFN f3 mulf(f3 a, float f) { return f3{a.x * f, a.y * f, a.z * f}; }
+MRT_DFN f3 fmul(float f, f3 a) { return f3{f * a.x, f * a.y, f * a.z}; }
 #if MRT_FAST_DIV && defined(__HIP_DEVICE_COMPILE__)
-__device__ __forceinline__ f3 divf(f3 a, float f) {
+MRT_DFN f3 divf(f3 a, float f) {
     const float y = __builtin_amdgcn_rcpf(f);
     return f3{a.x * y, a.y * y, a.z * y};
 }
 #else
-__device__ __forceinline__ f3 divf(f3 a, float f) { return f3{a.x / f, a.y / f, a.z / f}; }
+MRT_DFN f3 divf(f3 a, float f) { return f3{a.x / f, a.y / f, a.z / f}; }
 #endif
-__device__ __forceinline__ float dot(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
-__device__ __forceinline__ float sdot(f3 a) { return (a.x * a.x + a.y * a.y) + a.z * a.z; }
+MRT_DFN float dot(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+MRT_DFN float sdot(f3 a) { return (a.x * a.x + a.y * a.y) + a.z * a.z; }
 // sphere::hit's quadratic (sphere.cpp:20-26): b = dot(oc, d), c = |oc|^2 - r^2, disc = b*b - c.
 // Never FMA-contracted, also in the tolerance-contract build (the CPU restatement built with
 // contraction loses 0.08% of book2's rays through this quadratic; DESIGN.md "Numerics contracts").
-__device__ __forceinline__ float sphere_disc(f3 oc, f3 d, float radius, float* bout) {
+MRT_DFN float sphere_disc(f3 oc, f3 d, float radius, float* bout) {
 #pragma clang fp contract(off)
     const float b = (oc.x * d.x + oc.y * d.y) + oc.z * d.z;
     const float c = ((oc.x * oc.x + oc.y * oc.y) + oc.z * oc.z) - radius * radius;
@@ -104,7 +125,7 @@ __device__ __forceinline__ float sphere_disc(f3 oc, f3 d, float radius, float* b
 // a == 0 or (q' normal and |a| >= 2^-100).  Call sites establish those conditions from cheap range
 // tests on their operands (a ray's `nice` flag, normalize's own test) and take the IEEE division in
 // a wave-uniform branch otherwise (never taken on real scenes).
-__device__ __forceinline__ float recip_nr(float b) {
+MRT_DFN float recip_nr(float b) {
 #if MRT_FAST_DIV && defined(__HIP_DEVICE_COMPILE__)
     return __builtin_amdgcn_rcpf(b);
 #elif defined(__HIP_DEVICE_COMPILE__)
@@ -114,7 +135,7 @@ __device__ __forceinline__ float recip_nr(float b) {
     return 1.0f / b;
 #endif
 }
-__device__ __forceinline__ float div_core(float a, float b, float y) {
+MRT_DFN float div_core(float a, float b, float y) {
 #if MRT_FAST_DIV
     return a * y;
 #endif
@@ -122,7 +143,7 @@ __device__ __forceinline__ float div_core(float a, float b, float y) {
     const float r = __builtin_fmaf(-b, q, a);
     return __builtin_copysignf(__builtin_fmaf(r, y, q), q);
 }
-__device__ __forceinline__ bool any_lane(bool p) {
+MRT_DFN bool any_lane(bool p) {
 #if defined(__HIP_DEVICE_COMPILE__)
     return __builtin_amdgcn_ballot_w64(p) != 0;
 #else
@@ -130,7 +151,7 @@ __device__ __forceinline__ bool any_lane(bool p) {
 #endif
 }
 // |x| as an unsigned key (sign shifted out): 2^e -> (e + 127) << 24, 0 -> 0, inf/NaN above all finite
-__device__ __forceinline__ uint32_t mag2(float x) { return __float_as_uint(x) << 1; }
+MRT_DFN uint32_t mag2(float x) { return __float_as_uint(x) << 1; }
 #define MRT_MAG2(e) ((uint32_t)((e) + 127) << 24)
 // |x| in [2^lo, 2^hi)
 #define MRT_MAG_IN(x, lo, hi) ((mag2(x) - MRT_MAG2(lo)) < (MRT_MAG2(hi) - MRT_MAG2(lo)))
@@ -139,7 +160,7 @@ __device__ __forceinline__ uint32_t mag2(float x) { return __float_as_uint(x) <<
 // equals it for every input with |x| >= 2^-96 or x == +-0 (all 2^32 patterns checked on MI355X,
 // tools/numcheck/sqrt_check.hip).  (RN32(v_sqrt_f64(x)) is NOT exact: v_sqrt_f64 misrounds 3.9% of
 // f32 inputs, tools/numcheck/divsqrt_check.hip.)
-__device__ __forceinline__ float sqrt_core(float x) {
+MRT_DFN float sqrt_core(float x) {
 #if MRT_FAST_SQRT && defined(__HIP_DEVICE_COMPILE__)
     return __builtin_amdgcn_sqrtf(x);
 #elif defined(__HIP_DEVICE_COMPILE__)
@@ -151,7 +172,7 @@ __device__ __forceinline__ float sqrt_core(float x) {
     return __builtin_sqrtf(x);
 #endif
 }
-__device__ __forceinline__ float sqrt_(float x) {
+MRT_DFN float sqrt_(float x) {
     float r = sqrt_core(x);
     if (MRT_FAST_SQRT) return r;
     const bool ok = mag2(x) - 1u >= MRT_MAG2(-96) - 1u;  // |x| >= 2^-96 or x == +-0
@@ -161,7 +182,7 @@ __device__ __forceinline__ float sqrt_(float x) {
 // a / |a| (Vec3::normalize, vec3.h:116-122): one reciprocal for the three quotients.  Fast path:
 // |a|^2 in [2^-52, 2^52) and every component 0 or >= 2^-100 in magnitude (then each quotient is 0
 // or normal, and y is normal).
-__device__ __forceinline__ f3 normalize(f3 a) {
+MRT_DFN f3 normalize(f3 a) {
     const float dd = sdot(a);
 #if MRT_FAST_NORM && defined(__HIP_DEVICE_COMPILE__)
     const float ry = __builtin_amdgcn_rsqf(dd);
@@ -175,12 +196,12 @@ __device__ __forceinline__ f3 normalize(f3 a) {
     if (__builtin_expect(any_lane(!ok), 0)) q = ok ? q : divf(a, __builtin_sqrtf(dd));
     return q;
 }
-__device__ __forceinline__ f3 cross(f3 a, f3 b) { return f3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
-__device__ __forceinline__ float maxps(float a, float b) { return a > b ? a : b; }
-__device__ __forceinline__ float minps(float a, float b) { return a < b ? a : b; }
-__device__ __forceinline__ f3 ld3(const float* p) { return f3{p[0], p[1], p[2]}; }
-__device__ __forceinline__ f3 ld3(float4 v) { return f3{v.x, v.y, v.z}; }
-__device__ __forceinline__ bool finite3(f3 a) { return isfinite(a.x) && isfinite(a.y) && isfinite(a.z); }
+MRT_DFN f3 cross(f3 a, f3 b) { return f3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+MRT_DFN float maxps(float a, float b) { return a > b ? a : b; }
+MRT_DFN float minps(float a, float b) { return a < b ? a : b; }
+MRT_DFN f3 ld3(const float* p) { return f3{p[0], p[1], p[2]}; }
+MRT_DFN f3 ld3(float4 v) { return f3{v.x, v.y, v.z}; }
+MRT_DFN bool finite3(f3 a) { return isfinite(a.x) && isfinite(a.y) && isfinite(a.z); }
 
 static constexpr float PI_F = 3.14159265358979323846f;
 static constexpr float FLT_MAX_ = 3.402823466e+38f;
@@ -188,65 +209,65 @@ static constexpr float FLT_MAX_ = 3.402823466e+38f;
 #if MRT_FAST_TRANS && defined(__HIP_DEVICE_COMPILE__)
 // tolerance contract: f32 library functions; sincos of a path angle in [0, 2 pi) by the hardware
 // v_sin/v_cos (argument in revolutions), log by v_log (log2)
-__device__ __forceinline__ float sin_(float x) { return sinf(x); }
-__device__ __forceinline__ float cos_(float x) { return cosf(x); }
-__device__ __forceinline__ void sincos_(float x, float* s, float* c) {
+MRT_DFN float sin_(float x) { return sinf(x); }
+MRT_DFN float cos_(float x) { return cosf(x); }
+MRT_DFN void sincos_(float x, float* s, float* c) {
     const float rev = x * 0.15915494309189535f;
     *s = __builtin_amdgcn_sinf(rev);
     *c = __builtin_amdgcn_cosf(rev);
 }
-__device__ __forceinline__ float log_(float x) { return __builtin_amdgcn_logf(x) * 0.69314718055994531f; }
-__device__ __forceinline__ float pow5_(float x) {
+MRT_DFN float log_(float x) { return __builtin_amdgcn_logf(x) * 0.69314718055994531f; }
+MRT_DFN float pow5_(float x) {
     const float x2 = x * x;
     return (x2 * x2) * x;
 }
-__device__ __forceinline__ float atan2_(float y, float x) { return atan2f(y, x); }
-__device__ __forceinline__ float asin_(float x) { return asinf(x); }
+MRT_DFN float atan2_(float y, float x) { return atan2f(y, x); }
+MRT_DFN float asin_(float x) { return asinf(x); }
 #else
 // transcendentals: the numerics contract of include/mrt_mathfn.h (same bits as host and oracle)
-__device__ __forceinline__ float sin_(float x) { return mrt_sinf(x); }
-__device__ __forceinline__ float cos_(float x) { return mrt_cosf(x); }
-__device__ __forceinline__ void sincos_(float x, float* s, float* c) {
+MRT_DFN float sin_(float x) { return mrt_sinf(x); }
+MRT_DFN float cos_(float x) { return mrt_cosf(x); }
+MRT_DFN void sincos_(float x, float* s, float* c) {
     double ds, dc;
     mrt_sincos_d((double)x, &ds, &dc);
     *s = (float)ds;
     *c = (float)dc;
 }
-__device__ __forceinline__ float log_(float x) { return mrt_logf(x); }
-__device__ __forceinline__ float pow5_(float x) { return mrt_pow5f(x); }
-__device__ __forceinline__ float atan2_(float y, float x) { return mrt_atan2f(y, x); }
-__device__ __forceinline__ float asin_(float x) { return mrt_asinf(x); }
+MRT_DFN float log_(float x) { return mrt_logf(x); }
+MRT_DFN float pow5_(float x) { return mrt_pow5f(x); }
+MRT_DFN float atan2_(float y, float x) { return mrt_atan2f(y, x); }
+MRT_DFN float asin_(float x) { return mrt_asinf(x); }
 #endif
 
 // ---------------------------------------------------------------- PCG32 (pcg.cpp:13-62)
 struct Pcg {
     uint64_t state, inc;
 };
-__device__ __forceinline__ uint32_t pcg_next(Pcg& r) {
+MRT_DFN uint32_t pcg_next(Pcg& r) {
     uint64_t old = r.state;
     r.state = old * 6364136223846793005ULL + r.inc;
     uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
     uint32_t rot = (uint32_t)(old >> 59u);
     return (xs >> rot) | (xs << ((0u - rot) & 31u));
 }
-__device__ __forceinline__ void pcg_seed(Pcg& r, uint64_t initstate, uint64_t initseq) {
+MRT_DFN void pcg_seed(Pcg& r, uint64_t initstate, uint64_t initseq) {
     r.state = 0u;
     r.inc = (initseq << 1u) | 1u;
     pcg_next(r);
     r.state += initstate;
     pcg_next(r);
 }
-__device__ __forceinline__ float randf(Pcg& r) {
+MRT_DFN float randf(Pcg& r) {
     return __uint_as_float(0x3f800000u | (pcg_next(r) & 0x007FFFFFu)) - 1.0f;
 }
-__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+MRT_DFN uint64_t splitmix64(uint64_t z) {
     z += 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
 // samplers (pcg.cpp:70-136); Vec3(randf(), randf(), ...) arguments drawn left to right
-__device__ __forceinline__ f3 random_in_sphere(Pcg& r) {
+MRT_DFN f3 random_in_sphere(Pcg& r) {
     f3 p;
     do {
         float a = randf(r), b = randf(r), c = randf(r);
@@ -254,7 +275,7 @@ __device__ __forceinline__ f3 random_in_sphere(Pcg& r) {
     } while (sdot(p) >= 1.0f);
     return p;
 }
-__device__ __forceinline__ f3 random_in_disk(Pcg& r) {
+MRT_DFN f3 random_in_disk(Pcg& r) {
     f3 p;
     do {
         float a = randf(r), b = randf(r);
@@ -265,7 +286,7 @@ __device__ __forceinline__ f3 random_in_disk(Pcg& r) {
 // random_cosine_direction (pcg.cpp:87-95) given its two draws r1, r2 (the caller draws them, in
 // that order).  NOTE: x,y scaled by 2*sqrt(r2), as the reference does (pcg.cpp:92-93).
 // randf() is 0 or >= 2^-23: both radicands are 0 or in [2^-23, 1], where sqrt_core is exact.
-__device__ __forceinline__ f3 random_cosine_direction_pre(float r1, float r2) {
+MRT_DFN f3 random_cosine_direction_pre(float r1, float r2) {
     float z = sqrt_core(1 - r2);
     float phi = (2 * PI_F) * r1;
     float s2 = sqrt_core(r2);
@@ -274,7 +295,7 @@ __device__ __forceinline__ f3 random_cosine_direction_pre(float r1, float r2) {
     return f3{(cp * 2) * s2, (sp * 2) * s2, z};
 }
 // random_towards_sphere (pcg.cpp:125-133) given its two draws r1, r2 (sphere::pdf_generate, sphere.cpp:63-78)
-__device__ __forceinline__ f3 random_towards_sphere_pre(float r1, float r2, float radius, float dist_sq) {
+MRT_DFN f3 random_towards_sphere_pre(float r1, float r2, float radius, float dist_sq) {
     float z = 1 + r2 * (sqrt_(1 - (radius * radius) / dist_sq) - 1);
     float phi = (2 * PI_F) * r1;
     float q = sqrt_(1 - z * z);
@@ -295,7 +316,7 @@ struct Ray {
 // component is 0 or in [2^-77, 2^60]: then inv = recip_nr(d) is exact, and a rect test's
 // (k - o_a) / d_a may use div_core with inv (the difference of two such coordinates -- rect planes are
 // checked on upload, MRT_F_SLOWDIV -- is 0 or >= 2^-100, and the quotient stays normal).
-__device__ __forceinline__ bool ray_nice(f3 o, f3 d) {
+MRT_DFN bool ray_nice(f3 o, f3 d) {
     if (MRT_FAST_GUARDS) return true;  // no exactness guards: every ray takes the hardware reciprocal
     const bool dn = MRT_MAG_IN(d.x, -26, 1) & MRT_MAG_IN(d.y, -26, 1) & MRT_MAG_IN(d.z, -26, 1);
     const uint32_t mn = min(min(mag2(o.x) - 1u, mag2(o.y) - 1u), mag2(o.z) - 1u);  // 0 -> UINT_MAX
@@ -303,12 +324,12 @@ __device__ __forceinline__ bool ray_nice(f3 o, f3 d) {
     return dn & (mn >= MRT_MAG2(-77) - 1u) & (mx <= 0x1p60f);
 }
 // 1/d per component (aabb.h:49), exact
-__device__ __forceinline__ f3 ray_inv(f3 d, bool nice) {
+MRT_DFN f3 ray_inv(f3 d, bool nice) {
     f3 y{recip_nr(d.x), recip_nr(d.y), recip_nr(d.z)};
     if (__builtin_expect(any_lane(!nice), 0)) y = nice ? y : f3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
     return y;
 }
-__device__ __forceinline__ Ray make_ray(f3 o, f3 dir, float time, int inside) {
+MRT_DFN Ray make_ray(f3 o, f3 dir, float time, int inside) {
     Ray r;
     r.o = o;
     r.d = normalize(dir);
@@ -327,7 +348,7 @@ __device__ __forceinline__ Ray make_ray(f3 o, f3 dir, float time, int inside) {
 #ifndef MRT_FAST_UNIT
 #define MRT_FAST_UNIT MRT_FAST
 #endif
-__device__ __forceinline__ Ray make_ray_unit(f3 o, f3 dir, float time, int inside) {
+MRT_DFN Ray make_ray_unit(f3 o, f3 dir, float time, int inside) {
 #if MRT_FAST_UNIT
     Ray r;
     r.o = o;
@@ -344,7 +365,7 @@ __device__ __forceinline__ Ray make_ray_unit(f3 o, f3 dir, float time, int insid
 #endif
 }
 // translate::hit's moved ray (scene_object.cpp:11): the same direction, a new origin
-__device__ __forceinline__ Ray moved_ray(const Ray& r0, f3 o) {
+MRT_DFN Ray moved_ray(const Ray& r0, f3 o) {
 #if MRT_FAST_UNIT
     Ray r = r0;  // direction, its reciprocal and mask reused as they are
     r.o = o;
@@ -355,10 +376,10 @@ __device__ __forceinline__ Ray moved_ray(const Ray& r0, f3 o) {
     return make_ray(o, r0.d, r0.time, 0);
 #endif
 }
-__device__ __forceinline__ f3 eval(const Ray& r, float t) { return add(r.o, fmul(t, r.d)); }
+MRT_DFN f3 eval(const Ray& r, float t) { return add(r.o, fmul(t, r.d)); }
 
 // aabb::hit, active SSE branch (aabb.h:49-76)
-__device__ __forceinline__ bool aabb_hit(const float* bmin, const float* bmax, const Ray& r, float tmin, float tmax) {
+MRT_DFN bool aabb_hit(const float* bmin, const float* bmax, const Ray& r, float tmin, float tmax) {
     float t0x = (bmin[0] - r.o.x) * r.inv.x, t0y = (bmin[1] - r.o.y) * r.inv.y, t0z = (bmin[2] - r.o.z) * r.inv.z;
     float t1x = (bmax[0] - r.o.x) * r.inv.x, t1y = (bmax[1] - r.o.y) * r.inv.y, t1z = (bmax[2] - r.o.z) * r.inv.z;
     // A nice ray (|inv| <= 2^26, |o| <= 2^60) with a box of finite coordinates gets no NaN slab
@@ -380,13 +401,17 @@ __device__ __forceinline__ bool aabb_hit(const float* bmin, const float* bmax, c
     return h;
 }
 
-__device__ __forceinline__ bool aabb_hit(f3 bmin, f3 bmax, const Ray& r, float tmin, float tmax) {
+MRT_DFN bool aabb_hit(f3 bmin, f3 bmax, const Ray& r, float tmin, float tmax) {
     const float b[6] = {bmin.x, bmin.y, bmin.z, bmax.x, bmax.y, bmax.z};
     return aabb_hit(b, b + 3, r, tmin, tmax);
 }
 
 // uniform-address reads of scene tables through the constant address space -> s_load
+#if defined(__HIP_DEVICE_COMPILE__)
 #define MRT_CONST_AS __attribute__((address_space(4)))
+#else
+#define MRT_CONST_AS
+#endif
 #define MRT_F_SLOWDIV 0x8u  /* set on upload on rects whose plane coordinate is outside {0} U [2^-77, 2^60] */
 #if defined(__HIP_DEVICE_COMPILE__)
 #define MRT_GLOBAL_AS __attribute__((address_space(1)))
@@ -397,10 +422,12 @@ __device__ __forceinline__ bool aabb_hit(f3 bmin, f3 bmax, const Ray& r, float t
 #endif
 typedef float v4f __attribute__((ext_vector_type(4)));  // native vector: loads/stores in any address space
 template <typename T>
-__device__ __forceinline__ const MRT_CONST_AS T* const_ptr(const T* p) {
+MRT_DFN const MRT_CONST_AS T* const_ptr(const T* p) {
     return (const MRT_CONST_AS T*)p;
 }
-__device__ __forceinline__ f3 ld3(const MRT_CONST_AS float* p) { return f3{p[0], p[1], p[2]}; }
+#if defined(__HIP_DEVICE_COMPILE__)  // (host: the same type as ld3(const float*))
+MRT_DFN f3 ld3(const MRT_CONST_AS float* p) { return f3{p[0], p[1], p[2]}; }
+#endif
 
 // Phase clock (experiment builds with -DMRT_PHASES): wave-uniform s_memtime deltas per phase.
 #ifdef MRT_PHASES

@@ -39,15 +39,17 @@ static_assert(sizeof(LinOp) == 64, "LinOp is one 64 B scalar load");
 #define LOP_KIND(o) (((o).code >> 8) & 0xFFu)
 #define LOP_FLAGS(o) (((o).code >> 16) & 0xFFu)
 
-__device__ __forceinline__ uint32_t op_flags(const LinOp& o) { return LOP_FLAGS(o); }
-__device__ __forceinline__ uint32_t op_flags(const MRT_CONST_AS LinOp& o) { return LOP_FLAGS(o); }
-__device__ __forceinline__ uint32_t op_flags(const mrt_node& n) { return MRT_NODE_FLAGS(n); }
+MRT_DFN uint32_t op_flags(const LinOp& o) { return LOP_FLAGS(o); }
+#if defined(__HIP_DEVICE_COMPILE__)
+MRT_DFN uint32_t op_flags(const MRT_CONST_AS LinOp& o) { return LOP_FLAGS(o); }
+#endif
+MRT_DFN uint32_t op_flags(const mrt_node& n) { return MRT_NODE_FLAGS(n); }
 
 // t of the primitive's hit() or a miss; no record written.  KIND is wave-uniform at the call.
 // Branch-free: every lane evaluates the whole test and the outcome is a predicate (the early
 // returns of the reference only skip work whose result is unused, so the outcome is the same).
 template <uint32_t F, uint32_t KIND, typename OP>
-__device__ __forceinline__ bool lin_prim_t(const OP& o, const Ray& r, float tmin, float tmax, float* tout) {
+MRT_DFN bool lin_prim_t(const OP& o, const Ray& r, float tmin, float tmax, float* tout) {
     if constexpr (KIND == MRT_K_SPHERE) {  // sphere::hit (sphere.cpp:13-46)
         f3 cen = f3{o.f[0], o.f[1], o.f[2]};
         if ((F & FT_MOVING) && (LOP_FLAGS(o) & MRT_F_MOVING))
@@ -95,7 +97,7 @@ __device__ __forceinline__ bool lin_prim_t(const OP& o, const Ray& r, float tmin
 // lin_prim_rec for a primitive op whose kind is known at compile time, its data read through the
 // constant address space (wave-uniform op: scalar loads).  Same arithmetic as lin_prim_rec.
 template <uint32_t F, uint32_t KIND>
-__device__ __forceinline__ void lin_prim_rec_op(const MRT_CONST_AS LinOp& o, const Ray& r, float t, HitRec& rec) {
+MRT_DFN void lin_prim_rec_op(const MRT_CONST_AS LinOp& o, const Ray& r, float t, HitRec& rec) {
     const uint32_t fl = LOP_FLAGS(o);
     const bool needuv = (F & FT_UV) && (fl & MRT_F_NEEDUV);
     rec.t = t;
@@ -134,7 +136,7 @@ __device__ __forceinline__ void lin_prim_rec_op(const MRT_CONST_AS LinOp& o, con
 // fetched whole (four 16-byte loads in flight together) rather than field by field, which the
 // compiler turned into two dependent round trips (kind/mat, then the kind's fields).
 template <uint32_t F>
-__device__ __forceinline__ void lin_prim_rec(const DScene& S, uint32_t node, const Ray& r, float t, HitRec& rec) {
+MRT_DFN void lin_prim_rec(const DScene& S, uint32_t node, const Ray& r, float t, HitRec& rec) {
 #ifndef MRT_REC_FIELDWISE
     const float4* q = reinterpret_cast<const float4*>(S.nodes + node);
     const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
@@ -180,7 +182,7 @@ __device__ __forceinline__ void lin_prim_rec(const DScene& S, uint32_t node, con
 }
 
 // the query ray parked in LDS while an instance ray occupies the registers ([word][lane])
-__device__ __forceinline__ void lin_save_ray(const LStack& L, const Ray& r) {
+MRT_DFN void lin_save_ray(const LStack& L, const Ray& r) {
     float* b = L.save + L.lane;
     b[0] = r.o.x; b[64] = r.o.y; b[128] = r.o.z;
     b[192] = r.d.x; b[256] = r.d.y; b[320] = r.d.z;
@@ -188,7 +190,7 @@ __device__ __forceinline__ void lin_save_ray(const LStack& L, const Ray& r) {
     b[448] = __int_as_float(r.inside);
     b[512] = __uint_as_float(r.mask);
 }
-__device__ __forceinline__ Ray lin_load_ray(const LStack& L) {
+MRT_DFN Ray lin_load_ray(const LStack& L) {
     const float* b = L.save + L.lane;
     Ray r;
     r.o = f3{b[0], b[64], b[128]};
@@ -204,7 +206,7 @@ __device__ __forceinline__ Ray lin_load_ray(const LStack& L) {
 // one point, so the loads cannot be sunk to their uses (the compiler otherwise split each op into
 // three load + s_waitcnt round trips to the scalar cache).
 template <uint32_t F, uint32_t KIND>
-__device__ __forceinline__ LinOp lin_fetch_op(const MRT_CONST_AS LinOp& o) {
+MRT_DFN LinOp lin_fetch_op(const MRT_CONST_AS LinOp& o) {
     const MRT_CONST_AS uint32_t* q = reinterpret_cast<const MRT_CONST_AS uint32_t*>(&o);
     LinOp r;
     r.code = q[0];
@@ -230,14 +232,14 @@ __device__ __forceinline__ LinOp lin_fetch_op(const MRT_CONST_AS LinOp& o) {
     return r;
 }
 // aabb::hit (invDir = 1/dir of the ray, aabb.h:49)
-__device__ __forceinline__ bool lin_box(const MRT_CONST_AS LinOp& o, const Ray& r, float tmin, float tmax) {
+MRT_DFN bool lin_box(const MRT_CONST_AS LinOp& o, const Ray& r, float tmin, float tmax) {
     const float b[6] = {o.f[0], o.f[1], o.f[2], o.f[3], o.f[4], o.f[5]};
     return aabb_hit(b, b + 3, r, tmin, tmax);
 }
 
 // record frames of instance hits, back to the world (scene_object.cpp:13-16, 85-93)
 template <typename OP>
-__device__ __forceinline__ void lin_untransform(const OP& io, HitRec& rec) {
+MRT_DFN void lin_untransform(const OP& io, HitRec& rec) {
     const uint32_t kind = LOP_KIND(io);
     if (kind == MRT_K_TRROTY) {
         unrotate_rec(rec, io.f[6], io.f[7]);
@@ -253,7 +255,7 @@ __device__ __forceinline__ void lin_untransform(const OP& io, HitRec& rec) {
 // LDS per lane (L.save): [0..8] the query ray, [9..14] origin/direction of the instance ray of
 // the closest hit (written at the instance's END op when that hit lies inside it).
 template <uint32_t F>
-__device__ __forceinline__ bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, const LStack& L, Pcg& rng, PhaseClock& ph) {
+MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, const LStack& L, Pcg& rng, PhaseClock& ph) {
     constexpr bool INST = (F & FT_INST) != 0;
     if (INST) lin_save_ray(L, r);
     Ray cur = r;
@@ -345,7 +347,7 @@ __device__ __forceinline__ bool scene_hit_lin(const DScene& S, Ray& r, float tmi
             if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, cur, tmin, closest);
             lvl++;
             act = (act & ~(1u << lvl)) | ((uint32_t)in << lvl);
-            if (!__any(in)) pc = o.skip - 1;
+            if (!any_lane(in)) pc = o.skip - 1;
         } else if (INST && op == LOP_INST) {
             const uint32_t kind = LOP_KIND(o);
             bool in = on;
@@ -360,7 +362,7 @@ __device__ __forceinline__ bool scene_hit_lin(const DScene& S, Ray& r, float tmi
             lvl++;
             act = (act & ~(1u << lvl)) | ((uint32_t)in << lvl);
             inst = pc;
-            if (!__any(in)) {
+            if (!any_lane(in)) {
                 pc = o.skip - 1;
                 continue;
             }

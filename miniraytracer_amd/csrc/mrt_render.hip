@@ -24,6 +24,8 @@
 
 #include "mrt_internal.h"
 #include "mrt_launch.h"
+#include "mrt_tables.h"
+#include "mrt_cpu.h"
 #include "../../include/mrt_tonemap.h"
 
 using namespace mrtd;
@@ -46,20 +48,6 @@ static uint32_t pick_variant(uint32_t features) {
     return kNumVariants - 1;
 }
 
-__device__ __forceinline__ float lum3(f3 c) { return (c.x * 0.212655f + c.y * 0.715158f) + c.z * 0.072187f; }
-
-// one sample of draw()/draw2()'s per-pixel loop
-__device__ __forceinline__ f3 fold_sample(f3 c, f3 smp, uint32_t s, uint32_t mode, float max_lum) {
-    if (mode == 0) {
-        if (!finite3(smp)) smp = c;
-        return add(c, smp);
-    }
-    if (!finite3(smp)) smp = s > 0 ? c : f3{0, 0, 0};
-    if (s > 0) smp = add(c, mulf(sub(smp, c), 1.0f / ((float)s + 1.0f)));
-    float l = lum3(smp);
-    if (l > max_lum) smp = mulf(smp, max_lum / l);
-    return smp;
-}
 // The sum is sequential per pixel (bit-exact order), so the kernel is load-latency bound when
 // few pixels are local (multi-GPU shards): samples are fetched FOLD_DEPTH at a time (coalesced
 // across the wave's pixels) before the dependent adds.
@@ -95,12 +83,7 @@ __global__ void __launch_bounds__(256) mrt_final_kernel(const float4* __restrict
     uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
     if (lp >= npix) return;
     float4 a = acc[lp];
-    f3 c{a.x, a.y, a.z};
-    if (mode == 0) {
-        c = divf(c, (float)ns);
-        float l = lum3(c);
-        if (l > max_lum) c = mulf(c, max_lum / l);
-    }
+    const f3 c = final_pixel(f3{a.x, a.y, a.z}, ns, mode, max_lum);
     out[lp] = make_float4(c.x, c.y, c.z, 0.0f);
 }
 
@@ -190,6 +173,7 @@ static void bfs_order(std::vector<W>& wide, std::vector<uint32_t*> roots, uint32
 
 struct mrt_scene {
     int device = 0;
+    mrt_cpu_scene* cpu = nullptr;  // MRT_DEVICE_CPU: the CPU backend's scene (mrt_cpu.hip); nothing below is used
     DScene S{};
     DScene* d_S = nullptr;
     std::vector<void*> allocs;
@@ -427,8 +411,10 @@ static uint32_t scene_features(const mrt_scene_view* v, const std::vector<mrt_no
     return f;
 }
 
-extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_scene** out) {
-    if (!v || !out || v->root >= v->n_nodes) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_scene_upload: bad view");
+// The scene's device tables (mrt_tables.h), built on the host from the caller's view; both
+// backends run on them: mrt_scene_upload copies them to HBM, mrt_cpu_scene_create keeps them.
+mrt_status mrt_internal_scene_tables(const mrt_scene_view* v, SceneTables* T) {
+    if (!v || !T || v->root >= v->n_nodes) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_scene_upload: bad view");
     // device node table: NEEDUV flags; translate(rotate_y(x)) fused into one instance node
     std::vector<mrt_node> nodes(v->nodes, v->nodes + v->n_nodes);
     for (mrt_node& n : nodes) {
@@ -614,20 +600,6 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
                 if ((nodes[v->children[b.a + i]].kind & 0xFF) == MRT_K_LIST)
                     return mrt_internal_fail(MRT_ERR_INVALID, "nested biased object_list");
     }
-    HIPCHK(hipSetDevice(device));
-    mrt_scene* s = new mrt_scene();
-    s->device = device;
-    mrt_status st;
-    DScene& S = s->S;
-#define UP(src, n, dst) { void* t_ = nullptr; if ((st = upload(s, src, (size_t)(n) * sizeof(*(src)), &t_))) { mrt_scene_free(s); return st; } *(dst) = (decltype(+*(dst)))t_; }
-    UP(nodes.data(), nodes.size(), &S.nodes);
-    UP(v->children, v->n_children, &S.children);
-    UP(v->mesh_nodes, v->n_mesh_nodes, &S.mnodes);
-    UP(wide.data(), wide.size(), &S.mwide);
-    UP(bwide.data(), bwide.size(), &S.bwide);
-    UP(bprims.data(), bprims.size(), &S.bprims);
-    UP((const float4*)v->tri_geo, (size_t)v->n_tris * 3, &S.tri_geo);
-    UP((const float4*)v->tri_nrm, (size_t)v->n_tris * 3, &S.tri_nrm);
     std::vector<DMat> dmats(v->n_materials);
     for (uint32_t i = 0; i < v->n_materials; i++) {
         const mrt_material& m = v->materials[i];
@@ -647,7 +619,6 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
             d.col[1] = r0 * r0;
         }
     }
-    UP(dmats.data(), dmats.size(), &S.mats);
     // scene.biased_objects flattened: an object_list's children, or the object itself
     std::vector<mrt_node> bleaf;
     uint32_t blist = 0;
@@ -661,20 +632,71 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
         }
     }
     if (bleaf.empty()) bleaf.push_back(mrt_node{});
-    UP(bleaf.data(), bleaf.size(), &S.bleaf);
-    S.nbleaf = blist ? nodes[v->biased].b : 1u;
-    S.blist = blist;
-    UP(v->textures, v->n_textures, &S.texs);
-    UP((const float4*)v->perlin_ranvec, 256, &S.ranvec);
-    UP(v->perlin_perm, 768, &S.perm);
-    UP(v->texels, (size_t)v->n_texels, &S.texels);
     LinCompiler lc{nodes, v, {}};
     const char* force_generic = getenv("MRT_FORCE_GENERIC");  // test hook: run the generic machine
     const bool lin = !(force_generic && *force_generic && *force_generic != '0') && lc.emit(v->root, 0, 0, 0);
     if (!lin) lc.prog.clear();
-    const uint32_t prog_ops = (uint32_t)lc.prog.size();
+    T->prog_ops = (uint32_t)lc.prog.size();
     lc.prog.push_back(LinOp{});  // LOP_END
-    UP(lc.prog.data(), lc.prog.size(), &S.prog);
+    T->features = scene_features(v, nodes, absorbed);
+    const char* no_sig = getenv("MRT_NO_SIG");  // test hook: run the interpreter on known shapes too
+    if (lin) T->features |= FT_LIN;
+    if (lin && !(no_sig && *no_sig && *no_sig != '0')) T->features |= MRT_SIG_BITS(lin_sig_of(lc.prog.data(), (uint32_t)lc.prog.size()));
+    T->nbleaf = blist ? nodes[v->biased].b : 1u;
+    T->blist = blist;
+    T->max_frames = gc.max_frames;
+    T->max_rays = gc.max_rays;
+    T->max_mesh = gc.max_mesh;
+    T->nodes.swap(nodes);
+    T->wide.swap(wide);
+    T->bwide.swap(bwide);
+    T->bprims.swap(bprims);
+    T->dmats.swap(dmats);
+    T->bleaf.swap(bleaf);
+    T->prog.swap(lc.prog);
+    return MRT_OK;
+}
+
+extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_scene** out) {
+    if (!out) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_scene_upload: null");
+    if (device == MRT_DEVICE_CPU) {  // the CPU backend (explicit choice only)
+        mrt_cpu_scene* c = nullptr;
+        mrt_status st = mrt_cpu_scene_create(v, &c);
+        if (st) return st;
+        mrt_scene* s = new mrt_scene();
+        s->device = MRT_DEVICE_CPU;
+        s->cpu = c;
+        s->n_nodes = v->n_nodes;
+        s->features = mrt_cpu_scene_features(c);
+        *out = s;
+        return MRT_OK;
+    }
+    if (device < 0) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_scene_upload: bad device");
+    SceneTables T;
+    mrt_status st = mrt_internal_scene_tables(v, &T);
+    if (st) return st;
+    HIPCHK(hipSetDevice(device));
+    mrt_scene* s = new mrt_scene();
+    s->device = device;
+    DScene& S = s->S;
+#define UP(src, n, dst) { void* t_ = nullptr; if ((st = upload(s, src, (size_t)(n) * sizeof(*(src)), &t_))) { mrt_scene_free(s); return st; } *(dst) = (decltype(+*(dst)))t_; }
+    UP(T.nodes.data(), T.nodes.size(), &S.nodes);
+    UP(v->children, v->n_children, &S.children);
+    UP(v->mesh_nodes, v->n_mesh_nodes, &S.mnodes);
+    UP(T.wide.data(), T.wide.size(), &S.mwide);
+    UP(T.bwide.data(), T.bwide.size(), &S.bwide);
+    UP(T.bprims.data(), T.bprims.size(), &S.bprims);
+    UP((const float4*)v->tri_geo, (size_t)v->n_tris * 3, &S.tri_geo);
+    UP((const float4*)v->tri_nrm, (size_t)v->n_tris * 3, &S.tri_nrm);
+    UP(T.dmats.data(), T.dmats.size(), &S.mats);
+    UP(T.bleaf.data(), T.bleaf.size(), &S.bleaf);
+    S.nbleaf = T.nbleaf;
+    S.blist = T.blist;
+    UP(v->textures, v->n_textures, &S.texs);
+    UP((const float4*)v->perlin_ranvec, 256, &S.ranvec);
+    UP(v->perlin_perm, 768, &S.perm);
+    UP(v->texels, (size_t)v->n_texels, &S.texels);
+    UP(T.prog.data(), T.prog.size(), &S.prog);
     UP(&v->camera, 1, &S.camp);
 #undef UP
     S.root = v->root;
@@ -682,7 +704,7 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     S.sky = v->sky;
     S.cam = v->camera;
     s->n_nodes = v->n_nodes;
-    s->prog_ops = prog_ops;
+    s->prog_ops = T.prog_ops;
     void* p;
     if ((st = upload(s, &s->S, sizeof(DScene), &p))) { mrt_scene_free(s); return st; }
     s->d_S = (DScene*)p;
@@ -690,16 +712,14 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     s->d_counter = (uint64_t*)p;
     s->d_rays = (unsigned long long*)((char*)p + 16);
     // kernel variant + LDS stacks sized from the scene graph (top frame lives in registers)
-    s->features = scene_features(v, nodes, absorbed);
-    const char* no_sig = getenv("MRT_NO_SIG");  // test hook: run the interpreter on known shapes too
-    if (lin) s->features |= FT_LIN;
-    if (lin && !(no_sig && *no_sig && *no_sig != '0')) s->features |= MRT_SIG_BITS(lin_sig_of(lc.prog.data(), (uint32_t)lc.prog.size()));
+    s->features = T.features;
     s->variant = pick_variant(s->features);
     const bool lin_kernel = (kVariants[s->variant] & FT_LIN) != 0;
-    s->lds_frames = lin_kernel ? 0 : (uint32_t)std::max(gc.max_frames - 1, 0);
-    s->lds_rays = lin_kernel ? 0 : (uint32_t)gc.max_rays;
-    s->lds_mesh = (uint32_t)gc.max_mesh;
+    s->lds_frames = lin_kernel ? 0 : (uint32_t)std::max(T.max_frames - 1, 0);
+    s->lds_rays = lin_kernel ? 0 : (uint32_t)T.max_rays;
+    s->lds_mesh = (uint32_t)T.max_mesh;
     s->lds_save = (lin_kernel && (kVariants[s->variant] & FT_INST)) ? 15u : 0u;
+    const std::vector<BvhWide>& bwide = T.bwide;
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
     // resident workgroups per CU: one 256-thread group = one wave per SIMD (a 64-thread group =
@@ -750,6 +770,11 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
 
 extern "C" void mrt_scene_free(mrt_scene* s) {
     if (!s) return;
+    if (s->cpu) {
+        mrt_cpu_scene_free(s->cpu);
+        delete s;
+        return;
+    }
     (void)hipSetDevice(s->device);
     if (s->ev_done_pending) (void)hipEventSynchronize(s->ev_done);
     for (void* p : s->allocs) (void)hipFree(p);
@@ -799,7 +824,11 @@ static mrt_status grow(mrt_scene* s, void** p, size_t* cap, size_t bytes) {
     return MRT_OK;
 }
 
+#define MRT_GPU_ONLY(s, what) \
+    if ((s) && (s)->cpu) return mrt_internal_fail(MRT_ERR_INVALID, what " is a GPU-backend entry point (scene on MRT_DEVICE_CPU)")
+
 extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
+    MRT_GPU_ONLY(s, "mrt_prepare");
     if (!s || !d || d->width == 0 || d->height == 0 || d->sqrt_samples == 0 || (d->world && d->rank >= d->world))
         return mrt_internal_fail(MRT_ERR_INVALID, "mrt_prepare: bad desc");
     HIPCHK(hipSetDevice(s->device));
@@ -872,6 +901,7 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
 }
 
 extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, float* d_local, uint64_t* d_rays, void* stream) {
+    MRT_GPU_ONLY(s, "mrt_render_device");
     if (!s || !d || !d_local) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_render_device: null");
     s->n_chunks.store(0, std::memory_order_release);  // progress: a new render, not started
     mrt_status st = mrt_prepare(s, d);
@@ -949,6 +979,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
 
 extern "C" mrt_status mrt_render(mrt_scene* s, const mrt_render_desc* d, float* rgb_out, uint64_t* rays_out, const volatile int* cancel) {
     if (!s || !d || !rgb_out) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_render: null");
+    if (s->cpu) return mrt_cpu_render(s->cpu, d, rgb_out, rays_out, cancel);
     s->n_chunks.store(0, std::memory_order_release);
     if (cancel && *cancel) return mrt_internal_fail(MRT_ERR_CANCELLED, "cancelled");
     mrt_render_desc dc = *d;  // a cancellable render runs as >= 16 launches; cancel lands between them
@@ -989,6 +1020,7 @@ extern "C" mrt_status mrt_render(mrt_scene* s, const mrt_render_desc* d, float* 
 }
 
 extern "C" mrt_status mrt_render_debug(mrt_scene* s, float* path_rgb, uint32_t* path_rays, uint64_t n_paths) {
+    MRT_GPU_ONLY(s, "mrt_render_debug");
     if (!s || !(s->wdesc.flags & MRT_RF_PATH_DEBUG) || n_paths != s->last_paths)
         return mrt_internal_fail(MRT_ERR_INVALID, "mrt_render_debug: no debug render of that size");
     HIPCHK(hipSetDevice(s->device));
@@ -1004,6 +1036,7 @@ extern "C" mrt_status mrt_render_debug(mrt_scene* s, float* path_rgb, uint32_t* 
 extern "C" mrt_status mrt_progress(mrt_scene* s, float* pct) {
     if (!s || !pct) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_progress: null");
     *pct = 0.0f;
+    if (s->cpu) return mrt_cpu_progress(s->cpu, pct);
     std::lock_guard<std::mutex> lk(s->prog_mu);
     const size_t n = s->n_chunks.load(std::memory_order_acquire);
     if (n == 0 || !s->h_prog || s->h_prog_cap < n || s->ev.size() < 2 * n || s->h_seen.size() < n) return MRT_OK;  // not started
@@ -1027,6 +1060,16 @@ extern "C" mrt_status mrt_progress(mrt_scene* s, float* pct) {
 extern "C" mrt_status mrt_scene_kernel_info(const mrt_scene* s, mrt_kernel_info* out) {
     if (!s || !out) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_scene_kernel_info: null");
     out->features = s->features;
+    if (s->cpu) {  // the host instantiation that runs it (mrt_cpu.hip), threads of the last render
+        float ms;
+        uint32_t threads = 0;
+        mrt_cpu_last_ms(s->cpu, &ms, &threads);
+        *out = mrt_kernel_info{};
+        out->features = s->features;
+        out->kernel_features = (s->features & FT_LIN) ? (FT_LIN | FT_ALL) : FT_ALL;
+        out->grid = threads;
+        return MRT_OK;
+    }
     out->kernel_features = kVariants[s->variant];
     const PathLaunch& L = s->pl[s->last_numerics];
     out->lds_bytes = (uint32_t)L.lds_bytes;
@@ -1040,6 +1083,10 @@ extern "C" mrt_status mrt_scene_kernel_info(const mrt_scene* s, mrt_kernel_info*
 
 extern "C" mrt_status mrt_kernel_ms(mrt_scene* s, float* path_ms, uint32_t* launches) {
     if (!s || !path_ms) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_kernel_ms: null");
+    if (s->cpu) {  // wall time of the last CPU render
+        if (launches) *launches = 1;
+        return mrt_cpu_last_ms(s->cpu, path_ms, nullptr);
+    }
     HIPCHK(hipSetDevice(s->device));
     float total = 0;
     for (uint32_t k = 0; k < s->n_launch; k++) {

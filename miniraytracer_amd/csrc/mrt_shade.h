@@ -5,7 +5,7 @@
 namespace mrtd {
 
 // perlin_noise::noise / turbulence (texture.cpp:68-165)
-__device__ __forceinline__ float perlin_noise(const DScene& S, f3 p) {
+MRT_DFN float perlin_noise(const DScene& S, f3 p) {
     float fx = floorf(p.x), fy = floorf(p.y), fz = floorf(p.z);
     float u = p.x - fx, v = p.y - fy, w = p.z - fz;
     int i = (int)fx, j = (int)fy, k = (int)fz;
@@ -27,7 +27,7 @@ __device__ __forceinline__ float perlin_noise(const DScene& S, f3 p) {
     }
     return acc;
 }
-__device__ __forceinline__ float turbulence(const DScene& S, f3 p) {
+MRT_DFN float turbulence(const DScene& S, f3 p) {
     float acc = 0, weight = 1.0f;
     for (int i = 0; i < 7; i++) {
         acc += weight * perlin_noise(S, p);
@@ -39,7 +39,7 @@ __device__ __forceinline__ float turbulence(const DScene& S, f3 p) {
 
 // texture::sample (texture.h:18-20, 56-62; texture.cpp:7-25, 207-224)
 template <uint32_t F>
-__device__ __forceinline__ f3 tex_sample(const DScene& S, uint32_t t, float u, float v, f3 p) {
+MRT_DFN f3 tex_sample(const DScene& S, uint32_t t, float u, float v, f3 p) {
     for (;;) {
         const mrt_texture& T = S.texs[t];
         if (!(F & FT_TEX)) return f3{T.f[0], T.f[1], T.f[2]};
@@ -72,13 +72,13 @@ __device__ __forceinline__ f3 tex_sample(const DScene& S, uint32_t t, float u, f
 
 // the material's texture at the hit (constant colours come inline with the material)
 template <uint32_t F>
-__device__ __forceinline__ f3 mat_color(const DScene& S, const DMat& M, const HitRec& rec) {
+MRT_DFN f3 mat_color(const DScene& S, const DMat& M, const HitRec& rec) {
     if (!(F & FT_TEX) || (M.flags & DMAT_COLOR)) return f3{M.col[0], M.col[1], M.col[2]};
     return tex_sample<F>(S, M.tex, rec.u, rec.v, rec.p);
 }
 
 // onb(n) * vec (onb.h:19-27)
-__device__ __forceinline__ f3 onb_apply(f3 w, f3 vec) {
+MRT_DFN f3 onb_apply(f3 w, f3 vec) {
     f3 a = fabsf(w.x) > 0.9f ? f3{0, 1, 0} : f3{1, 0, 0};
     f3 v = normalize(cross(w, a));
     f3 u = cross(w, v);
@@ -91,7 +91,7 @@ __device__ __forceinline__ f3 onb_apply(f3 w, f3 vec) {
 struct Draws {
     float v0, v1;
     uint32_t used;
-    __device__ __forceinline__ float next(Pcg& rng) {
+    MRT_DFN float next(Pcg& rng) {
         if (used == 0) { used = 1; return v0; }
         if (used == 1) { used = 2; return v1; }
         return randf(rng);
@@ -101,7 +101,7 @@ struct Draws {
 // biased object pdfs: object_list / xz_rect / sphere pdf_value & pdf_generate
 // (scene_object.h:64-77, rect.cpp:92-107, sphere.cpp:63-78, scene_object.h:24-29)
 template <uint32_t F>
-__device__ __forceinline__ float leaf_pdf_value(const DScene& S, const mrt_node& n, f3 origin, f3 dir, float time) {
+MRT_DFN float leaf_pdf_value(const DScene& S, const mrt_node& n, f3 origin, f3 dir, float time) {
     uint32_t k = MRT_NODE_KIND(n);
     HitRec rec;
     if (k == MRT_K_XZ) {  // xz_rect::pdf_value (rect.cpp:92-102), the hit test branch-free
@@ -130,7 +130,7 @@ __device__ __forceinline__ float leaf_pdf_value(const DScene& S, const mrt_node&
 // object_list::pdf_value over the biased list (scene_object.h:64-70): the leaves are read through
 // the constant address space (uniform index: scalar loads, no node -> children -> node chain)
 template <uint32_t F>
-__device__ __forceinline__ float biased_pdf_value(const DScene& S, f3 origin, f3 dir, float time) {
+MRT_DFN float biased_pdf_value(const DScene& S, f3 origin, f3 dir, float time) {
     const MRT_CONST_AS mrt_node* bl = const_ptr(S.bleaf);
     if (!S.blist) {
         const mrt_node n = ld_node(bl);
@@ -144,7 +144,7 @@ __device__ __forceinline__ float biased_pdf_value(const DScene& S, f3 origin, f3
     return sum / (float)S.nbleaf;
 }
 template <uint32_t F>
-__device__ __forceinline__ f3 leaf_pdf_generate(const DScene& S, const mrt_node& n, f3 origin, float time, Pcg& rng, Draws& dr) {
+MRT_DFN f3 leaf_pdf_generate(const DScene& S, const mrt_node& n, f3 origin, float time, Pcg& rng, Draws& dr) {
     uint32_t k = MRT_NODE_KIND(n);
     if (k == MRT_K_XZ) {
         float a = dr.next(rng);
@@ -163,7 +163,7 @@ __device__ __forceinline__ f3 leaf_pdf_generate(const DScene& S, const mrt_node&
     return f3{1, 0, 0};
 }
 template <uint32_t F>
-__device__ __forceinline__ f3 biased_pdf_generate(const DScene& S, f3 origin, float time, Pcg& rng, Draws& dr) {
+MRT_DFN f3 biased_pdf_generate(const DScene& S, f3 origin, float time, Pcg& rng, Draws& dr) {
     if (!S.blist) {
         const mrt_node n = ld_node(const_ptr(S.bleaf));
         return leaf_pdf_generate<F>(S, n, origin, time, rng, dr);
@@ -210,7 +210,7 @@ struct LevStore {
     uint32_t lds_base;        // uniform: LDS byte address of this wave's level 0 row (64 float4)
     // this lane's first LDS slot, formed at use from the lane id (a per-lane pointer kept live
     // across the path loop was spilled)
-    __device__ __forceinline__ MRT_LDS_AS v4f* lds() const {
+    MRT_DFN MRT_LDS_AS v4f* lds() const {
 #if defined(__HIP_DEVICE_COMPILE__)
         const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 #else
@@ -218,19 +218,19 @@ struct LevStore {
 #endif
         return (MRT_LDS_AS v4f*)(uintptr_t)(lds_base + lane * 16u);
     }
-    __device__ __forceinline__ MRT_GLOBAL_AS v4f* g() const {
+    MRT_DFN MRT_GLOBAL_AS v4f* g() const {
         uint32_t sl = slot;
 #if defined(__HIP_DEVICE_COMPILE__)
         asm volatile("" : "+v"(sl));  // keeps the address from being hoisted out of the loop
 #endif
         return base + (uint64_t)sl * rows;
     }
-    __device__ __forceinline__ void put(uint32_t d, float4 v) const {
+    MRT_DFN void put(uint32_t d, float4 v) const {
         const v4f w = {v.x, v.y, v.z, v.w};
         if (LK > 0 && d < LK) lds()[d * 64] = w;
         else g()[d] = w;
     }
-    __device__ __forceinline__ float4 get(uint32_t d) const {
+    MRT_DFN float4 get(uint32_t d) const {
         v4f w;
         if (LK > 0 && d < LK) w = lds()[d * 64];
         else w = g()[d];
@@ -239,7 +239,7 @@ struct LevStore {
 };
 // A level is quiet when folding +0 through it gives +0 exactly: finite factors, for diffuse a
 // pdf > 0 (0 + (a * 0) / pdf == +0), for metal non-negative factors (att * +0 == +0).
-__device__ __forceinline__ bool quiet_level(float4 v) {
+MRT_DFN bool quiet_level(float4 v) {
     const bool fin = isfinite(v.x) && isfinite(v.y) && isfinite(v.z);
     if (v.w < 0.0f) return fin & (((__float_as_uint(v.x) | __float_as_uint(v.y) | __float_as_uint(v.z)) >> 31) == 0);
     return fin & (v.w > 0.0f) & isfinite(v.w);
@@ -248,7 +248,7 @@ __device__ __forceinline__ bool quiet_level(float4 v) {
 // One bounce's level (a, pdf; pdf < 0: metal, L = a*L): stored for the deepest-first fold, or
 // (forward fold) multiplied into the path's throughput.
 template <uint32_t LK>
-__device__ __forceinline__ void push_level(PathState& ps, const LevStore<LK>& lev, float4 lv) {
+MRT_DFN void push_level(PathState& ps, const LevStore<LK>& lev, float4 lv) {
 #if MRT_FWD_FOLD
     (void)lev;
     if (lv.w < 0.0f) ps.T = f3{ps.T.x * lv.x, ps.T.y * lv.y, ps.T.z * lv.z};
@@ -260,12 +260,14 @@ __device__ __forceinline__ void push_level(PathState& ps, const LevStore<LK>& le
 }
 
 // camera::get_ray (camera.h:38-44)
-__device__ __forceinline__ Ray camera_ray(const DScene& S, Pcg& rng, float s, float t) {
+MRT_DFN Ray camera_ray(const DScene& S, Pcg& rng, float s, float t) {
     // through a pointer the compiler cannot prove loop-invariant: the camera is re-read (scalar
     // loads, constant cache) at each path start instead of being held in ~40 SGPRs across the
     // path loop, where it spilled to VGPR lanes and cost a v_readlane per use
     const MRT_CONST_AS mrt_camera* cp = const_ptr(S.camp);
+#if defined(__HIP_DEVICE_COMPILE__)
     asm volatile("" : "+s"(cp));
+#endif
     const MRT_CONST_AS mrt_camera& C = *cp;
     f3 rd = fmul(C.lens_radius, random_in_disk(rng));
     f3 offset = add(mulf(ld3(C.u), rd.x), mulf(ld3(C.v), rd.y));
@@ -278,9 +280,11 @@ __device__ __forceinline__ Ray camera_ray(const DScene& S, Pcg& rng, float s, fl
 // camera::get_ray without the ray constructor: origin, direction argument and time of the ray
 // (the constructor -- normalize, 1/dir, dirMask -- runs once per iteration for every lane that
 // has a new ray, see PendRay)
-__device__ __forceinline__ void camera_ray_args(const DScene& S, Pcg& rng, float s, float t, f3* o, f3* dir, float* time) {
+MRT_DFN void camera_ray_args(const DScene& S, Pcg& rng, float s, float t, f3* o, f3* dir, float* time) {
     const MRT_CONST_AS mrt_camera* cp = const_ptr(S.camp);
+#if defined(__HIP_DEVICE_COMPILE__)
     asm volatile("" : "+s"(cp));
+#endif
     const MRT_CONST_AS mrt_camera& C = *cp;
     f3 rd = fmul(C.lens_radius, random_in_disk(rng));
     f3 offset = add(mulf(ld3(C.u), rd.x), mulf(ld3(C.v), rd.y));
@@ -294,7 +298,7 @@ __device__ __forceinline__ void camera_ray_args(const DScene& S, Pcg& rng, float
 // limit, material::scatter and the next ray.  Returns true when the path has ended; its radiance
 // is then in *L.
 template <uint32_t F, uint32_t LK>
-__device__ __forceinline__ bool shade_hit(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev, bool hit,
+MRT_DFN bool shade_hit(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev, bool hit,
                                           const HitRec& rec, f3* L, PhaseClock& ph) {
     Ray& r = ps.r;
     if (!hit) {
@@ -400,7 +404,7 @@ __device__ __forceinline__ bool shade_hit(const DScene& S, PathState& ps, uint32
 
 // One segment.  Returns true when the path has ended; its radiance is then in *L.
 template <uint32_t F, uint32_t LK>
-__device__ __forceinline__ bool trace_segment(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev,
+MRT_DFN bool trace_segment(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev,
                                               const LStack& Ls, f3* L, PhaseClock& ph) {
     ps.rays++;
     HitRec rec;
@@ -426,7 +430,7 @@ struct PendRay {
 // trace_segment up to the next ray's constructor arguments.  Returns true when the path has
 // ended (radiance in *L); otherwise *pr holds the next ray's arguments.
 template <uint32_t F, uint32_t LK>
-__device__ __forceinline__ bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev,
+MRT_DFN bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev,
                                             const LStack& Ls, f3* L, PendRay* pr, PhaseClock& ph) {
     ps.rays++;
     HitRec rec;
@@ -524,7 +528,7 @@ __device__ __forceinline__ bool trace_split(const DScene& S, PathState& ps, uint
 
 // the rest of a diffuse scatter once ps.r = make_ray(pr): mix_pdf value (main.cpp:84-102), level
 template <uint32_t F, uint32_t LK>
-__device__ __forceinline__ void finish_scatter(const DScene& S, PathState& ps, const LevStore<LK>& lev, const PendRay& pr) {
+MRT_DFN void finish_scatter(const DScene& S, PathState& ps, const LevStore<LK>& lev, const PendRay& pr) {
     const Ray& sc = ps.r;
     float sval, spdf;
     if (pr.kind == 1u) {
@@ -545,12 +549,12 @@ __device__ __forceinline__ void finish_scatter(const DScene& S, PathState& ps, c
 
 // the recursion's return path, deepest level first; the lane's levels are contiguous, so they
 // are fetched four at a time (one or two cache lines) instead of one dependent load per level
-__device__ __forceinline__ f3 fold_level(float4 a, f3 L) {
+MRT_DFN f3 fold_level(float4 a, f3 L) {
     if (a.w < 0.0f) return f3{a.x * L.x, a.y * L.y, a.z * L.z};
     return f3{0.0f + ((a.x * L.x) / a.w), 0.0f + ((a.y * L.y) / a.w), 0.0f + ((a.z * L.z) / a.w)};
 }
 template <uint32_t LK>
-__device__ __forceinline__ f3 fold_levels(const LevStore<LK>& lev, uint32_t nlev, f3 L) {
+MRT_DFN f3 fold_levels(const LevStore<LK>& lev, uint32_t nlev, f3 L) {
     // a black end through quiet levels stays +0 (the common escaped path): nothing to fold
     if (!(nlev & LEV_LOUD) && ((__float_as_uint(L.x) | __float_as_uint(L.y) | __float_as_uint(L.z)) == 0)) return L;
     int d = (int)(nlev & ~LEV_LOUD) - 1;
@@ -574,13 +578,39 @@ __device__ __forceinline__ f3 fold_levels(const LevStore<LK>& lev, uint32_t nlev
 }
 // a path's radiance from its end's emitted (or sky / black) L
 template <uint32_t LK>
-__device__ __forceinline__ f3 end_path(const PathState& ps, const LevStore<LK>& lev, f3 L) {
+MRT_DFN f3 end_path(const PathState& ps, const LevStore<LK>& lev, f3 L) {
 #if MRT_FWD_FOLD
     (void)lev;
     return f3{ps.T.x * L.x, ps.T.y * L.y, ps.T.z * L.z};
 #else
     return fold_levels(lev, ps.nlev, L);
 #endif
+}
+
+// ---- draw() / draw2()'s per-pixel accumulation (main.cpp:150-175, 205-231), both backends ----
+MRT_DFN float lum3(f3 c) { return (c.x * 0.212655f + c.y * 0.715158f) + c.z * 0.072187f; }
+
+// one sample of draw()/draw2()'s per-pixel loop
+MRT_DFN f3 fold_sample(f3 c, f3 smp, uint32_t s, uint32_t mode, float max_lum) {
+    if (mode == 0) {
+        if (!finite3(smp)) smp = c;
+        return add(c, smp);
+    }
+    if (!finite3(smp)) smp = s > 0 ? c : f3{0, 0, 0};
+    if (s > 0) smp = add(c, mulf(sub(smp, c), 1.0f / ((float)s + 1.0f)));
+    float l = lum3(smp);
+    if (l > max_lum) smp = mulf(smp, max_lum / l);
+    return smp;
+}
+// the pixel after its last sample: mode 0 divides by the sample count and clamps the luminance
+// (main.cpp:168-173); mode 1's running average is final as it is
+MRT_DFN f3 final_pixel(f3 c, uint32_t ns, uint32_t mode, float max_lum) {
+    if (mode == 0) {
+        c = divf(c, (float)ns);
+        float l = lum3(c);
+        if (l > max_lum) c = mulf(c, max_lum / l);
+    }
+    return c;
 }
 
 }  // namespace mrtd

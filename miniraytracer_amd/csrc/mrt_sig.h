@@ -74,7 +74,7 @@ struct SigWalk {
 
     // ops [PC, END) of the program, lanes `on` taking part
     template <uint32_t PC, uint32_t END>
-    __device__ static __forceinline__ void run(const DScene& S, const MRT_CONST_AS LinOp* prog, float tmin, SigState& w, bool on,
+    MRT_DATTR static __forceinline__ void run(const DScene& S, const MRT_CONST_AS LinOp* prog, float tmin, SigState& w, bool on,
                                                HitRec& rec, const LStack& L) {
         if constexpr (PC < END) {
             constexpr uint32_t op = G.op[PC];
@@ -111,7 +111,7 @@ struct SigWalk {
             } else if constexpr (op == LOP_LIST) {  // object_list::hit box reject (scene_object.h:83)
                 constexpr uint32_t skip = G.skip[PC];
                 const bool in = on && (!(LOP_FLAGS(o) & MRT_F_HASBOX) || lin_box(o, w.cur, tmin, w.closest));
-                if (__any(in)) run<PC + 1, skip>(S, prog, tmin, w, in, rec, L);
+                if (any_lane(in)) run<PC + 1, skip>(S, prog, tmin, w, in, rec, L);
                 run<skip + 1, END>(S, prog, tmin, w, on, rec, L);
             } else if constexpr (op == LOP_INST) {  // scene_object.cpp:9-18, 70-98
                 constexpr uint32_t skip = G.skip[PC];
@@ -124,7 +124,7 @@ struct SigWalk {
                     w.cur = r0;
                     if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, w.cur, tmin, w.closest);
                 }
-                if (__any(in)) {
+                if (any_lane(in)) {
                     if constexpr (kind == MRT_K_TRROTY || kind == MRT_K_ROTY) w.cur = rotate_ray(w.cur, o.f[6], o.f[7]);
                     else w.cur = moved_ray(r0, sub(r0.o, f3{o.f[0], o.f[1], o.f[2]}));
                     run<PC + 1, skip>(S, prog, tmin, w, in, rec, L);
@@ -145,11 +145,11 @@ struct SigWalk {
     // the record of the closest hit, op by op: for each primitive op some lane hit, that op's
     // data by scalar loads and its compile-time kind (no per-lane node loads or kind switch)
     template <uint32_t PC>
-    __device__ static __forceinline__ void derive(const MRT_CONST_AS LinOp* prog, const SigState& w, const Ray& r, const Ray& ir,
+    MRT_DATTR static __forceinline__ void derive(const MRT_CONST_AS LinOp* prog, const SigState& w, const Ray& r, const Ray& ir,
                                                   HitRec& rec) {
         if constexpr (PC < G.n) {
             if constexpr (G.op[PC] == LOP_PRIM) {
-                if (__any(w.hnode == PC)) {
+                if (any_lane(w.hnode == PC)) {
                     if (w.hnode == PC) lin_prim_rec_op<F, G.kind[PC]>(prog[PC], cur_inst<PC>() != MRT_NONE ? ir : r, w.closest, rec);
                 }
             }
@@ -157,7 +157,7 @@ struct SigWalk {
         }
     }
     // the program's only instance op (MRT_NONE if it has none or several)
-    __device__ static constexpr uint32_t only_inst() {
+    MRT_DATTR static constexpr uint32_t only_inst() {
         uint32_t found = MRT_NONE, count = 0;
         for (uint32_t i = 0; i < G.n; i++)
             if (G.op[i] == LOP_INST) { found = i; count++; }
@@ -165,7 +165,7 @@ struct SigWalk {
     }
     // op index of the instance enclosing op PC (MRT_NONE: world frame)
     template <uint32_t PC>
-    __device__ static constexpr uint32_t cur_inst() {
+    MRT_DATTR static constexpr uint32_t cur_inst() {
         uint32_t found = MRT_NONE;
         for (uint32_t i = 0; i < PC; i++)
             if (G.op[i] == LOP_INST && G.skip[i] > PC) found = i;
@@ -175,7 +175,7 @@ struct SigWalk {
 
 // scene_object::hit for a program of shape SIG (same contract as scene_hit_lin)
 template <uint32_t F>
-__device__ __forceinline__ bool scene_hit_sig(const DScene& S, Ray& r, float tmin, HitRec& rec, const LStack& L) {
+MRT_DFN bool scene_hit_sig(const DScene& S, Ray& r, float tmin, HitRec& rec, const LStack& L) {
     constexpr uint32_t SIG = MRT_SIG_OF(F);
     constexpr bool INST = (F & FT_INST) != 0;
     if (INST) lin_save_ray(L, r);
@@ -191,7 +191,7 @@ __device__ __forceinline__ bool scene_hit_sig(const DScene& S, Ray& r, float tmi
     if (w.hnode == MRT_NONE) return false;
     if constexpr (SigWalk<F, SIG>::kDerive) {
         Ray ir = r;
-        if (INST && __any(w.hinst != MRT_NONE && !w.hdone)) {  // instance-frame ray of the hit (LDS)
+        if (INST && any_lane(w.hinst != MRT_NONE && !w.hdone)) {  // instance-frame ray of the hit (LDS)
             const float* b = L.save + L.lane + 9 * 64;
             ir.o = f3{b[0], b[64], b[128]};
             ir.d = f3{b[192], b[256], b[320]};

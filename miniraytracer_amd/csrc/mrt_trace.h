@@ -60,7 +60,7 @@ struct WideNode {
     uint32_t lref, rref, order, flags;
 };
 template <typename W>
-__device__ __forceinline__ WideNode load_wide(const W* p) {
+MRT_DFN WideNode load_wide(const W* p) {
     static_assert(sizeof(W) == 64, "wide node is 64 B");
     const float4* q = reinterpret_cast<const float4*>(p);
     const float4 a = q[0], b = q[1], c = q[2], d = q[3];
@@ -79,7 +79,7 @@ __device__ __forceinline__ WideNode load_wide(const W* p) {
 // The same from any address space: with a treelet (MRT_TREELET) the top wide nodes of the scene's
 // BVHs are copied into the workgroup's LDS at kernel start, and a node ref below the treelet size
 // reads there -- one flat load per 16 B that the hardware routes to LDS or memory per lane.
-__device__ __forceinline__ WideNode load_wide_q(const float4* q) {
+MRT_DFN WideNode load_wide_q(const float4* q) {
     const float4 a = q[0], b = q[1], c = q[2], d = q[3];
     WideNode n;
     n.lmin = f3{a.x, a.y, a.z};
@@ -94,7 +94,7 @@ __device__ __forceinline__ WideNode load_wide_q(const float4* q) {
 }
 
 // a node record read through the constant address space (scalar loads at a uniform address)
-__device__ __forceinline__ mrt_node ld_node(const MRT_CONST_AS mrt_node* p) {
+MRT_DFN mrt_node ld_node(const MRT_CONST_AS mrt_node* p) {
     mrt_node n;
     n.kind = p->kind;
     n.a = p->a;
@@ -105,7 +105,7 @@ __device__ __forceinline__ mrt_node ld_node(const MRT_CONST_AS mrt_node* p) {
 }
 
 // a per-lane node record fetched whole (four 16-byte loads in flight together)
-__device__ __forceinline__ mrt_node ld_node_v(const mrt_node* p) {
+MRT_DFN mrt_node ld_node_v(const mrt_node* p) {
     const float4* q = reinterpret_cast<const float4*>(p);
     const float4 a = q[0], b = q[1], c = q[2], d = q[3];
     mrt_node n;
@@ -200,7 +200,7 @@ struct TreeOf {
 };
 // wide node `ref` of a BvhWide / MeshWide array: from the LDS treelet when it holds it
 template <bool TREE, typename W>
-__device__ __forceinline__ WideNode wide_at(const W* base, uint32_t ref, const LStack& L) {
+MRT_DFN WideNode wide_at(const W* base, uint32_t ref, const LStack& L) {
     if constexpr (TREE) {
         const float4* q = ref < L.tree_b ? L.tree + (size_t)ref * 4 : reinterpret_cast<const float4*>(base + ref);
         return load_wide_q(q);
@@ -211,13 +211,13 @@ __device__ __forceinline__ WideNode wide_at(const W* base, uint32_t ref, const L
 }
 
 template <uint32_t F>
-__device__ __forceinline__ bool is_prim(uint32_t kind) {
+MRT_DFN bool is_prim(uint32_t kind) {
     return kind == MRT_K_SPHERE || kind == MRT_K_XY || kind == MRT_K_XZ || kind == MRT_K_YZ || ((F & FT_MESH) && kind == MRT_K_MESH) ||
            ((F & FT_BVHW) && kind == MRT_K_BVHW);
 }
 
 // get_sphere_uv (sphere.cpp:6-11)
-__device__ __forceinline__ void sphere_uv(f3 p, float* u, float* v) {
+MRT_DFN void sphere_uv(f3 p, float* u, float* v) {
     float phi = atan2_(p.z, p.x);
     float theta = asin_(p.y);
     *u = 0.5f - phi * (1.0f / (2.0f * PI_F));
@@ -225,7 +225,7 @@ __device__ __forceinline__ void sphere_uv(f3 p, float* u, float* v) {
 }
 
 template <uint32_t F>
-__device__ __forceinline__ f3 sphere_center(const mrt_node& n, float time) {
+MRT_DFN f3 sphere_center(const mrt_node& n, float time) {
     f3 c0 = ld3(n.f);
     if ((F & FT_MOVING) && (MRT_NODE_FLAGS(n) & MRT_F_MOVING))
         return add(c0, fmul((time - n.f[6]) / (n.f[7] - n.f[6]), sub(ld3(n.f + 3), c0)));
@@ -234,7 +234,7 @@ __device__ __forceinline__ f3 sphere_center(const mrt_node& n, float time) {
 
 // sphere::hit (sphere.cpp:13-46).  `full` = write p/n/uv (false inside volume boundary queries).
 template <uint32_t F>
-__device__ __forceinline__ bool sphere_hit(const mrt_node& n, const Ray& r, float tmin, float tmax, HitRec& rec, bool full) {
+MRT_DFN bool sphere_hit(const mrt_node& n, const Ray& r, float tmin, float tmax, HitRec& rec, bool full) {
     f3 cen = sphere_center<F>(n, r.time);
     float radius = n.f[8];
     f3 oc = sub(r.o, cen);
@@ -264,7 +264,7 @@ __device__ __forceinline__ bool sphere_hit(const mrt_node& n, const Ray& r, floa
 
 // xy/xz/yz_rect::hit (rect.cpp:24-152); AX = plane axis (2: xy, 1: xz, 0: yz)
 template <uint32_t F, int AX>
-__device__ __forceinline__ bool rect_hit(const mrt_node& n, const Ray& r, float tmin, float tmax, HitRec& rec, bool full) {
+MRT_DFN bool rect_hit(const mrt_node& n, const Ray& r, float tmin, float tmax, HitRec& rec, bool full) {
     const float ns = n.f[5];
     // dot(r.dir, normal) with the zero lanes kept (NaN directions behave as in the reference)
     float dn = AX == 2 ? (r.d.x * 0.0f + r.d.y * 0.0f) + r.d.z * ns
@@ -299,7 +299,7 @@ __device__ __forceinline__ bool rect_hit(const mrt_node& n, const Ray& r, float 
 }
 
 // triangle::hit (triangle.cpp:222-265) without the normal (deferred to the closest hit)
-__device__ __forceinline__ bool tri_hit(const DScene& S, uint32_t i, const Ray& r, float tmin, float tmax, float* tout, float* uout, float* vout) {
+MRT_DFN bool tri_hit(const DScene& S, uint32_t i, const Ray& r, float tmin, float tmax, float* tout, float* uout, float* vout) {
     const float4* g = S.tri_geo + (size_t)i * 3;
     f3 m = ld3(g[0]), u = ld3(g[1]), v = ld3(g[2]);
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -334,7 +334,7 @@ __device__ __forceinline__ bool tri_hit(const DScene& S, uint32_t i, const Ray& 
 // Both children's boxes are tested when their parent is reached -- with the same (tmin, tmax) the
 // reference uses when it visits them, since nothing narrows tmax before the walk ends -- and only
 // a farther child whose box was hit is pushed (short stack in LDS).  n.a = root node, n.b = root ref.
-__device__ __forceinline__ bool mesh_leaf(const DScene& S, uint32_t ref, const mrt_node& n, const Ray& r, float tmin, float tmax, HitRec& rec,
+MRT_DFN bool mesh_leaf(const DScene& S, uint32_t ref, const mrt_node& n, const Ray& r, float tmin, float tmax, HitRec& rec,
                                           bool full) {
     const uint32_t first = ref & 0xFFFFFFu, cnt = (ref >> 24) & 0x7Fu;
     bool has = false;
@@ -367,7 +367,7 @@ __device__ __forceinline__ bool mesh_leaf(const DScene& S, uint32_t ref, const m
 // UNIFORM: the mesh node is the same for the whole wave (linear programs): the root box is read
 // through the constant address space (scalar loads) instead of by a per-lane load chain.
 template <bool UNIFORM = false>
-__device__ __forceinline__ bool mesh_hit(const DScene& S, const mrt_node& n, const Ray& r, float tmin, float tmax, HitRec& rec, bool full,
+MRT_DFN bool mesh_hit(const DScene& S, const mrt_node& n, const Ray& r, float tmin, float tmax, HitRec& rec, bool full,
                                          const LStack& L) {
     if constexpr (UNIFORM) {
         const MRT_CONST_AS mrt_mesh_node& root = const_ptr(S.mnodes)[n.a];
@@ -436,7 +436,7 @@ __device__ __forceinline__ bool mesh_hit(const DScene& S, const mrt_node& n, con
 // triangles) and lanes at inner nodes cost about the same per step.  Returns 0: keep walking,
 // 1: hit (rec complete, tt = its t; the walk is over: first-hit early-out), 2: no hit.  Every lane
 // performs mesh_hit's operations in mesh_hit's order: the results are bit-identical.
-__device__ __forceinline__ uint32_t mesh_step(const DScene& S, const mrt_node& n, const Ray& r, float tmin, float& tt, HitRec& rec,
+MRT_DFN uint32_t mesh_step(const DScene& S, const mrt_node& n, const Ray& r, float tmin, float& tt, HitRec& rec,
                                               const LStack& L, uint32_t& ref, uint32_t& msp, bool& in_hit) {
     if (ref & MESH_LEAF) {
         const uint32_t first = ref & 0xFFFFFFu, cnt = (ref >> 24) & 0x7Fu;
@@ -486,7 +486,7 @@ __device__ __forceinline__ uint32_t mesh_step(const DScene& S, const mrt_node& n
 }
 
 template <uint32_t F>
-__device__ __forceinline__ bool leaf_prim_hit(const mrt_node& n, uint32_t kind, const Ray& r, float tmin, float tmax, HitRec& rec, bool full) {
+MRT_DFN bool leaf_prim_hit(const mrt_node& n, uint32_t kind, const Ray& r, float tmin, float tmax, HitRec& rec, bool full) {
     switch (kind) {
     case MRT_K_SPHERE: return sphere_hit<F>(n, r, tmin, tmax, rec, full);
     case MRT_K_XY: return rect_hit<F, 2>(n, r, tmin, tmax, rec, full);
@@ -500,7 +500,7 @@ __device__ __forceinline__ bool leaf_prim_hit(const mrt_node& n, uint32_t kind, 
 // the running closest narrowing across children (scene_object.h:79-103).  The leaf is a run of
 // node records (BVHW_LEAF ref); a nested list's record carries its box and child count.
 template <uint32_t F>
-__device__ __forceinline__ bool bvhw_leaf(const DScene& S, uint32_t ref, const Ray& r, float tmin, float tmax, HitRec& rec, bool full) {
+MRT_DFN bool bvhw_leaf(const DScene& S, uint32_t ref, const Ray& r, float tmin, float tmax, HitRec& rec, bool full) {
     const uint32_t first = ref & BVHW_FIRST_MASK, cnt = (ref >> 24) & BVHW_MAX_RUN;
     const mrt_node* run = S.bprims + first;
     if (cnt == 1) {  // a primitive leaf (or a list of one): hit() with the bvh_node's (tmin, tmax)
@@ -531,7 +531,7 @@ __device__ __forceinline__ bool bvhw_leaf(const DScene& S, uint32_t ref, const R
 // it; only a farther child whose box was hit is pushed (short stack in LDS, shared with meshes).
 // n.a = root ref, n.f[0..5] = the root bvh_node's box.
 template <uint32_t F>
-__device__ __forceinline__ bool bvhw_hit(const DScene& S, const mrt_node& n, const Ray& r, float tmin, float tmax, HitRec& rec, bool full,
+MRT_DFN bool bvhw_hit(const DScene& S, const mrt_node& n, const Ray& r, float tmin, float tmax, HitRec& rec, bool full,
                                          const LStack& L) {
     if (!aabb_hit(n.f, n.f + 3, r, tmin, tmax)) return false;
     uint32_t ref = n.a, sp = 0;
@@ -590,7 +590,7 @@ __device__ __forceinline__ bool bvhw_hit(const DScene& S, const mrt_node& n, con
 }
 
 template <uint32_t F>
-__device__ __forceinline__ bool prim_hit(const DScene& S, const mrt_node& n, uint32_t kind, const Ray& r, float tmin, float tmax, HitRec& rec,
+MRT_DFN bool prim_hit(const DScene& S, const mrt_node& n, uint32_t kind, const Ray& r, float tmin, float tmax, HitRec& rec,
                                          bool full, const LStack& L) {
     switch (kind) {
     case MRT_K_SPHERE: return sphere_hit<F>(n, r, tmin, tmax, rec, full);
@@ -605,7 +605,7 @@ __device__ __forceinline__ bool prim_hit(const DScene& S, const mrt_node& n, uin
     }
 }
 
-__device__ __forceinline__ void push_ray(const LStack& L, uint32_t slot, const Ray& r) {
+MRT_DFN void push_ray(const LStack& L, uint32_t slot, const Ray& r) {
     float* b = L.rays + slot * 11 * 64 + L.lane;
     b[0] = r.o.x; b[64] = r.o.y; b[128] = r.o.z;
     b[192] = r.d.x; b[256] = r.d.y; b[320] = r.d.z;
@@ -613,7 +613,7 @@ __device__ __forceinline__ void push_ray(const LStack& L, uint32_t slot, const R
     b[576] = __int_as_float(r.inside);
     b[640] = __uint_as_float(r.mask | ((uint32_t)r.nice << 31));
 }
-__device__ __forceinline__ void pop_ray(const LStack& L, uint32_t slot, Ray& r) {
+MRT_DFN void pop_ray(const LStack& L, uint32_t slot, Ray& r) {
     const float* b = L.rays + slot * 11 * 64 + L.lane;
     r.o = f3{b[0], b[64], b[128]};
     r.d = f3{b[192], b[256], b[320]};
@@ -625,7 +625,7 @@ __device__ __forceinline__ void pop_ray(const LStack& L, uint32_t slot, Ray& r) 
 }
 
 // rotate_y::hit ray transform (scene_object.cpp:75-82)
-__device__ __forceinline__ Ray rotate_ray(const Ray& ray, float s, float c) {
+MRT_DFN Ray rotate_ray(const Ray& ray, float s, float c) {
     f3 o = ray.o, d = ray.d;
     o.x = c * ray.o.x - s * ray.o.z;
     o.z = c * ray.o.z + s * ray.o.x;
@@ -634,7 +634,7 @@ __device__ __forceinline__ Ray rotate_ray(const Ray& ray, float s, float c) {
     return make_ray_unit(o, d, ray.time, 0);
 }
 // ... and the record back (scene_object.cpp:85-93)
-__device__ __forceinline__ void unrotate_rec(HitRec& rec, float s, float c) {
+MRT_DFN void unrotate_rec(HitRec& rec, float s, float c) {
     f3 p = rec.p, nn = rec.n;
     p.x = c * rec.p.x + s * rec.p.z;
     p.z = c * rec.p.z - s * rec.p.x;
@@ -655,7 +655,7 @@ __device__ __forceinline__ void unrotate_rec(HitRec& rec, float s, float c) {
 enum : uint32_t { ST_ENTER = 0xFFFFFFFFu, ST_PH1 = 0x40000000u, ST_PH2 = 0x40000001u };
 
 template <uint32_t F>
-__device__ __forceinline__ bool scene_hit(const DScene& S, Ray ray, float tmin0, HitRec& rec, Pcg& rng, const LStack& L) {
+MRT_DFN bool scene_hit(const DScene& S, Ray ray, float tmin0, HitRec& rec, Pcg& rng, const LStack& L) {
     uint32_t depth = 0, rsp = 0;
     uint32_t tnode = 0, tstate = 0;  // top frame
     float closest = FLT_MAX_, tmin = tmin0;

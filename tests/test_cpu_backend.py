@@ -1,0 +1,102 @@
+"""CPU backend (libmrt.so, mrt_scene_upload(MRT_DEVICE_CPU)): the hot-path headers compiled for the
+host (miniraytracer_amd/csrc/mrt_cpu.hip) behind the same C-ABI as the GPU path.
+
+Bar: bit-exact.  Images and ray totals equal the reference's own trace() (stream-matched fixtures
+made from oracle/_ref/mrt_ref_exact: the reference's sources built exact, with the project's
+transcendentals, tests/golden/stream_*.npz) and the C restatement (oracle/), float bits included.
+These tests need no GPU: they are the product's hot-path code checked on the CPU."""
+import os
+import subprocess
+import threading
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, golden_stream
+
+STREAMS = [f"stream_{s}.npz" for s in range(10)] + ["stream_5_mode1.npz"]
+_scenes = {}
+
+
+def cpu_renderer(mrt, sid, w, h):
+    key = (sid, w / h)
+    if key not in _scenes:
+        sc = mrt.select_scene(sid, w / h)
+        _scenes[key] = (sc, mrt.Renderer(sc, "cpu"))
+    return _scenes[key]
+
+
+@pytest.mark.parametrize("name", STREAMS)
+def test_cpu_backend_matches_reference_fixture(mrt, name):
+    g = golden_stream(name)
+    _, r = cpu_renderer(mrt, g["sid"], g["w"], g["h"])
+    img, rays = r.render(mrt.render_desc(g["w"], g["h"], g["spp"], depth=g["depth"], mode=g["mode"], threads=3))
+    assert rays == g["rays"]
+    assert np.array_equal(img[..., :3].view(np.uint32), g["image"].view(np.uint32))
+
+
+@pytest.mark.parametrize("sid,w,h,spp,depth,mode", [(0, 200, 100, 16, 8, 1), (5, 48, 40, 16, 32, 0), (7, 24, 24, 4, 32, 1),
+                                                    (8, 24, 24, 4, 32, 0), (6, 24, 24, 4, 32, 1), (9, 24, 24, 4, 32, 0)])
+def test_cpu_backend_matches_c_restatement(mrt, orc, sid, w, h, spp, depth, mode):
+    """Config C1 (scene 0, 200x100, 16 spp, depth 8: the reference's CPU work_queue case) and
+    ragged / mode-1 renders of the other scene kinds: the CPU backend == the C restatement."""
+    sc, r = cpu_renderer(mrt, sid, w, h)
+    img, rays = r.render(mrt.render_desc(w, h, spp, depth=depth, mode=mode, tile_size=7))
+    oimg, orays, _, _ = orc.render(sc, orc.desc(w, h, spp, depth=depth, mode=mode, threads=4))
+    assert rays == orays
+    assert np.array_equal(img, oimg)
+
+
+def test_cpu_backend_independent_of_threads_and_ranks(mrt):
+    """Per-path stream keys: 1 thread, 5 threads and two rank shards (tile k -> rank k % 2)
+    assembled give the same image bit for bit."""
+    sc, r = cpu_renderer(mrt, 5, 40, 24)
+    a, ra = r.render(mrt.render_desc(40, 24, 9, tile_size=8, threads=1))
+    b, rb = r.render(mrt.render_desc(40, 24, 9, tile_size=8, threads=5))
+    assert ra == rb and np.array_equal(a, b)
+    full = np.zeros_like(a)
+    total = 0
+    for rank in range(2):
+        d = mrt.render_desc(40, 24, 9, tile_size=8, rank=rank, world=2, threads=2)
+        part, rr = r.render(d)
+        px = mrt.local_pixels(d)
+        full.reshape(-1, 4)[px] = part.reshape(-1, 4)[px]
+        total += rr
+    assert total == ra and np.array_equal(full, a)
+
+
+def test_cpu_backend_progress_cancel_and_gpu_only_calls(mrt):
+    sc, r = cpu_renderer(mrt, 0, 64, 32)
+    d = mrt.render_desc(64, 32, 16, depth=8, tile_size=8, threads=2)
+    r.render(d)
+    assert r.progress() == pytest.approx(100.0)
+    assert r.kernel_info()["grid"] == 2  # worker threads of the last render
+    flag = __import__("ctypes").c_int(1)
+    with pytest.raises(mrt.MrtError):
+        r.render(d, cancel=flag)
+    # a cancel raised mid-render stops it between tiles (G_isRunning, main.cpp:180)
+    big = mrt.render_desc(200, 100, 256, depth=8, tile_size=8, threads=1)
+    flag.value = 0
+    t = threading.Timer(0.05, lambda: setattr(flag, "value", 1))
+    t.start()
+    with pytest.raises(mrt.MrtError, match="cancel"):
+        r.render(big, cancel=flag)
+    t.join()
+    assert 0.0 < r.progress() < 100.0
+    with pytest.raises(mrt.MrtError):  # GPU-only entry points
+        r.render_device(d, 0, 0)
+    with pytest.raises(mrt.MrtError):  # the CPU backend runs the exact contract only
+        r.render(mrt.render_desc(8, 8, 1, numerics="fast"))
+
+
+def test_cli_cpu_backend_writes_reference_image(mrt, tmp_path):
+    """bin/mrt -backend cpu: the reference's flags (-threads = CPU workers), image == fixture."""
+    g = golden_stream("stream_5.npz")
+    out = tmp_path / "x.pfm"
+    p = subprocess.run([os.path.join(ROOT, "bin", "mrt"), "-backend", "cpu", "-threads", "3", "-scene", "5", "-width", str(g["w"]),
+                        "-height", str(g["h"]), "-samples", str(g["spp"]), "-depth", str(g["depth"]), "-mode", str(g["mode"]),
+                        "-tilesize", "8", "-o", str(out)], capture_output=True, text=True, timeout=120, check=True)
+    assert "CPU, 3 threads" in p.stdout
+    assert int(p.stdout.split("rays ")[-1].split()[0]) == g["rays"]
+    img = mrt.read_pfm(str(out))
+    assert np.array_equal(img.view(np.uint32), g["image"].view(np.uint32))

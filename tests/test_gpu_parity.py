@@ -422,3 +422,15 @@ def test_cli_drop_in_writes_reference_image(gpu, tmp_path):
     bad = subprocess.run([os.path.join(ROOT, "bin", "mrt"), "-scene", "5", "-width", "8", "-height", "8", "-gpus", "64"],
                          capture_output=True, text=True, timeout=120)
     assert bad.returncode != 0
+
+
+@pytest.mark.parametrize("sid,w,h,spp,mode", [(5, 64, 64, 64, 0), (7, 48, 48, 16, 1), (8, 48, 48, 16, 0), (0, 200, 100, 16, 1)])
+def test_gpu_equals_cpu_backend(gpu, sid, w, h, spp, mode):
+    """The two backends of the same hot-path source (the gfx950 path kernel and its host build,
+    MRT_DEVICE_CPU) render the same image bit for bit under the exact contract."""
+    sc, r = renderer(gpu, sid, w, h)
+    d = gpu.render_desc(w, h, spp, mode=mode, depth=8 if sid == 0 else 32)
+    a, ra = r.render(d)
+    b, rb = gpu.Renderer(sc, "cpu").render(d)
+    assert ra == rb
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
