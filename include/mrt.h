@@ -109,6 +109,11 @@ typedef struct mrt_render_desc {
                                   f32 transcendentals; per-pixel RMSE < 1e-3 vs the reference as
                                   shipped (DESIGN.md "Numerics contracts").  Unset: the exact
                                   contract, bit-for-bit the reference built exact. */
+#define MRT_RF_PREVIEW 0x4u    /* keep a progressive preview for mrt_preview: after every launch's
+                                  fold, the running image (mode 1: the running average, draw2();
+                                  mode 0: the mean of the samples so far) is copied to pinned host
+                                  memory in stream order (G_linearBackBuffer as the UI thread reads
+                                  it every 33 ms, main.cpp:387-444) */
 
 void mrt_default_render_desc(const mrt_params* p, mrt_render_desc* d);
 
@@ -131,6 +136,13 @@ mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d);
  * last render made with MRT_RF_PATH_DEBUG (host copies). */
 mrt_status mrt_render_debug(mrt_scene* s, float* path_rgb, uint32_t* path_rays, uint64_t n_paths);
 mrt_status mrt_progress(mrt_scene* s, float* pct);
+/* The newest preview of the running render, callable from another host thread while it runs: the
+ * image after *samples_done samples of every pixel (W*H*4 floats, owned pixels only, as rgb_out of
+ * mrt_render), never a mix of two passes (the snapshot is sequence-locked).  GPU backend: renders
+ * made with MRT_RF_PREVIEW (samples_done = 0 until the first launch is folded); CPU backend: the
+ * framebuffer as far as its tiles are done (every sample of a finished pixel; samples_done = spp
+ * once the render is over, 0 before). */
+mrt_status mrt_preview(mrt_scene* s, float* rgb_out, uint32_t* samples_done);
 /* Device time of the path-kernel launches of the last render (HIP events recorded on the render's
  * stream around each mrt_path_kernel launch); waits for the last one. */
 mrt_status mrt_kernel_ms(mrt_scene* s, float* path_ms, uint32_t* launches);

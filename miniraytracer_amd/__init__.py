@@ -90,7 +90,7 @@ NUMERICS = ("exact", "fast")
 
 
 def render_desc(width, height, samples, depth=32, max_luminance=1000.0, mode=0, seed=MAIN_SEED, tile_size=32,
-                rank=0, world=1, chunk_samples=0, flags=0, numerics="exact", threads=0):
+                rank=0, world=1, chunk_samples=0, flags=0, numerics="exact", threads=0, preview=False):
     """Render description; `samples` is floored to a perfect square like main.cpp:319-320.
     numerics: "exact" (bit-for-bit the reference built exact) or "fast" (tolerance contract:
     per-pixel RMSE < 1e-3 vs the reference as shipped; MRT_RF_FAST)."""
@@ -98,6 +98,8 @@ def render_desc(width, height, samples, depth=32, max_luminance=1000.0, mode=0, 
         raise ValueError(f"numerics must be one of {NUMERICS}")
     if numerics == "fast":
         flags |= _lib.RF_FAST
+    if preview:
+        flags |= _lib.RF_PREVIEW
     sq = int(np.sqrt(np.float32(samples)))
     return MrtRenderDesc(width, height, sq, depth, max_luminance, mode, seed, tile_size, rank, world,
                          chunk_samples, flags, threads)
@@ -151,6 +153,15 @@ class Renderer:
         """Enqueue a render into device memory (torch tensor data_ptr()s) on a HIP stream."""
         check(lib().mrt_render_device(self._h, C.byref(desc), C.c_void_p(d_out_ptr), C.c_void_p(d_rays_ptr),
                                       C.c_void_p(stream_ptr)), "mrt_render_device")
+
+    def preview(self, width, height):
+        """The running render as the reference's UI thread sees G_linearBackBuffer (main.cpp:387-444):
+        (H, W, 4) float32 image after `samples` samples of every pixel, callable from another thread
+        while render() runs.  GPU: renders made with flags=RF_PREVIEW (render_desc(preview=True))."""
+        img = np.zeros((height, width, 4), dtype=np.float32)
+        n = C.c_uint32()
+        check(lib().mrt_preview(self._h, img.ctypes.data, C.byref(n)), "mrt_preview")
+        return img, n.value
 
     def progress(self):
         """Percent of the current / last render's paths handed out (work_queue::getPercentDone)."""

@@ -16,6 +16,7 @@ if os.environ.get("MRT_EXPERIMENT_LIB"):
 MRT_NONE = 0xFFFFFFFF
 RF_PATH_DEBUG = 0x1
 RF_FAST = 0x2  # tolerance numerics contract (include/mrt.h MRT_RF_FAST)
+RF_PREVIEW = 0x4  # keep a progressive preview for mrt_preview (include/mrt.h MRT_RF_PREVIEW)
 DEVICE_CPU = -1  # mrt_scene_upload device of the CPU backend (include/mrt.h MRT_DEVICE_CPU)
 
 
@@ -114,6 +115,8 @@ def lib():
     L.mrt_lum_max_device.restype = st
     L.mrt_tonemap_device.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
     L.mrt_tonemap_device.restype = st
+    L.mrt_preview.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint32)]
+    L.mrt_preview.restype = st
     L.mrt_scene_kernel_info.argtypes = [C.c_void_p, C.POINTER(KernelInfo)]
     L.mrt_scene_kernel_info.restype = st
     L.mrt_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_uint32)]
@@ -144,5 +147,5 @@ EXPORTS = [
     "mrt_scene_upload", "mrt_scene_free", "mrt_default_render_desc", "mrt_local_pixels",
     "mrt_render", "mrt_render_device", "mrt_prepare", "mrt_render_debug", "mrt_progress",
     "mrt_tonemap_argb", "mrt_strerror", "mrt_last_error", "mrt_kernel_ms", "mrt_pack_obj",
-    "mrt_scene_kernel_info", "mrt_lum_max_device", "mrt_tonemap_device", "mrt_worker_seeds",
+    "mrt_scene_kernel_info", "mrt_preview", "mrt_lum_max_device", "mrt_tonemap_device", "mrt_worker_seeds",
 ]

@@ -10,3 +10,4 @@ uint32_t mrt_cpu_scene_features(const mrt_cpu_scene* c);
 mrt_status mrt_cpu_render(mrt_cpu_scene* c, const mrt_render_desc* d, float* rgb_out, uint64_t* rays_out, const volatile int* cancel);
 mrt_status mrt_cpu_progress(mrt_cpu_scene* c, float* pct);
 mrt_status mrt_cpu_last_ms(mrt_cpu_scene* c, float* ms, uint32_t* threads);
+mrt_status mrt_cpu_preview(mrt_cpu_scene* c, float* rgb_out, uint32_t* samples_done);

@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <mutex>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -48,6 +49,12 @@ struct mrt_cpu_scene {
     std::atomic<uint64_t> done{0}, total{0};
     double last_ms = 0;
     uint32_t last_threads = 0;
+    // the framebuffer the workers fill (G_linearBackBuffer): mrt_preview reads it while they run
+    std::vector<float> fb;
+    std::vector<uint32_t> fb_px;  // owned pixels, row-major
+    uint32_t fb_w = 0, fb_h = 0, fb_ns = 0;
+    std::atomic<uint32_t> tiles_done{0};
+    std::mutex fb_mu;  // render start / preview: the framebuffer's size and owner list
 };
 
 // the two hot-path instantiations of the host backend: any linear hit program through the
@@ -169,13 +176,14 @@ static void render_tiles(mrt_cpu_scene* c, const mrt_render_desc* d, const std::
                     col = fold_sample(col, L, s, d->mode, d->max_luminance);
                 }
                 col = final_pixel(col, ns, d->mode, d->max_luminance);
-                float* o = rgb_out + (size_t)pix * 4;
+                float* o = c->fb.data() + (size_t)pix * 4;
                 o[0] = col.x;
                 o[1] = col.y;
                 o[2] = col.z;
                 o[3] = 0.0f;
             }
         c->done.fetch_add((uint64_t)(t.xmax - t.xmin) * (t.ymax - t.ymin) * ns, std::memory_order_relaxed);
+        c->tiles_done.fetch_add(1, std::memory_order_release);
     }
     rays_total.fetch_add(my_rays, std::memory_order_relaxed);
 }
@@ -198,6 +206,15 @@ mrt_status mrt_cpu_render(mrt_cpu_scene* c, const mrt_render_desc* d, float* rgb
     for (const mrt_tile& t : tiles) px += (uint64_t)(t.xmax - t.xmin) * (t.ymax - t.ymin);
     c->done.store(0, std::memory_order_relaxed);
     c->total.store(px * ns, std::memory_order_relaxed);
+    {
+        std::lock_guard<std::mutex> lk(c->fb_mu);
+        c->fb.assign((size_t)d->width * d->height * 4, 0.0f);
+        c->fb_px = mrt_internal_local_pixels(d);
+        c->fb_w = d->width;
+        c->fb_h = d->height;
+        c->fb_ns = ns;
+        c->tiles_done.store(0, std::memory_order_relaxed);
+    }
     uint32_t n = d->threads ? d->threads : std::max(1u, std::thread::hardware_concurrency());
     n = (uint32_t)std::min<size_t>(n, std::max<size_t>(tiles.size(), 1));
     std::atomic<uint32_t> next{0};
@@ -211,6 +228,7 @@ mrt_status mrt_cpu_render(mrt_cpu_scene* c, const mrt_render_desc* d, float* rgb
     for (uint32_t i = 1; i < n; i++) pool.emplace_back(work);
     work();
     for (std::thread& t : pool) t.join();
+    for (uint32_t p : c->fb_px) memcpy(rgb_out + (size_t)p * 4, c->fb.data() + (size_t)p * 4, 16);
     c->last_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     c->last_threads = n;
     if (rays_out) *rays_out = rays.load();
@@ -227,5 +245,18 @@ mrt_status mrt_cpu_progress(mrt_cpu_scene* c, float* pct) {
 mrt_status mrt_cpu_last_ms(mrt_cpu_scene* c, float* ms, uint32_t* threads) {
     *ms = (float)c->last_ms;
     if (threads) *threads = c->last_threads;
+    return MRT_OK;
+}
+
+// draw()'s framebuffer as the UI thread sees it (main.cpp:387-444): every finished tile's pixels
+// with all their samples, the others still black.  A pixel is written once, after its last sample,
+// as the reference's workers write G_linearBackBuffer.
+mrt_status mrt_cpu_preview(mrt_cpu_scene* c, float* rgb_out, uint32_t* samples_done) {
+    std::lock_guard<std::mutex> lk(c->fb_mu);
+    *samples_done = 0;
+    if (c->fb.empty()) return MRT_OK;
+    const uint32_t done = c->tiles_done.load(std::memory_order_acquire);
+    for (uint32_t p : c->fb_px) memcpy(rgb_out + (size_t)p * 4, c->fb.data() + (size_t)p * 4, 16);
+    *samples_done = done ? c->fb_ns : 0u;
     return MRT_OK;
 }

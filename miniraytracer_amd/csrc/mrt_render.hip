@@ -190,6 +190,17 @@ struct mrt_scene {
     float4* d_acc = nullptr;
     float4* d_lev = nullptr;
     float4* d_out = nullptr;         // mrt_render's device framebuffer (local-pixel order)
+    // progressive preview (MRT_RF_PREVIEW): device staging image, pinned host copy guarded by a
+    // sequence word the render's stream writes around each copy (odd = copy in flight) and the
+    // sample count the copy holds
+    float4* d_prev = nullptr;
+    size_t prev_cap = 0;
+    float4* h_prev = nullptr;
+    size_t h_prev_cap = 0;
+    uint32_t* h_seq = nullptr;       // [0] sequence, [1] samples folded into h_prev
+    uint32_t prev_epoch = 0;
+    std::vector<uint32_t> prev_px;   // local pixel -> row-major pixel of the previewed render
+    uint32_t prev_w = 0, prev_h = 0;
     uint32_t lev_rows = 0;
     uint64_t* d_counter = nullptr;   // 64 B scratch: [0] unused, [2] ray total of mrt_render, [4] cancel flag
     uint64_t* d_counters = nullptr;  // one work counter per chunk launch (progress reads them)
@@ -782,9 +793,11 @@ extern "C" void mrt_scene_free(mrt_scene* s) {
     if (s->pstream) (void)hipStreamDestroy(s->pstream);
     if (s->h_prog) (void)hipHostFree(s->h_prog);
     if (s->h_one) (void)hipHostFree(s->h_one);
+    if (s->h_prev) (void)hipHostFree(s->h_prev);
+    if (s->h_seq) (void)hipHostFree(s->h_seq);
     if (s->ev_done) (void)hipEventDestroy(s->ev_done);
     for (void* p : {(void*)s->d_counters, (void*)s->d_pixels, (void*)s->d_sdist, (void*)s->d_rad, (void*)s->d_path_rays, (void*)s->d_acc,
-                    (void*)s->d_lev, (void*)s->d_out})
+                    (void*)s->d_lev, (void*)s->d_out, (void*)s->d_prev})
         if (p) (void)hipFree(p);
     delete s;
 }
@@ -865,6 +878,27 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
     if ((st = grow(s, (void**)&s->d_rad, &s->rad_cap, paths * 12))) return st;
     if ((st = grow(s, (void**)&s->d_acc, &s->acc_cap, (size_t)s->npix * 16))) return st;
     if ((st = grow(s, (void**)&s->d_out, &s->out_cap, (size_t)s->npix * 16 + 16))) return st;
+    if (d->flags & MRT_RF_PREVIEW) {
+        if ((st = grow(s, (void**)&s->d_prev, &s->prev_cap, (size_t)s->npix * 16 + 16))) return st;
+        std::lock_guard<std::mutex> lk(s->prog_mu);
+        if (s->h_prev_cap < s->npix) {
+            if ((st = quiesce(s))) return st;
+            if (s->h_prev) (void)hipHostFree(s->h_prev);
+            s->h_prev = nullptr;
+            s->h_prev_cap = 0;
+            HIPCHK(hipHostMalloc((void**)&s->h_prev, (size_t)s->npix * 16 + 16, hipHostMallocPortable));
+            s->h_prev_cap = s->npix;
+        }
+        if (!s->h_seq) {
+            HIPCHK(hipHostMalloc((void**)&s->h_seq, 64, hipHostMallocPortable | hipHostMallocCoherent));
+            memset(s->h_seq, 0, 64);
+        }
+        if (relayout || s->prev_px.size() != s->npix) {
+            s->prev_px = mrt_internal_local_pixels(d);
+        }
+        s->prev_w = d->width;
+        s->prev_h = d->height;
+    }
     if (d->flags & MRT_RF_PATH_DEBUG)
         if ((st = grow(s, (void**)&s->d_path_rays, &s->pr_cap, paths * 4))) return st;
     s->lev_rows = std::max<uint32_t>(d->max_bounces, 1);
@@ -923,6 +957,14 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
     }
     s->n_launch = 0;
     s->last_numerics = (d->flags & MRT_RF_FAST) ? 1u : 0u;
+    const bool preview = (d->flags & MRT_RF_PREVIEW) != 0;
+    uint32_t seq = 0;
+    if (preview) {  // a new render: no snapshot yet (sequence 0), in stream order
+        std::lock_guard<std::mutex> lk(s->prog_mu);
+        HIPCHK(hipStreamWriteValue32(q, s->h_seq + 1, 0u, 0));
+        HIPCHK(hipStreamWriteValue32(q, s->h_seq, 0u, 0));
+        s->prev_epoch++;
+    }
     for (uint32_t s0 = 0; s0 < ns; s0 += s->chunk) {
         uint32_t s1 = std::min(ns, s0 + s->chunk);
         PathParams P{};
@@ -966,6 +1008,15 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         uint32_t blocks = (s->npix + 255) / 256;
         hipLaunchKernelGGL(mrt_fold_kernel, dim3(blocks), dim3(256), 0, q, s->d_rad, s->d_acc, s->npix, s0, s1, d->mode, d->max_luminance);
         HIPCHK(hipGetLastError());
+        if (preview) {  // the image after s1 samples, copied under the sequence lock
+            hipLaunchKernelGGL(mrt_final_kernel, dim3(blocks), dim3(256), 0, q, s->d_acc, s->d_prev, s->npix, s1, d->mode, d->max_luminance);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipStreamWriteValue32(q, s->h_seq, 2 * seq + 1, 0));
+            HIPCHK(hipMemcpyAsync(s->h_prev, s->d_prev, (size_t)s->npix * 16, hipMemcpyDeviceToHost, q));
+            HIPCHK(hipStreamWriteValue32(q, s->h_seq + 1, s1, 0));
+            HIPCHK(hipStreamWriteValue32(q, s->h_seq, 2 * seq + 2, 0));
+            seq++;
+        }
         s->last_paths = P.n_paths;
     }
     uint32_t blocks = (s->npix + 255) / 256;
@@ -984,7 +1035,9 @@ extern "C" mrt_status mrt_render(mrt_scene* s, const mrt_render_desc* d, float* 
     if (cancel && *cancel) return mrt_internal_fail(MRT_ERR_CANCELLED, "cancelled");
     mrt_render_desc dc = *d;  // a cancellable render runs as >= 16 launches; cancel lands between them
     const uint32_t ns = d->sqrt_samples * d->sqrt_samples;
-    if (cancel && dc.chunk_samples == 0 && !(dc.flags & MRT_RF_PATH_DEBUG)) dc.chunk_samples = std::max(1u, ns / 16);
+    // (so does a previewed one: each launch adds a snapshot)
+    if ((cancel || (dc.flags & MRT_RF_PREVIEW)) && dc.chunk_samples == 0 && !(dc.flags & MRT_RF_PATH_DEBUG))
+        dc.chunk_samples = std::max(1u, ns / 16);
     d = &dc;
     mrt_status st = mrt_prepare(s, d);
     if (st) return st;
@@ -1055,6 +1108,33 @@ extern "C" mrt_status mrt_progress(mrt_scene* s, float* pct) {
     }
     *pct = total > 0 ? (float)std::min(100.0, done * 100.0 / total) : 0.0f;
     return MRT_OK;
+}
+
+// The UI thread's view of G_linearBackBuffer (main.cpp:387-444) without stopping the render: the
+// newest snapshot whose sequence word was even, and unchanged, around the copy out of pinned memory.
+extern "C" mrt_status mrt_preview(mrt_scene* s, float* rgb_out, uint32_t* samples_done) {
+    if (!s || !rgb_out || !samples_done) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_preview: null");
+    *samples_done = 0;
+    if (s->cpu) return mrt_cpu_preview(s->cpu, rgb_out, samples_done);
+    std::lock_guard<std::mutex> lk(s->prog_mu);
+    if (!s->h_seq || !s->h_prev || s->prev_px.empty()) return MRT_OK;  // no preview render yet
+    std::vector<float4> snap(s->prev_px.size());
+    for (int tries = 0; tries < 1000; tries++) {
+        const uint32_t a = __atomic_load_n(s->h_seq, __ATOMIC_ACQUIRE);
+        if (a == 0) return MRT_OK;  // nothing folded yet
+        if (a & 1u) {               // a copy is landing: the previous one is being overwritten
+            usleep(50);
+            continue;
+        }
+        const uint32_t n = __atomic_load_n(s->h_seq + 1, __ATOMIC_ACQUIRE);
+        memcpy(snap.data(), s->h_prev, snap.size() * 16);
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        if (__atomic_load_n(s->h_seq, __ATOMIC_ACQUIRE) != a) continue;  // torn: retry
+        for (size_t i = 0; i < snap.size(); i++) memcpy(rgb_out + (size_t)s->prev_px[i] * 4, &snap[i], 16);
+        *samples_done = n;
+        return MRT_OK;
+    }
+    return MRT_OK;  // the render outran every attempt: report nothing rather than a torn image
 }
 
 extern "C" mrt_status mrt_scene_kernel_info(const mrt_scene* s, mrt_kernel_info* out) {

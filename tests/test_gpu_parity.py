@@ -4,6 +4,7 @@ Bar: bit-exact.  Per-path radiance, per-path ray counts, total ray count (the Mr
 main.cpp:68) and the accumulated image must equal the reference's own trace() (stream-matched
 fixtures) and the C restatement, float bits included."""
 import os
+import threading
 
 import numpy as np
 import pytest
@@ -434,3 +435,62 @@ def test_gpu_equals_cpu_backend(gpu, sid, w, h, spp, mode):
     b, rb = gpu.Renderer(sc, "cpu").render(d)
     assert ra == rb
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def _fold_mode1(rad, n, max_lum=1000.0):
+    """draw2()'s per-pixel running average over the first n samples (main.cpp:205-231) in float32,
+    operation by operation as mrt_shade.h fold_sample (no contraction)."""
+    f = np.float32
+    c = np.zeros(rad.shape[1:], dtype=f)
+    for s in range(n):
+        smp = rad[s].copy()
+        bad = ~np.isfinite(smp).all(axis=1)
+        smp[bad] = c[bad] if s > 0 else 0
+        if s > 0:
+            smp = c + (smp - c) * (f(1.0) / (f(s) + f(1.0)))
+        lum = (smp[:, 0] * f(0.212655) + smp[:, 1] * f(0.715158)) + smp[:, 2] * f(0.072187)
+        big = lum > f(max_lum)
+        smp[big] = smp[big] * (f(max_lum) / lum[big])[:, None]
+        c = smp.astype(f)
+    return c
+
+
+def test_progressive_preview_is_the_running_average(gpu):
+    """MRT_RF_PREVIEW (the reference's UI thread tone-mapping G_linearBackBuffer every 33 ms while
+    the workers run, main.cpp:387-444): a poller on another thread reads snapshots while a 16-launch
+    mode-1 render runs.  Each snapshot reports n samples and equals draw2()'s running average of the
+    first n samples of every pixel exactly (never a mix of two passes); the last one is the image."""
+    sc, r = renderer(gpu, 5, 160, 120)
+    w, h, spp = 160, 120, 64
+    dbg = gpu.render_desc(w, h, spp, mode=1, flags=gpu._lib.RF_PATH_DEBUG)
+    r.render(dbg)
+    ns = dbg.sqrt_samples ** 2
+    px = gpu.local_pixels(dbg)
+    prgb, _ = r.paths(len(px) * ns)
+    rad = prgb.reshape(ns, len(px), 3)
+    d = gpu.render_desc(w, h, spp, mode=1, chunk_samples=4, preview=True)
+    seen = []
+    done = threading.Event()
+
+    def poll():
+        while not done.is_set():
+            seen.append(r.preview(w, h))
+
+    t = threading.Thread(target=poll)
+    t.start()
+    img, _ = r.render(d)
+    done.set()
+    t.join()
+    final, n = r.preview(w, h)
+    assert n == ns and np.array_equal(final, img)
+    counts = sorted({k for _, k in seen} | {n})
+    assert all(k % 4 == 0 for k in counts)
+    checked = 0
+    for snap, k in seen[:: max(1, len(seen) // 8)] + [(final, n)]:
+        if k == 0:
+            continue
+        ref = _fold_mode1(rad, k)
+        got = snap.reshape(-1, 4)[px, :3]
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), k
+        checked += 1
+    assert checked >= 1
