@@ -245,9 +245,14 @@ def main():
             tg.finish(pending[0])
             pending[0] = None
 
+    def note(msg):  # progress on stderr: long renders (C5 at full size) keep the log moving
+        if rank == 0:
+            print(f"bench.py: {msg} ({time.strftime('%H:%M:%S')})", file=sys.stderr, flush=True)
+
     def measure(d):
         """W untimed warmup steps, then EXACTLY K steps between barrier + synchronize on both
         sides; (max-over-ranks seconds, total rays of all ranks, this rank's rays per step)."""
+        note(f"measuring numerics={'fast' if d.flags & m._lib.RF_FAST else 'exact'}")
         # setup, untimed: one render per context, so every context's first-use costs (workspace
         # first touch, first launch on its stream) are paid before the warmup steps
         for j in range(npipe):
@@ -262,6 +267,7 @@ def main():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
+        note("timed steps")
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step(d)

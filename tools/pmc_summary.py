@@ -74,6 +74,13 @@ def main():
     sqd = per_dispatch(sqp) if os.path.exists(sqp) else {}
     sq, _, _ = mean_by_kernel(sqd)
     res = {"workload_config": [int(x) for x in a.config.split()], "kernels": {}, "sq_wave_check": []}
+    # rays of one launch: the bench line of the trace pass (one launch per step at these sizes)
+    rays_per_launch = None
+    tl = os.path.join(a.prof, "trace.log")
+    if os.path.exists(tl):
+        for line in open(tl):
+            if line.startswith("{") and '"rays_per_step"' in line:
+                rays_per_launch = json.loads(line)["config"]["rays_per_step"]
     for did, (k, c, m) in sorted(sqd.items(), key=lambda t: int(t[0])):
         try:
             grid_waves = int(m["Grid_Size"]) // 64
@@ -83,7 +90,7 @@ def main():
     for k in fetch:
         if not k.startswith("mrt_path_kernel"):
             continue
-        e = {"launches": n_f[k], "dispatch": meta[k], "FETCH_SIZE_KiB": fetch[k].get("FETCH_SIZE"),
+        e = {"launches": n_f[k], "dispatch": meta[k], "rays_per_launch": rays_per_launch, "FETCH_SIZE_KiB": fetch[k].get("FETCH_SIZE"),
              "WRITE_SIZE_KiB": write.get(k, {}).get("WRITE_SIZE")}
         e["hbm_bytes_per_launch"] = 2 * e["FETCH_SIZE_KiB"] * 1024 + (e["WRITE_SIZE_KiB"] or 0) * 1024
         if k in avg_ns:
