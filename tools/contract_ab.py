@@ -65,7 +65,7 @@ def summarize(tag, pmcs):
             rays = e.get("rays_per_launch")
             if name and sq and rays:
                 inst[f"{name}_{num}"] = {"valu_wave_inst_per_ray": sq["SQ_INSTS_VALU"] / rays,
-                                         "valu_lane_inst_per_ray": sq["SQ_THREAD_CYCLES_VALU"] / 2.0 / rays,
+                                         "valu_lane_inst_per_ray": sq["SQ_THREAD_CYCLES_VALU"] / rays,  # active lanes summed over VALU instructions
                                          "valu_lane_util": e.get("valu_lane_util"), "pmc": os.path.relpath(p, ROOT)}
     res = {}
     print(f"{'config':6s} {'contract':8s} {'Grays/s':>8s} {'wave-inst/ray':>13s} {'lane-inst/ray':>13s} {'RMSE vs shipped':>15s} {'rays vs shipped':>15s}")
