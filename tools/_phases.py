@@ -9,7 +9,7 @@ from miniraytracer_amd._lib import lib
 scene, w, h, spp = (int(a) for a in (sys.argv[1:] + ["5", "500", "500", "256"])[:4])
 sc = m.select_scene(scene, w / h)
 r = m.Renderer(sc, 0)
-d = m.render_desc(w, h, spp)
+d = m.render_desc(w, h, spp, numerics=__import__("os").environ.get("NUMERICS", "exact"))
 r.render(d)
 NPH = int(__import__("os").environ.get("NPH", "12"))
 out = (C.c_ulonglong * NPH)()

@@ -9,7 +9,7 @@ set -e
 cd "$(dirname "$0")/.."
 tag=$1; shift
 flags="$*"
-make -s build/obj/scene_builder.o build/obj/mrt_common.o build/obj/mrt_render.o build/obj/mrt_kernels_exact.o
+make -s build/obj/scene_builder.o build/obj/mrt_common.o build/obj/mrt_render.o build/obj/mrt_kernels_exact.o build/obj/mrt_cpu.o
 mkdir -p exp/obj_$tag
 BASE="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-fast-math -fno-slp-vectorize -w -mllvm -disable-promote-alloca-to-vector -mllvm -structurizecfg-skip-uniform-regions -DMRT_EXPERIMENTS"
 /opt/rocm/bin/hipcc $BASE -DMRT_TABLE_FAST=1 $flags -c miniraytracer_amd/csrc/mrt_kernels.hip -o exp/obj_$tag/mrt_kernels_fast.o
@@ -24,5 +24,5 @@ if [ -n "${HOST_FLAGS:-}" ]; then  # host TU too (e.g. -DMRT_PATH_WG=..., which 
   RO=exp/obj_$tag/mrt_render.o
 fi
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $RO $EX exp/obj_$tag/mrt_kernels_fast.o \
-    build/obj/scene_builder.o build/obj/mrt_common.o -ldl -o exp/libmrt_$tag.so
+    build/obj/mrt_cpu.o build/obj/scene_builder.o build/obj/mrt_common.o -ldl -o exp/libmrt_$tag.so
 echo "built exp/libmrt_$tag.so"
