@@ -80,6 +80,10 @@ __host__ static inline bool signbit(double x) { return std::signbit(x); }
 // every bounce's (a, pdf) and folding them deepest-first.  Same factors, another association (a
 // rounding difference per bounce), so tolerance contract only; it needs no per-bounce level
 // storage (LDS / HBM) and no fold loop.
+// box.h's six rects as one slab test (mrt_sig.h box6_hit), tolerance contract only
+#ifndef MRT_FAST_BOX
+#define MRT_FAST_BOX MRT_FAST
+#endif
 #ifndef MRT_FWD_FOLD
 #define MRT_FWD_FOLD MRT_FAST
 #endif

@@ -441,6 +441,38 @@ mrt_status mrt_internal_scene_tables(const mrt_scene_view* v, SceneTables* T) {
         const float c = std::fabs(n.f[4]);
         if (!(c == 0.0f || (c >= 0x1p-77f && c <= 0x1p60f))) n.kind |= MRT_F_SLOWDIV << 16;
     }
+    // box.h:12-20 recognised: an object_list of exactly six outward-facing rects over one box
+    // (xy at max z / min z, xz at max y / min y, yz at max x / min x, bounds spanning the box, one
+    // material, no uv, no slow divisions).  Flag MRT_F_BOX6, planes in f[6..11] (min xyz, max xyz):
+    // the tolerance contract tests such a list as one slab test (mrt_sig.h box6_hit).
+    for (size_t i = 0; i < nodes.size(); i++) {
+        mrt_node& n = nodes[i];
+        if ((n.kind & 0xFF) != MRT_K_LIST || n.b != 6 || n.a + 6 > v->n_children) continue;
+        const mrt_node* c[6];
+        bool ok = true;
+        for (int j = 0; j < 6 && ok; j++) {
+            const uint32_t ci = v->children[n.a + j];
+            ok = ci < nodes.size();
+            if (ok) c[j] = &nodes[ci];
+        }
+        if (!ok) continue;
+        static const uint32_t kinds[6] = {MRT_K_XY, MRT_K_XY, MRT_K_XZ, MRT_K_XZ, MRT_K_YZ, MRT_K_YZ};
+        for (int j = 0; j < 6 && ok; j++)
+            ok = (c[j]->kind & 0xFF) == kinds[j] && c[j]->f[5] == ((j & 1) ? -1.0f : 1.0f) && c[j]->mat == c[0]->mat &&
+                 !((c[j]->kind >> 16) & (MRT_F_NEEDUV | MRT_F_SLOWDIV));
+        if (!ok) continue;
+        const float xmin = c[5]->f[4], xmax = c[4]->f[4], ymin = c[3]->f[4], ymax = c[2]->f[4], zmin = c[1]->f[4], zmax = c[0]->f[4];
+        auto span = [&](const mrt_node* r, float a0, float a1, float b0, float b1) {
+            return r->f[0] == a0 && r->f[1] == a1 && r->f[2] == b0 && r->f[3] == b1;
+        };
+        ok = xmin < xmax && ymin < ymax && zmin < zmax && span(c[0], xmin, xmax, ymin, ymax) && span(c[1], xmin, xmax, ymin, ymax) &&
+             span(c[2], xmin, xmax, zmin, zmax) && span(c[3], xmin, xmax, zmin, zmax) && span(c[4], ymin, ymax, zmin, zmax) &&
+             span(c[5], ymin, ymax, zmin, zmax);
+        if (!ok) continue;
+        n.kind |= MRT_F_BOX6 << 16;
+        n.f[6] = xmin; n.f[7] = ymin; n.f[8] = zmin;
+        n.f[9] = xmax; n.f[10] = ymax; n.f[11] = zmax;
+    }
     for (mrt_node& n : nodes) {
         if ((n.kind & 0xFF) != MRT_K_TRANSLATE || n.a >= nodes.size()) continue;
         const mrt_node& c = nodes[n.a];

@@ -111,6 +111,13 @@ struct SigWalk {
             } else if constexpr (op == LOP_LIST) {  // object_list::hit box reject (scene_object.h:83)
                 constexpr uint32_t skip = G.skip[PC];
                 const bool in = on && (!(LOP_FLAGS(o) & MRT_F_HASBOX) || lin_box(o, w.cur, tmin, w.closest));
+                if constexpr (MRT_FAST_BOX && is_box6<PC>()) {
+                    if (LOP_FLAGS(o) & MRT_F_BOX6) {  // uniform: box.h's six rects as one slab test
+                        if (any_lane(in)) box6_hit<PC>(prog, w, in, tmin);
+                        run<skip + 1, END>(S, prog, tmin, w, on, rec, L);
+                        return;
+                    }
+                }
                 if (any_lane(in)) run<PC + 1, skip>(S, prog, tmin, w, in, rec, L);
                 run<skip + 1, END>(S, prog, tmin, w, on, rec, L);
             } else if constexpr (op == LOP_INST) {  // scene_object.cpp:9-18, 70-98
@@ -140,6 +147,43 @@ struct SigWalk {
                 run<PC + 1, END>(S, prog, tmin, w, on, rec, L);
             }
         }
+    }
+
+    // ops PC+1..PC+6 are the six rects of box.h in its order (the list at PC ends at PC+7)
+    template <uint32_t PC>
+    MRT_DATTR static constexpr bool is_box6() {
+        if (PC + 7 >= G.n || G.op[PC] != LOP_LIST || G.skip[PC] != PC + 7) return false;
+        constexpr uint32_t k[6] = {MRT_K_XY, MRT_K_XY, MRT_K_XZ, MRT_K_XZ, MRT_K_YZ, MRT_K_YZ};
+        for (uint32_t j = 0; j < 6; j++)
+            if (G.op[PC + 1 + j] != LOP_PRIM || G.kind[PC + 1 + j] != k[j]) return false;
+        return true;
+    }
+    // Tolerance contract: box.h's object_list of six outward-facing one-sided rects (MRT_F_BOX6)
+    // as one slab test.  From outside the box the one front-facing face a ray can hit is where it
+    // enters, at the slab entry t (the same (k - o) * 1/d the rect test forms); from inside or from
+    // the surface every face is behind or back-facing, and so is the entry (t < tmin).  Ties
+    // (edges) go to the later rect of box.h's order, as object_list::hit's closest narrowing does.
+    // Differs from the six tests only by rounding at edges.
+    template <uint32_t PC>
+    MRT_DATTR static __forceinline__ void box6_hit(const MRT_CONST_AS LinOp* prog, SigState& w, bool in, float tmin) {
+        const MRT_CONST_AS LinOp& o = prog[PC];
+        const Ray& r = w.cur;
+        const float t0x = (o.f[6] - r.o.x) * r.inv.x, t1x = (o.f[9] - r.o.x) * r.inv.x;
+        const float t0y = (o.f[7] - r.o.y) * r.inv.y, t1y = (o.f[10] - r.o.y) * r.inv.y;
+        const float t0z = (o.f[8] - r.o.z) * r.inv.z, t1z = (o.f[11] - r.o.z) * r.inv.z;
+        const float nx = fminf(t0x, t1x), ny = fminf(t0y, t1y), nz = fminf(t0z, t1z);
+        const float tn = fmaxf(fmaxf(nx, ny), nz);
+        const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+        const bool h = in & (tn <= tf) & (tn >= tmin) & (tn <= w.closest);
+        // the entry face: rects 0/1 = z max/min, 2/3 = y max/min, 4/5 = x max/min
+        const uint32_t nz_node = r.d.z > 0.0f ? prog[PC + 2].node : prog[PC + 1].node;
+        const uint32_t ny_node = r.d.y > 0.0f ? prog[PC + 4].node : prog[PC + 3].node;
+        const uint32_t nx_node = r.d.x > 0.0f ? prog[PC + 6].node : prog[PC + 5].node;
+        const uint32_t node = tn == nx ? nx_node : (tn == ny ? ny_node : nz_node);
+        w.closest = h ? tn : w.closest;
+        w.hnode = h ? (kDerive ? PC + 1 : node) : w.hnode;
+        w.hinst = h ? cur_inst<PC + 1>() : w.hinst;
+        w.hdone = h ? false : w.hdone;
     }
 
     // the record of the closest hit, op by op: for each primitive op some lane hit, that op's
