@@ -470,6 +470,7 @@ mrt_status mrt_internal_scene_tables(const mrt_scene_view* v, SceneTables* T) {
              span(c[5], ymin, ymax, zmin, zmax);
         if (!ok) continue;
         n.kind |= MRT_F_BOX6 << 16;
+        n.mat = c[0]->mat;  // (an object_list has no material of its own)
         n.f[6] = xmin; n.f[7] = ymin; n.f[8] = zmin;
         n.f[9] = xmax; n.f[10] = ymax; n.f[11] = zmax;
     }

@@ -496,6 +496,41 @@ MRT_DFN bool leaf_prim_hit(const mrt_node& n, uint32_t kind, const Ray& r, float
     }
 }
 
+// Tolerance contract: an object_list flagged MRT_F_BOX6 (box.h's six outward-facing rects, planes
+// in f[6..11], the rects' material in mat) as one slab test -- the entry face is the one
+// front-facing rect a ray from outside can hit (mrt_sig.h box6_hit); its record is the rect's
+// (rect.cpp:40-44: p on the plane, n = the face's axis and sign).  Its own bounding-box test is
+// implied by the slab test.
+MRT_DFN bool box6_leaf_hit(const mrt_node& c, const Ray& r, float tmin, float tmax, HitRec& rec, bool full) {
+    const float t0x = (c.f[6] - r.o.x) * r.inv.x, t1x = (c.f[9] - r.o.x) * r.inv.x;
+    const float t0y = (c.f[7] - r.o.y) * r.inv.y, t1y = (c.f[10] - r.o.y) * r.inv.y;
+    const float t0z = (c.f[8] - r.o.z) * r.inv.z, t1z = (c.f[11] - r.o.z) * r.inv.z;
+    const float nx = fminf(t0x, t1x), ny = fminf(t0y, t1y), nz = fminf(t0z, t1z);
+    const float tn = fmaxf(fmaxf(nx, ny), nz);
+    const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+    if (!((tn <= tf) & (tn >= tmin) & (tn <= tmax))) return false;
+    rec.t = tn;
+    if (full) {
+        rec.mat = c.mat;
+        rec.p = eval(r, tn);
+        // ties go to the later rect of box.h's order (x faces, then y, then z)
+        if (tn == nx) {
+            const bool lo = r.d.x > 0.0f;
+            rec.p.x = lo ? c.f[6] : c.f[9];
+            rec.n = f3{lo ? -1.0f : 1.0f, 0, 0};
+        } else if (tn == ny) {
+            const bool lo = r.d.y > 0.0f;
+            rec.p.y = lo ? c.f[7] : c.f[10];
+            rec.n = f3{0, lo ? -1.0f : 1.0f, 0};
+        } else {
+            const bool lo = r.d.z > 0.0f;
+            rec.p.z = lo ? c.f[8] : c.f[11];
+            rec.n = f3{0, 0, lo ? -1.0f : 1.0f};
+        }
+    }
+    return true;
+}
+
 // a bvh_node leaf: a primitive, or an object_list (its box already tested by the parent) of
 // primitives and object_lists of primitives (box, box.h:6-30) -- object_list::hit semantics,
 // the running closest narrowing across children (scene_object.h:79-103).  The leaf is a run of
@@ -515,6 +550,14 @@ MRT_DFN bool bvhw_leaf(const DScene& S, uint32_t ref, const Ray& r, float tmin, 
         const mrt_node c = ld_node_v(run + i);
         const uint32_t ck = MRT_NODE_KIND(c);
         if (ck == MRT_K_LIST) {
+            if (MRT_FAST_BOX && (MRT_NODE_FLAGS(c) & MRT_F_BOX6)) {  // box.h's six rects as one slab test
+                if (box6_leaf_hit(c, r, tmin, closest, rec, full)) {
+                    hit = true;
+                    closest = rec.t;
+                }
+                i += c.b;
+                continue;
+            }
             if ((MRT_NODE_FLAGS(c) & MRT_F_HASBOX) && !aabb_hit(c.f, c.f + 3, r, tmin, closest)) i += c.b;
             continue;
         }
