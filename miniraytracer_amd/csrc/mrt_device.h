@@ -450,6 +450,36 @@ struct PhaseClock {};
     do {               \
     } while (0)
 #endif
+// Branch occupancy (experiment builds with -DMRT_EXPERIMENTS -DMRT_BSTATS): per counting point,
+// the wave executions reaching it and the lanes active there (g_bstats[2i], g_bstats[2i+1]).
+#if defined(MRT_EXPERIMENTS) && defined(MRT_BSTATS) && defined(__HIP_DEVICE_COMPILE__)
+extern __device__ unsigned long long g_bstats[64];
+#define BSTAT(i)                                                                      \
+    do {                                                                              \
+        const uint64_t m_ = __builtin_amdgcn_ballot_w64(true);                        \
+        if (__builtin_amdgcn_mbcnt_hi((uint32_t)(m_ >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m_, 0u)) == 0u) { \
+            atomicAdd(&g_bstats[2 * (i)], 1ull);                                      \
+            atomicAdd(&g_bstats[2 * (i) + 1], (unsigned long long)__popcll(m_));      \
+        }                                                                             \
+    } while (0)
+// lanes where cond holds, counted at an execution of the wave (all active lanes reach it)
+#define BSTATC(i, cond)                                                               \
+    do {                                                                              \
+        const uint64_t m_ = __builtin_amdgcn_ballot_w64(true);                        \
+        const uint64_t c_ = __builtin_amdgcn_ballot_w64(cond);                        \
+        if (__builtin_amdgcn_mbcnt_hi((uint32_t)(m_ >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m_, 0u)) == 0u) { \
+            atomicAdd(&g_bstats[2 * (i)], 1ull);                                      \
+            atomicAdd(&g_bstats[2 * (i) + 1], (unsigned long long)__popcll(c_));      \
+        }                                                                             \
+    } while (0)
+#else
+#define BSTAT(i) \
+    do {         \
+    } while (0)
+#define BSTATC(i, cond) \
+    do {                \
+    } while (0)
+#endif
 
 struct HitRec {
     float t;

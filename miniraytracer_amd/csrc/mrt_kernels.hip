@@ -63,6 +63,17 @@ extern "C" int mrt_debug_phases(unsigned long long* out, int reset) {
     return 0;
 }
 #endif
+#if defined(MRT_EXPERIMENTS) && defined(MRT_BSTATS)  // build ONE of the two TUs with it
+namespace mrtd { __device__ unsigned long long g_bstats[64]; }
+extern "C" int mrt_debug_bstats(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mrtd::g_bstats), sizeof(g_bstats)) != hipSuccess) return 1;
+    if (reset) {
+        unsigned long long z[64] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(mrtd::g_bstats), z, sizeof(z)) != hipSuccess) return 1;
+    }
+    return 0;
+}
+#endif
 // resumable mesh walk (room + mesh kernels): the walk loop returns the wave to shading / new rays
 // once at most MRT_WALK_MIN lanes still walk and at least MRT_WALK_OTHER lanes have other work
 #ifndef MRT_WALK_MIN
@@ -189,6 +200,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                     u = nu / (float)P.width;
                     v = nv / (float)P.height;
                 }
+                BSTAT(10);
                 const uint64_t path_id = (uint64_t)pix * P.ns + s;
                 pcg_seed(ps.rng, splitmix64(P.seed ^ path_id), path_id);
                 start(u, v);
@@ -258,7 +270,9 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
             });
             if (!__any(active)) break;
             PH_MARK(ph, 0);
+            BSTATC(15, active);
             if (want_ray) {
+                BSTATC(12, pr.kind != 0);
                 ps.r = make_ray(pr.o, pr.dir, pr.time, pr.inside);
                 if (pr.kind) finish_scatter<F, LK>(S, ps, lev, pr);
             }

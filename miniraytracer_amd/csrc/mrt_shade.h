@@ -440,7 +440,10 @@ MRT_DFN bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, c
     else if constexpr ((F & FT_LIN) != 0) hit = scene_hit_lin<F>(S, r, 0.001f, rec, Ls, ps.rng, ph);
     else hit = scene_hit<F>(S, r, 0.001f, rec, ps.rng, Ls);
     PH_MARK(ph, 1);
+    BSTAT(0);
+    BSTATC(14, hit);
     if (!hit) {
+        BSTAT(1);
         if ((F & FT_SKY) && S.sky) {  // main.cpp:113-115
             float tt = 0.5f * (r.d.y + 1.0f);
             float o = 1.0f - tt;
@@ -452,10 +455,12 @@ MRT_DFN bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, c
     }
     const DMat M = S.mats[rec.mat];
     if (M.kind == MRT_M_LIGHT) {  // diffuse_light: sampleEmissive, never scatters (material.h:190-199)
+        BSTAT(2);
         *L = dot(rec.n, r.d) < 0.0f ? fmul(M.p, mat_color<F>(S, M, rec)) : f3{0, 0, 0};
         return true;
     }
     if (ps.depth >= max_bounces) {  // the emitted term of a non-emissive material
+        BSTAT(3);
         *L = f3{0, 0, 0};
         return true;
     }
@@ -474,6 +479,7 @@ MRT_DFN bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, c
         return false;
     }
     if (M.kind == MRT_M_DIELECTRIC) {  // dielectric::scatter (material.h:121-175)
+        BSTAT(5);
         const float ref = M.p;
         const float cosI = -dot(r.d, rec.n);
         f3 facing;
@@ -513,6 +519,7 @@ MRT_DFN bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, c
     pr->att = mat_color<F>(S, M, rec);
     pr->n = rec.n;
     pr->kind = lamb ? 1u : 2u;
+    BSTAT(6);
     const bool light = S.biased != MRT_NONE && randf(ps.rng) < 0.5f;
     Draws dr{0.0f, 0.0f, 2u};
     if (lamb) {
@@ -520,6 +527,7 @@ MRT_DFN bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, c
         dr.v1 = randf(ps.rng);
         dr.used = 0;
     }
+    BSTATC(7, light);
     if (light) pr->dir = biased_pdf_generate<F>(S, rec.p, r.time, ps.rng, dr);
     else pr->dir = lamb ? onb_apply(rec.n, random_cosine_direction_pre(dr.v0, dr.v1)) : random_in_sphere(ps.rng);
     PH_MARK(ph, 6);

@@ -113,6 +113,7 @@ struct SigWalk {
                 const bool in = on && (!(LOP_FLAGS(o) & MRT_F_HASBOX) || lin_box(o, w.cur, tmin, w.closest));
                 if constexpr (MRT_FAST_BOX && is_box6<PC>()) {
                     if (LOP_FLAGS(o) & MRT_F_BOX6) {  // uniform: box.h's six rects as one slab test
+                        BSTATC(11, in);
                         if (any_lane(in)) box6_hit<PC>(prog, w, in, tmin);
                         run<skip + 1, END>(S, prog, tmin, w, on, rec, L);
                         return;
@@ -131,7 +132,9 @@ struct SigWalk {
                     w.cur = r0;
                     if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, w.cur, tmin, w.closest);
                 }
+                BSTATC(8, in);
                 if (any_lane(in)) {
+                    BSTATC(9, in);
                     if constexpr (kind == MRT_K_TRROTY || kind == MRT_K_ROTY) w.cur = rotate_ray(w.cur, o.f[6], o.f[7]);
                     else w.cur = moved_ray(r0, sub(r0.o, f3{o.f[0], o.f[1], o.f[2]}));
                     run<PC + 1, skip>(S, prog, tmin, w, in, rec, L);
@@ -217,11 +220,127 @@ struct SigWalk {
     }
 };
 
+// Tolerance contract, Cornell box shape (scene 5, scene.cpp:286-330) whose box is box.h's six rects
+// (MRT_F_BOX6 on op 8): the walk written out for the ops the shape fixes, with the closest hit's
+// record carried per lane through the walk (a code, a plane, a sign, a material: a few selects per
+// primitive) instead of derived afterwards from the winning op (per-lane node loads and a switch on
+// its kind) -- no branch, no LDS.
+//   * the root list's and the instance's bounding boxes are not tested: every primitive test below
+//     is exact geometry, a box test only skips work (object_list::hit, scene_object.h:83;
+//     rotate_y::hit, scene_object.cpp:72);
+//   * translate(rotate_y(box)) (scene_object.cpp:9-18, 70-98) is ONE slab test of the box in its own
+//     frame (the ray moved and rotated; box6_hit's entry-face rule), the record taken in the world
+//     frame: p = o + t d (t is frame-independent: translate keeps d, rotate_y keeps |d|), the entry
+//     face's outward normal rotated back (scene_object.cpp:85-93).  Differs from the reference's
+//     per-face tests and frame round trip by rounding only.
+// Walls and sphere are lin_prim_t's tests in op order (ties to the later op, as closest narrowing).
+struct CornellRec {
+    float closest, k, ns;
+    uint32_t code, mat;  // code: 0 none; 1-3 world rect of axis code-1 (plane k); 4-6 box face of axis code-4; 7 sphere
+};
+template <uint32_t F, uint32_t PC>
+MRT_DFN void cornell_rect(const MRT_CONST_AS LinOp* prog, const Ray& r, float tmin, CornellRec& w) {
+    constexpr uint32_t KIND = kSigs[SIG_CORNELL].kind[PC];
+    static_assert(kSigs[SIG_CORNELL].op[PC] == LOP_PRIM && KIND != MRT_K_SPHERE, "Cornell shape: world rect");
+    constexpr uint32_t AX = KIND == MRT_K_XY ? 2u : KIND == MRT_K_XZ ? 1u : 0u;
+    const MRT_CONST_AS LinOp& o = prog[PC];
+    float t;
+    const bool h = lin_prim_t<F, KIND>(o, r, tmin, w.closest, &t);
+    w.closest = h ? t : w.closest;
+    w.code = h ? 1u + AX : w.code;
+    w.k = h ? o.f[4] : w.k;
+    w.ns = h ? o.f[5] : w.ns;
+    w.mat = h ? o.mat : w.mat;
+}
+template <uint32_t F>
+MRT_DFN bool cornell_fast_hit(const MRT_CONST_AS LinOp* prog, const Ray& r, float tmin, HitRec& rec) {
+    constexpr const LinSig& G = kSigs[SIG_CORNELL];
+    static_assert(G.op[7] == LOP_INST && G.kind[7] == MRT_K_TRROTY && G.op[8] == LOP_LIST && G.skip[8] == 15 &&
+                      G.op[17] == LOP_PRIM && G.kind[17] == MRT_K_SPHERE,
+                  "Cornell shape: translate(rotate_y(box)) at op 7, its six rects under op 8, the sphere at op 17");
+    CornellRec w{FLT_MAX_, 0.0f, 0.0f, 0u, 0u};
+    cornell_rect<F, 1>(prog, r, tmin, w);
+    cornell_rect<F, 2>(prog, r, tmin, w);
+    cornell_rect<F, 3>(prog, r, tmin, w);
+    cornell_rect<F, 4>(prog, r, tmin, w);
+    cornell_rect<F, 5>(prog, r, tmin, w);
+    cornell_rect<F, 6>(prog, r, tmin, w);
+    // the box in its own frame: o' = R(o - offset), d' = R d, R = rotate_y's (s, c)
+    const MRT_CONST_AS LinOp& io = prog[7];
+    const MRT_CONST_AS LinOp& bo = prog[8];
+    const float s = io.f[6], c = io.f[7];
+    const float mx = r.o.x - io.f[8], my = r.o.y - io.f[9], mz = r.o.z - io.f[10];
+    const float ox = c * mx - s * mz, oz = c * mz + s * mx;
+    const float dx = c * r.d.x - s * r.d.z, dz = c * r.d.z + s * r.d.x;
+    const float ix = recip_nr(dx), iz = recip_nr(dz);
+    const float t0x = (bo.f[6] - ox) * ix, t1x = (bo.f[9] - ox) * ix;
+    const float t0y = (bo.f[7] - my) * r.inv.y, t1y = (bo.f[10] - my) * r.inv.y;
+    const float t0z = (bo.f[8] - oz) * iz, t1z = (bo.f[11] - oz) * iz;
+    const float nx = fminf(t0x, t1x), ny = fminf(t0y, t1y), nz = fminf(t0z, t1z);
+    const float tn = fmaxf(fmaxf(nx, ny), nz);
+    const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+    const bool hb = (tn <= tf) & (tn >= tmin) & (tn <= w.closest);
+    // the entry face: its axis, and its outward normal's sign (against the ray's direction there)
+    const uint32_t bax = tn == nx ? 0u : (tn == ny ? 1u : 2u);
+    const float bd = bax == 0u ? dx : (bax == 1u ? r.d.y : dz);
+    w.closest = hb ? tn : w.closest;
+    w.code = hb ? 4u + bax : w.code;
+    w.ns = hb ? (bd > 0.0f ? -1.0f : 1.0f) : w.ns;
+    w.mat = hb ? bo.mat : w.mat;
+    // the sphere (op 17)
+    {
+        const MRT_CONST_AS LinOp& so = prog[17];
+        float t;
+        const bool h = lin_prim_t<F, MRT_K_SPHERE>(so, r, tmin, w.closest, &t);
+        w.closest = h ? t : w.closest;
+        w.code = h ? 7u : w.code;
+        w.mat = h ? so.mat : w.mat;
+    }
+    if (w.code == 0u) return false;
+    rec.t = w.closest;
+    rec.mat = w.mat;
+    f3 p = eval(r, w.closest);
+    // world rects: the point on the rect's plane (MRT_FAST_SNAP, lin_prim_rec_op)
+    p.x = w.code == 1u ? w.k : p.x;
+    p.y = w.code == 2u ? w.k : p.y;
+    p.z = w.code == 3u ? w.k : p.z;
+    if (w.code >= 4u && w.code <= 6u) {
+        // a box face: the point in the box frame put on the face's plane, then back to the world
+        // (as lin_prim_rec_op + lin_untransform do).  o + t d in the world frame lands up to ~1e-4
+        // off the face (t from a reciprocal, |t| ~ 1e3), and a grazing inward light-sampling ray
+        // from there re-enters the box at t > tmin: +0.35% rays (measured).
+        const float t = w.closest;
+        float px = ox + t * dx, py = my + t * r.d.y, pz = oz + t * dz;
+        const float pl = w.code == 4u ? (w.ns < 0.0f ? bo.f[6] : bo.f[9])
+                       : w.code == 5u ? (w.ns < 0.0f ? bo.f[7] : bo.f[10])
+                                      : (w.ns < 0.0f ? bo.f[8] : bo.f[11]);
+        px = w.code == 4u ? pl : px;
+        py = w.code == 5u ? pl : py;
+        pz = w.code == 6u ? pl : pz;
+        p = f3{(c * px + s * pz) + io.f[8], py + io.f[9], (c * pz - s * px) + io.f[10]};
+    }
+    rec.p = p;
+    const uint32_t a = w.code >= 4u ? w.code - 4u : w.code - 1u;
+    const float lx = a == 0u ? w.ns : 0.0f, ly = a == 1u ? w.ns : 0.0f, lz = a == 2u ? w.ns : 0.0f;
+    f3 n{lx, ly, lz};
+    if (w.code >= 4u) n = f3{c * lx + s * lz, ly, c * lz - s * lx};  // unrotate_rec's normal
+    if (w.code == 7u) {
+        const MRT_CONST_AS LinOp& so = prog[17];
+        n = divf(sub(p, f3{so.f[0], so.f[1], so.f[2]}), so.f[8]);
+    }
+    rec.n = n;
+    return true;
+}
+
 // scene_object::hit for a program of shape SIG (same contract as scene_hit_lin)
 template <uint32_t F>
 MRT_DFN bool scene_hit_sig(const DScene& S, Ray& r, float tmin, HitRec& rec, const LStack& L) {
     constexpr uint32_t SIG = MRT_SIG_OF(F);
     constexpr bool INST = (F & FT_INST) != 0;
+    if constexpr (MRT_FAST_BOX && SIG == SIG_CORNELL && !(F & (FT_UV | FT_MOVING))) {
+        const MRT_CONST_AS LinOp* prog = const_ptr(S.prog);
+        if (LOP_FLAGS(prog[8]) & MRT_F_BOX6) return cornell_fast_hit<F>(prog, r, tmin, rec);  // uniform
+    }
     if (INST) lin_save_ray(L, r);
     const MRT_CONST_AS LinOp* prog = const_ptr(S.prog);
     SigState w;
