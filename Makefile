@@ -19,7 +19,9 @@ OBJDIR   = build/obj
 LIB_OBJS = $(OBJDIR)/mrt_render.o $(OBJDIR)/mrt_kernels_exact.o $(OBJDIR)/mrt_kernels_fast.o $(OBJDIR)/mrt_cpu.o $(OBJDIR)/scene_builder.o $(OBJDIR)/mrt_common.o
 # the path kernels twice: exact contract (no contraction, IEEE division) and tolerance contract
 # (FMA contraction, reciprocal division, hardware rcp/sqrt/rsq, f32 transcendentals)
-FASTFLAGS = -DMRT_FAST=1 -ffp-contract=fast -freciprocal-math
+# (-fno-hip-fp32-correctly-rounded-divide-sqrt: f32 division by v_rcp_f32 + multiply instead of
+# the 10-instruction IEEE sequence; -freciprocal-math alone does not lower it)
+FASTFLAGS = -DMRT_FAST=1 -ffp-contract=fast -freciprocal-math -fno-hip-fp32-correctly-rounded-divide-sqrt
 HDRS     = include/mrt.h include/mrt_scene.h include/mrt_mathfn.h $(wildcard $(CSRC)/*.h) Makefile
 
 all: miniraytracer_amd/libmrt.so bin/mrt oracle/liboracle.so

@@ -7,8 +7,8 @@
 // Each build exports its KernelTable (mrt_launch.h); the host picks one per render
 // (mrt_render_desc.flags & MRT_RF_FAST).
 //
-// mrt_path_kernel: persistent waves pull 256-path batches (64 near the end of a launch) from one
-// device counter (one atomic per wave per batch, like work_queue::getWork pulls a tile,
+// mrt_path_kernel: persistent waves pull 256-path batches (64 near the end of a launch) from
+// per-XCD partition counters (one atomic per wave per batch, like work_queue::getWork pulls a tile,
 // work_queue.cpp:158-166) and run trace() for each lane's path to completion; per-path radiance
 // is written sample-major [s][local pixel] (coalesced).
 #include <hip/hip_runtime.h>
@@ -106,13 +106,22 @@ template <uint32_t F> struct PathLevLds {
                                   : ((F & FT_MESH) != 0)               ? MRT_LEVK_MESH
                                                                        : 0u;
 };
+// Path starts made a wave at a time (see the path loop): on in the tolerance-contract build for the
+// shared-constructor loop of one-wave workgroups
+#ifndef MRT_PATHQ
+#define MRT_PATHQ MRT_FAST
+#endif
+template <uint32_t F> struct PathQ {
+    static constexpr bool on = MRT_PATHQ && (F & FT_MESH) == 0 && !TreeOf<F>::on;
+    static constexpr uint32_t words = on ? 12u : 0u;  // LDS words per lane slot: o, dir, time, PCG state + inc, index
+};
 template <uint32_t F>
 __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per_eu(MRT_OCC(F)))) MRT_PATH_KERNEL(PathParams P) {
     constexpr uint32_t LK = PathLevLds<F>::K;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t words = (P.lds_frames * 2 + P.lds_rays * 11 + P.lds_mesh + P.lds_save + LK * 4) * 64;
+    const uint32_t words = (P.lds_frames * 2 + P.lds_rays * 11 + P.lds_mesh + P.lds_save + LK * 4 + PathQ<F>::words) * 64;
     uint32_t* wb = lds + wave * words;
     uint32_t* const wmesh = wb + P.lds_frames * 128 + P.lds_rays * 704;
     float4* tree = nullptr;
@@ -125,6 +134,8 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
     }
     const LStack Ls{wb, (float*)(wb + P.lds_frames * 128), wmesh, (float*)(wmesh + P.lds_mesh * 64), lane, tree,
                     TreeOf<F>::on ? P.tree_n : 0u};
+    // the wave's queue of path starts ([word][entry], PathQ): after the fold levels
+    float* const Lq = (float*)(wmesh + (P.lds_mesh + P.lds_save + LK * 4) * 64);
     const DScene& S = P.sc;
     const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const LevStore<LK> lev{(MRT_GLOBAL_AS v4f*)P.lev, P.lev_rows, (uint32_t)slot,
@@ -140,15 +151,27 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
     bool active = false;
     uint32_t idx = 0;
     PathState ps;
-    // every wave's first claim is static (wave w: paths [w*B, (w+1)*B)); the work counter hands
-    // out what follows, so a launch does not open with one atomic per wave on one address
-    // (short launches only -- P.static_first, set by the host when a wave gets fewer than 64
-    // claims: there the opening atomics are a visible share; in long launches the static batch of
-    // a wave that starts late in a pipelined step delays that launch's end)
-    const uint64_t static_paths = P.static_first ? (uint64_t)gridDim.x * (blockDim.x >> 6) * MRT_BATCH : 0;
-    uint64_t pool_next = P.static_first ? ((uint64_t)blockIdx.x * (blockDim.x >> 6) + wave) * MRT_BATCH : 0;  // wave-uniform
-    uint64_t pool_end = P.static_first ? pool_next + MRT_BATCH : 0;
-    bool exhausted = P.static_first && pool_next >= P.n_paths;
+    // The launch's paths are split into MRT_NPART equal contiguous partitions, one work counter
+    // each (128 B apart): the waves of workgroup b start on partition b % MRT_NPART -- the XCD the
+    // workgroup is dispatched to, round robin -- and move on to the next partition once theirs is
+    // handed out.  One counter for all 7168 waves serialised ~1 M claims per C2 launch on one
+    // address (measured: claims 4x larger, 1024 paths, made the kernel 14% faster).
+    // Every wave's first claim is static (the waves of a partition take its first batches in order);
+    // its counter hands out what follows, so a launch does not open with one atomic per wave (short
+    // launches only -- P.static_first, set by the host when a wave gets fewer than 64 claims: there
+    // the opening atomics are a visible share; in long launches the static batch of a wave that
+    // starts late in a pipelined step delays that launch's end).
+    auto umin64 = [](uint64_t a, uint64_t b) -> uint64_t { return a < b ? a : b; };
+    const uint32_t wpb = blockDim.x >> 6;  // waves per workgroup
+    uint32_t part = blockIdx.x % MRT_NPART;  // wave-uniform: the partition claims come from
+    uint32_t part_tries = 0;                 // partitions found handed out
+    bool in_tail = false;                    // the partition's last paths: small claims
+    uint64_t pool_next = 0, pool_end = 0;    // wave-uniform: the wave's claimed, not yet taken paths
+    if (P.static_first) {
+        pool_next = umin64(P.part_base[part] + ((uint64_t)(blockIdx.x / MRT_NPART) * wpb + wave) * MRT_BATCH, P.part_base[part + 1]);
+        pool_end = umin64(pool_next + MRT_BATCH, P.part_base[part + 1]);
+    }
+    bool exhausted = false;  // no paths left in the pool nor in any partition
     uint32_t done_rays = 0;
     PhaseClock ph{};
 #ifdef MRT_PHASES
@@ -158,70 +181,100 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
     // compaction), the pool refilled by one atomic per claim (work_queue::getWork,
     // work_queue.cpp:158-166).  start(u, v) begins a lane's path at camera coordinates (u, v) with
     // its PCG stream seeded from the path key.
+    // path index -> its camera coordinates (u, v) and its PCG stream seeded from the path key
+    auto path_key = [&](uint32_t i, Pcg& rng, float* uo, float* vo) {
+        // i = sl * npix + lp; the double estimate is off by at most one either way
+        uint32_t sl = (uint32_t)((double)i * P.inv_npix);
+        uint32_t lp = i - sl * P.npix;
+        if ((int32_t)lp < 0) { sl--; lp += P.npix; }
+        if (lp >= P.npix) { sl++; lp -= P.npix; }
+        const uint32_t s = P.s0 + sl;
+        const uint2 xy = P.pixels[lp];
+        const uint32_t x = xy.x, y = xy.y;
+        const uint32_t pix = x + y * P.width;
+        const float2 dd = P.sdist[s];  // ((i + 0.5) / sq, (j + 0.5) / sq), s = i*sq + j
+        // (x + dx) / W with RN(1/W) from the host: numerator >= 1/(2 sq) >= 2^-17, W <= 2^24
+        const float nu = (float)x + dd.x, nv = (float)y + dd.y;
+        float u = div_core(nu, (float)P.width, P.inv_w), v = div_core(nv, (float)P.height, P.inv_h);
+        if (!P.fast_uv) {  // a real (uniform) branch: the barrier keeps it from being if-converted
+            asm volatile("" ::: "memory");
+            u = nu / (float)P.width;
+            v = nv / (float)P.height;
+        }
+        const uint64_t path_id = (uint64_t)pix * P.ns + s;
+        pcg_seed(rng, splitmix64(P.seed ^ path_id), path_id);
+        *uo = u;
+        *vo = v;
+    };
+    // the next c path indices of the wave's pool, the lane of rank r taking index *i (>= n_paths:
+    // none); the pool refilled by one atomic per claim (work_queue::getWork, work_queue.cpp:158-166)
+    auto claim = [&](uint32_t c, uint32_t r, bool want, uint64_t* i) {
+        const uint32_t have = (uint32_t)(pool_end - pool_next);
+        uint64_t nb = 0, ne = 0;
+        if (have < c) {
+            while (part_tries < MRT_NPART) {  // wave-uniform
+                const uint64_t pe = P.part_base[part + 1], p0 = P.part_dyn[part];
+                const uint32_t batch = in_tail ? MRT_TAIL_BATCH : MRT_BATCH;
+                if (lane == 0) {
+                    nb = p0 + atomicAdd(P.counter + part * MRT_COUNTER_STRIDE, (unsigned long long)batch);
+                    // every 32nd claim: a system-scope store to host memory, read by mrt_progress
+                    // without any GPU queue (a device-to-host copy could wait behind this launch)
+                    if (P.hprog && (((nb - p0) / batch) & 31u) == 0)
+                        __hip_atomic_store(P.hprog + part, nb + batch - P.part_base[part], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+                // lane 0's claim to every lane, as a scalar (the whole wave runs claim())
+                nb = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(nb >> 32)) << 32) |
+                     (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)nb);
+                if (nb < pe) {
+                    ne = umin64(nb + batch, pe);
+                    // near the partition's end, claims shrink so the last ones finish together
+                    in_tail = in_tail || pe - ne <= P.tail_zone / MRT_NPART;
+                    break;
+                }
+                part_tries++;
+                part = (part + 1) % MRT_NPART;
+                in_tail = false;
+            }
+        }
+        if (want) {
+            const uint64_t j = nb + (r - have);
+            *i = r < have ? pool_next + r : (j < ne ? j : ~0ull);
+        }
+        if (have < c) {
+            pool_next = umin64(nb + (c - have), ne);
+            pool_end = ne;
+        } else {
+            pool_next += c;
+        }
+        exhausted = part_tries >= MRT_NPART && pool_next >= pool_end;
+    };
+    auto begin_path = [&]() {
+        ps.depth = 0;
+        ps.nlev = 0;
+#if MRT_FWD_FOLD
+        ps.T = f3{1.0f, 1.0f, 1.0f};
+#endif
+        ps.rays = 0;
+        active = true;
+    };
+    // Lanes without a path take the next path indices from the wave's pool (ballot + mbcnt
+    // compaction).  start(u, v) begins a lane's path at camera coordinates (u, v).
     auto take_paths = [&](auto&& start) {
         const uint64_t need = __ballot(!active);
         if (!need || exhausted) return;
         const uint32_t c = (uint32_t)__popcll(need);
-        const uint32_t have = (uint32_t)(pool_end - pool_next);
-        // near the end of the launch, claims shrink so the last ones finish together
-        const uint32_t batch = pool_end + P.tail_zone >= P.n_paths ? MRT_TAIL_BATCH : MRT_BATCH;
-        uint64_t nb = 0;
-        if (have < c) {
-            if (lane == 0) {
-                nb = static_paths + atomicAdd(P.counter, (unsigned long long)batch);
-                // every 32nd claim: a system-scope store to host memory, read by mrt_progress
-                // without any GPU queue (a device-to-host copy could wait behind this launch)
-                if (P.hprog && ((nb / MRT_BATCH) & 31u) == 0)
-                    __hip_atomic_store(P.hprog, nb + batch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-            nb = __shfl(nb, 0);
-        }
+        uint64_t i = 0;
+        claim(c, active ? 0u : rank_below(need), !active, &i);
         PH_MARK(ph, 0);
-        if (!active) {
-            const uint32_t rank = rank_below(need);
-            const uint64_t i = rank < have ? pool_next + rank : nb + (rank - have);
-            if (i < P.n_paths) {
-                idx = (uint32_t)i;
-                // idx = sl * npix + lp; the double estimate is off by at most one either way
-                uint32_t sl = (uint32_t)((double)idx * P.inv_npix);
-                uint32_t lp = idx - sl * P.npix;
-                if ((int32_t)lp < 0) { sl--; lp += P.npix; }
-                if (lp >= P.npix) { sl++; lp -= P.npix; }
-                const uint32_t s = P.s0 + sl;
-                const uint2 xy = P.pixels[lp];
-                const uint32_t x = xy.x, y = xy.y;
-                const uint32_t pix = x + y * P.width;
-                const float2 dd = P.sdist[s];  // ((i + 0.5) / sq, (j + 0.5) / sq), s = i*sq + j
-                // (x + dx) / W with RN(1/W) from the host: numerator >= 1/(2 sq) >= 2^-17, W <= 2^24
-                const float nu = (float)x + dd.x, nv = (float)y + dd.y;
-                float u = div_core(nu, (float)P.width, P.inv_w), v = div_core(nv, (float)P.height, P.inv_h);
-                if (!P.fast_uv) {  // a real (uniform) branch: the barrier keeps it from being if-converted
-                    asm volatile("" ::: "memory");
-                    u = nu / (float)P.width;
-                    v = nv / (float)P.height;
-                }
-                BSTAT(10);
-                const uint64_t path_id = (uint64_t)pix * P.ns + s;
-                pcg_seed(ps.rng, splitmix64(P.seed ^ path_id), path_id);
-                start(u, v);
-                ps.depth = 0;
-                ps.nlev = 0;
-#if MRT_FWD_FOLD
-                ps.T = f3{1.0f, 1.0f, 1.0f};
-#endif
-                ps.rays = 0;
-                active = true;
-            }
+        if (!active && i < P.n_paths) {
+            idx = (uint32_t)i;
+            BSTAT(10);
+            float u, v;
+            path_key(idx, ps.rng, &u, &v);
+            start(u, v);
+            begin_path();
         }
         PH_MARK(ph, 4);
-        if (have < c) {
-            pool_next = nb + (c - have);
-            pool_end = nb + batch;
-            if (nb >= P.n_paths) exhausted = true;
-        } else {
-            pool_next += c;
-        }
-        if (pool_next >= P.n_paths) exhausted = true;
     };
     // a finished path: the recursion's fold, radiance out (sample-major, coalesced), rays counted
     auto finish_path = [&](f3 L) {
@@ -252,28 +305,123 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
         // constructor per branch at partial lane occupancy; (4) diffuse scatters finish their pdfs
         // on the new ray.
         PendRay pr;
+        uint32_t q_head = 0, q_n = 0;  // wave-uniform: the queue's next entry, its valid entries
+        // The radiance store of a path that ended is held in registers and issued in the NEXT
+        // iteration, after the hit, beside the material load: the code waits for the vector memory
+        // counter (stores count in vmcnt on gfx950) right after a store wherever it reuses nearby
+        // registers, which stalled the wave for the store's whole round trip every iteration
+        // (measured: SQ_WAIT_ANY 23 -> 36 quad-cycles per ray once the path loop had fewer
+        // instructions); beside the material load the two round trips overlap.
+        f3 st_v{0.0f, 0.0f, 0.0f};
+        uint32_t st_off = 0;  // byte offset of the path's radiance (a launch chunk is < 4 GiB)
+        bool st_pend = false;
         for (;;) {
             bool want_ray = false;
             if (active) {
                 f3 L;
-                const bool ended = trace_split<F, LK>(S, ps, P.max_bounces, lev, Ls, &L, &pr, ph);
+                // (the held store is issued inside, after the hit, beside the material load)
+                const bool ended = trace_split<F, LK>(S, ps, P.max_bounces, lev, Ls, &L, &pr, ph, [&]() {
+                    if (st_pend) {
+                        float* dst = reinterpret_cast<float*>(reinterpret_cast<char*>(P.rad) + st_off);
+                        dst[0] = st_v.x;
+                        dst[1] = st_v.y;
+                        dst[2] = st_v.z;
+                    }
+                    st_pend = false;
+                });
                 PH_MARK(ph, 2);
-                if (ended) finish_path(L);
-                else want_ray = true;
+                if (ended) {
+                    st_v = end_path(ps, lev, L);
+                    st_off = idx * 12u;
+                    st_pend = true;
+                    if (P.path_rays) P.path_rays[idx] = ps.rays;
+                    done_rays += ps.rays;
+                    active = false;
+                } else {
+                    want_ray = true;
+                }
             }
             PH_MARK(ph, 3);
-            take_paths([&](float u, float v) {
-                camera_ray_args(S, ps.rng, u, v, &pr.o, &pr.dir, &pr.time);
-                pr.inside = 0;
-                pr.kind = 0;
-                want_ray = true;
-            });
-            if (!__any(active)) break;
+            if constexpr (PathQ<F>::on) {
+                // new paths from the wave's queue of path starts; when it runs short, the next 64
+                // starts are made at once, one per lane at full width (path key, PCG seeding, the
+                // camera's disk-rejection and time draws), instead of by the ~1/3 of lanes whose
+                // path just ended: the same paths with the same streams, in the same order
+                auto pop = [&](uint32_t e) {
+                    const float* q = Lq + e;
+                    pr.o = f3{q[0], q[64], q[128]};
+                    pr.dir = f3{q[192], q[256], q[320]};
+                    pr.time = q[384];
+                    ps.rng.state = (uint64_t)__float_as_uint(q[448]) | ((uint64_t)__float_as_uint(q[512]) << 32);
+                    ps.rng.inc = (uint64_t)__float_as_uint(q[576]) | ((uint64_t)__float_as_uint(q[640]) << 32);
+                    idx = __float_as_uint(q[704]);
+                    pr.inside = 0;
+                    pr.kind = 0;
+                    want_ray = true;
+                    begin_path();
+                };
+                const uint64_t need = __ballot(!active);
+                const uint32_t c = (uint32_t)__popcll(need);
+                const uint32_t avail = q_n - q_head;
+                if (c != 0u && (avail != 0u || !exhausted)) {
+                    const uint32_t rank = active ? 64u : rank_below(need);
+                    if (rank < avail) pop(q_head + rank);
+                    if (c <= avail) {
+                        q_head += c;
+                    } else {
+                        q_head = q_n = 0;
+                        if (!exhausted) {
+                            uint64_t i = 0;
+                            claim(64u, lane, true, &i);
+                            const bool valid = i < P.n_paths;
+                            if (valid) {
+                                BSTAT(10);
+                                Pcg rng;
+                                float u, v, time;
+                                f3 o, dir;
+                                path_key((uint32_t)i, rng, &u, &v);
+                                camera_ray_args(S, rng, u, v, &o, &dir, &time);
+                                float* q = Lq + lane;
+                                q[0] = o.x; q[64] = o.y; q[128] = o.z;
+                                q[192] = dir.x; q[256] = dir.y; q[320] = dir.z;
+                                q[384] = time;
+                                q[448] = __uint_as_float((uint32_t)rng.state);
+                                q[512] = __uint_as_float((uint32_t)(rng.state >> 32));
+                                q[576] = __uint_as_float((uint32_t)rng.inc);
+                                q[640] = __uint_as_float((uint32_t)(rng.inc >> 32));
+                                q[704] = __uint_as_float((uint32_t)i);
+                            }
+                            q_n = (uint32_t)__popcll(__ballot(valid));  // a prefix of the lanes
+                            const uint32_t r2 = rank - avail;
+                            if (!active && r2 < q_n) pop(r2);
+                            q_head = min(c - avail, q_n);
+                        }
+                    }
+                }
+                PH_MARK(ph, 4);
+            } else {
+                take_paths([&](float u, float v) {
+                    camera_ray_args(S, ps.rng, u, v, &pr.o, &pr.dir, &pr.time);
+                    pr.inside = 0;
+                    pr.kind = 0;
+                    want_ray = true;
+                });
+            }
+            if (!__any(active)) {  // the last store
+                if (st_pend) {
+                    float* dst = reinterpret_cast<float*>(reinterpret_cast<char*>(P.rad) + st_off);
+                    dst[0] = st_v.x;
+                    dst[1] = st_v.y;
+                    dst[2] = st_v.z;
+                }
+                break;
+            }
             PH_MARK(ph, 0);
             BSTATC(15, active);
             if (want_ray) {
                 BSTATC(12, pr.kind != 0);
                 ps.r = make_ray(pr.o, pr.dir, pr.time, pr.inside);
+                PH_MARK(ph, 8);
                 if (pr.kind) finish_scatter<F, LK>(S, ps, lev, pr);
             }
             PH_MARK(ph, 7);
@@ -397,7 +545,11 @@ const KernelTable& mrtd::kernel_table_exact() {
         {TreeOf<kVariants[0]>::wg, TreeOf<kVariants[1]>::wg, TreeOf<kVariants[2]>::wg, TreeOf<kVariants[3]>::wg,
          TreeOf<kVariants[4]>::wg, TreeOf<kVariants[5]>::wg, TreeOf<kVariants[6]>::wg},
         {TreeOf<kVariants[0]>::on, TreeOf<kVariants[1]>::on, TreeOf<kVariants[2]>::on, TreeOf<kVariants[3]>::on,
-         TreeOf<kVariants[4]>::on, TreeOf<kVariants[5]>::on, TreeOf<kVariants[6]>::on}};
+         TreeOf<kVariants[4]>::on, TreeOf<kVariants[5]>::on, TreeOf<kVariants[6]>::on},
+        {PathQ<kVariants[0]>::words, PathQ<kVariants[1]>::words, PathQ<kVariants[2]>::words, PathQ<kVariants[3]>::words,
+         PathQ<kVariants[4]>::words, PathQ<kVariants[5]>::words, PathQ<kVariants[6]>::words},
+        {kBox6Walk<kVariants[0]>, kBox6Walk<kVariants[1]>, kBox6Walk<kVariants[2]>, kBox6Walk<kVariants[3]>,
+         kBox6Walk<kVariants[4]>, kBox6Walk<kVariants[5]>, kBox6Walk<kVariants[6]>}};
     static_assert(kNumVariants == 7, "one table entry per variant");
     return t;
 }

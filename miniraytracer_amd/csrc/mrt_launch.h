@@ -8,6 +8,11 @@
 
 namespace mrtd {
 
+#ifndef MRT_NPART
+#define MRT_NPART 8u  // work partitions (and counters) per launch: one per XCD (mrt_kernels.hip)
+#endif
+#define MRT_COUNTER_STRIDE 16u  // uint64 words between two partitions' counters (128 B)
+
 struct PathParams {
     DScene sc;                            // by value: kernarg (constant) memory, scalar-loaded
     const uint2* __restrict__ pixels;     // local pixel -> (x, y), row 0 = bottom
@@ -19,14 +24,16 @@ struct PathParams {
     uint32_t fast_uv;                     // width, height <= 2^24 and sq <= 2^16: u, v through div_core
     uint32_t s0;                          // first sample of this chunk
     uint32_t n_paths;                     // npix * chunk samples (< 2^32, enforced on the host)
-    uint32_t tail_zone;                   // last paths of the launch handed out MRT_TAIL_BATCH at a time
+    uint32_t tail_zone;                   // last paths of a partition handed out MRT_TAIL_BATCH at a time
+    uint64_t part_base[MRT_NPART + 1];    // work partition k: paths [part_base[k], part_base[k+1])
+    uint64_t part_dyn[MRT_NPART];         // its first path handed out by its counter (after the static claims)
     uint32_t static_first;                // every wave's first claim is static (short launches)
     uint64_t seed;
     uint32_t max_bounces;
     float* __restrict__ rad;              // n_paths * 3 floats, [s - s0][lp]
     uint32_t* __restrict__ path_rays;     // optional (debug): n_paths
-    unsigned long long* __restrict__ counter;  // work counter (paths handed out)
-    unsigned long long* hprog;            // host-coherent pinned snapshot of `counter` (mrt_progress), or null
+    unsigned long long* __restrict__ counter;  // MRT_NPART work counters, MRT_COUNTER_STRIDE apart (paths handed out)
+    unsigned long long* hprog;            // host-coherent pinned snapshots, one per partition (mrt_progress), or null
     const int* cancel;                    // device flag: non-zero makes the launch exit (G_isRunning)
     unsigned long long* __restrict__ rays;
     float4* __restrict__ lev;             // fold levels, lane-major: [slot][lev_rows]
@@ -70,6 +77,8 @@ struct KernelTable {
     uint32_t lev_k[kNumVariants];
     uint32_t wg[kNumVariants];    // threads per workgroup
     uint32_t tree[kNumVariants];  // 1: the kernel reads the top BvhWide nodes from an LDS treelet
+    uint32_t pq[kNumVariants];    // LDS words per lane slot of the kernel's queue of path starts
+    uint32_t box6_walk[kNumVariants];  // 1: Cornell shape walked by cornell_fast_hit when op 8 is MRT_F_BOX6
 };
 const KernelTable& kernel_table_exact();
 const KernelTable& kernel_table_fast();

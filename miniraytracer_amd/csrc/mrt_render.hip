@@ -1,7 +1,7 @@
 // mrt_render.hip -- the MI355X render path behind the C-ABI (include/mrt.h).
 //
 // Kernels (DESIGN.md "Kernels"):
-//   mrt_path_kernel   persistent waves pull 256-path batches (64 near the end of a launch) from one device counter (one atomic
+//   mrt_path_kernel   persistent waves pull 256-path batches (64 near the end of a launch) from per-XCD partition counters (one atomic
 //                     per wave per batch, like work_queue::getWork pulls a tile,
 //                     work_queue.cpp:158-166) and run trace() for each lane's path to completion;
 //                     per-path radiance is written sample-major [s][local pixel] (coalesced).
@@ -141,6 +141,7 @@ struct PathLaunch {
     uint32_t vgprs = 0;
     uint32_t wg = 64;     // threads per workgroup
     uint32_t tree_n = 0;  // BvhWide nodes kept in each workgroup's LDS (treelet kernels)
+    uint32_t lds_save = 0;  // LDS words per lane slot for the query ray parked during instances
 };
 
 // Wide nodes renumbered breadth-first over all roots together (level 0 of every tree, then level
@@ -776,8 +777,11 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
         L.fn = tabs[k]->kernel[s->variant];
         L.wg = tabs[k]->wg[s->variant];
         const uint32_t waves_per_wg = L.wg / 64u;
+        // the Cornell walk of the tolerance contract (mrt_sig.h cornell_fast_hit) parks no ray
+        L.lds_save = tabs[k]->box6_walk[s->variant] ? 0u : s->lds_save;
         L.lds_bytes = (size_t)waves_per_wg * 64 * 4 *
-                      (s->lds_frames * 2 + s->lds_rays * 11 + s->lds_mesh + s->lds_save + tabs[k]->lev_k[s->variant] * 4);
+                      (s->lds_frames * 2 + s->lds_rays * 11 + s->lds_mesh + L.lds_save + tabs[k]->lev_k[s->variant] * 4 +
+                       tabs[k]->pq[s->variant]);
         if (L.lds_bytes > (size_t)prop.sharedMemPerBlock) {
             mrt_scene_free(s);
             return mrt_internal_fail(MRT_ERR_INVALID, "scene graph too deep for the LDS stacks");
@@ -903,6 +907,8 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
     }
     uint32_t chunk = d->chunk_samples ? std::min(d->chunk_samples, ns) : auto_chunk(s->npix, ns);
     chunk = (uint32_t)std::min<uint64_t>(chunk, 0xFFFFFFFFull / std::max<uint32_t>(s->npix, 1));  // 32-bit path index
+    // 32-bit byte offsets of the chunk's radiance (the path kernel's held store, mrt_kernels.hip)
+    chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(chunk, 0xFFFFFFFFull / (12ull * std::max<uint32_t>(s->npix, 1))));
     if (chunk == 0) return mrt_internal_fail(MRT_ERR_INVALID, "image too large for one launch");
     if (d->flags & MRT_RF_PATH_DEBUG) chunk = ns;  // debug keeps every path
     if (chunk != s->chunk && (st = quiesce(s))) return st;  // the fold of a running render reads `chunk` rows
@@ -937,7 +943,8 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
     s->lev_rows = std::max<uint32_t>(d->max_bounces, 1);
     if ((st = grow(s, (void**)&s->d_lev, &s->lev_cap, (size_t)s->lev_rows * s->max_threads * 16))) return st;
     uint32_t launches = (ns + s->chunk - 1) / s->chunk;
-    if ((st = grow(s, (void**)&s->d_counters, &s->cnt_cap, (size_t)launches * 8))) return st;
+    const size_t cnt_words = (size_t)MRT_NPART * MRT_COUNTER_STRIDE;  // per launch
+    if ((st = grow(s, (void**)&s->d_counters, &s->cnt_cap, (size_t)launches * cnt_words * 8))) return st;
     if (!s->pstream) HIPCHK(hipStreamCreateWithFlags(&s->pstream, hipStreamNonBlocking));
     if (!s->ev_done) HIPCHK(hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming));
     {
@@ -947,10 +954,10 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
             if (s->h_prog) (void)hipHostFree(s->h_prog);
             s->h_prog = nullptr;
             s->h_prog_cap = 0;
-            HIPCHK(hipHostMalloc((void**)&s->h_prog, (size_t)launches * 8, hipHostMallocPortable | hipHostMallocCoherent));
+            HIPCHK(hipHostMalloc((void**)&s->h_prog, (size_t)launches * MRT_NPART * 8, hipHostMallocPortable | hipHostMallocCoherent));
             s->h_prog_cap = launches;
         }
-        if (s->h_seen.size() < (size_t)launches) s->h_seen.resize(launches, 0);
+        if (s->h_seen.size() < (size_t)launches * MRT_NPART) s->h_seen.resize((size_t)launches * MRT_NPART, 0);
         if (s->chunk_paths.size() < launches) s->chunk_paths.resize(launches, 0);
         while (s->ev.size() < 2 * (size_t)launches) {
             hipEvent_t e;
@@ -978,14 +985,16 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
     uint32_t ns = d->sqrt_samples * d->sqrt_samples;
     HIPCHK(hipMemsetAsync(s->d_acc, 0, (size_t)s->npix * 16, q));
     const uint32_t launches = (ns + s->chunk - 1) / s->chunk;
-    HIPCHK(hipMemsetAsync(s->d_counters, 0, (size_t)launches * 8, q));
+    HIPCHK(hipMemsetAsync(s->d_counters, 0, (size_t)launches * MRT_NPART * MRT_COUNTER_STRIDE * 8, q));
     HIPCHK(hipMemsetAsync(s->d_counter + 4, 0, 8, q));  // cancel flag
     {
         std::lock_guard<std::mutex> lk(s->prog_mu);
         for (uint32_t k = 0; k < launches; k++) {
             s->chunk_paths[k] = (uint64_t)s->npix * (std::min(ns, (k + 1) * s->chunk) - k * s->chunk);
-            __atomic_store_n(&s->h_prog[k], (uint64_t)0, __ATOMIC_RELAXED);
-            s->h_seen[k] = 0;
+            for (uint32_t j = 0; j < MRT_NPART; j++) {
+                __atomic_store_n(&s->h_prog[(size_t)k * MRT_NPART + j], (uint64_t)0, __ATOMIC_RELAXED);
+                s->h_seen[(size_t)k * MRT_NPART + j] = 0;
+            }
         }
     }
     s->n_launch = 0;
@@ -1005,7 +1014,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.lds_frames = s->lds_frames;
         P.lds_rays = s->lds_rays;
         P.lds_mesh = s->lds_mesh;
-        P.lds_save = s->lds_save;
+        P.lds_save = PL.lds_save;
         P.tree_src = reinterpret_cast<const float4*>(s->S.bwide);
         P.tree_n = PL.tree_n;
         P.pixels = s->d_pixels;
@@ -1023,12 +1032,19 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.n_paths = s->npix * (s1 - s0);
         P.tail_zone = (uint32_t)std::min<uint64_t>((uint64_t)PL.grid * (PL.wg / 64u) * 2 * MRT_BATCH, P.n_paths);  // ~2 big claims per wave
         P.static_first = (uint64_t)P.n_paths < (uint64_t)PL.grid * (PL.wg / 64u) * MRT_BATCH * 64u;
+        // MRT_NPART contiguous work partitions, one counter each; the waves of partition k (workgroups
+        // b with b % MRT_NPART == k) take its first batches statically when P.static_first
+        for (uint32_t k = 0; k <= MRT_NPART; k++) P.part_base[k] = (uint64_t)P.n_paths * k / MRT_NPART;
+        for (uint32_t k = 0; k < MRT_NPART; k++) {
+            const uint64_t waves_k = (uint64_t)((PL.grid - k + MRT_NPART - 1) / MRT_NPART) * (PL.wg / 64u);
+            P.part_dyn[k] = P.part_base[k] + (P.static_first ? waves_k * MRT_BATCH : 0);
+        }
         P.seed = d->seed;
         P.max_bounces = d->max_bounces;
         P.rad = s->d_rad;
         P.path_rays = (d->flags & MRT_RF_PATH_DEBUG) ? s->d_path_rays : nullptr;
-        P.counter = (unsigned long long*)(s->d_counters + s->n_launch);
-        P.hprog = (unsigned long long*)(s->h_prog + s->n_launch);
+        P.counter = (unsigned long long*)(s->d_counters + (size_t)s->n_launch * MRT_NPART * MRT_COUNTER_STRIDE);
+        P.hprog = (unsigned long long*)(s->h_prog + (size_t)s->n_launch * MRT_NPART);
         P.cancel = (const int*)(s->d_counter + 4);
         P.rays = d_rays ? (unsigned long long*)d_rays : s->d_rays;
         P.lev = s->d_lev;
@@ -1125,18 +1141,22 @@ extern "C" mrt_status mrt_progress(mrt_scene* s, float* pct) {
     if (s->cpu) return mrt_cpu_progress(s->cpu, pct);
     std::lock_guard<std::mutex> lk(s->prog_mu);
     const size_t n = s->n_chunks.load(std::memory_order_acquire);
-    if (n == 0 || !s->h_prog || s->h_prog_cap < n || s->ev.size() < 2 * n || s->h_seen.size() < n) return MRT_OK;  // not started
+    if (n == 0 || !s->h_prog || s->h_prog_cap < n || s->ev.size() < 2 * n || s->h_seen.size() < n * MRT_NPART) return MRT_OK;  // not started
     double done = 0, total = 0;
     for (size_t k = 0; k < n; k++) {
         total += (double)s->chunk_paths[k];
         if (hipEventQuery(s->ev[2 * k + 1]) == hipSuccess) {
             done += (double)s->chunk_paths[k];
         } else if (hipEventQuery(s->ev[2 * k]) == hipSuccess) {
-            // snapshots from different waves land out of order: report the largest seen so far
-            uint64_t c = __atomic_load_n(&s->h_prog[k], __ATOMIC_RELAXED);
-            c = std::max(c, s->h_seen[k]);
-            s->h_seen[k] = c;
-            done += (double)std::min<uint64_t>(c, s->chunk_paths[k]);
+            // one snapshot per work partition (the paths it has handed out); snapshots from
+            // different waves land out of order: report the largest seen so far
+            const uint64_t np = s->chunk_paths[k];
+            for (uint32_t j = 0; j < MRT_NPART; j++) {
+                uint64_t c = __atomic_load_n(&s->h_prog[k * MRT_NPART + j], __ATOMIC_RELAXED);
+                c = std::max(c, s->h_seen[k * MRT_NPART + j]);
+                s->h_seen[k * MRT_NPART + j] = c;
+                done += (double)std::min<uint64_t>(c, np * (j + 1) / MRT_NPART - np * j / MRT_NPART);
+            }
         }
     }
     *pct = total > 0 ? (float)std::min(100.0, done * 100.0 / total) : 0.0f;

@@ -132,7 +132,10 @@ MRT_DFN float leaf_pdf_value(const DScene& S, const mrt_node& n, f3 origin, f3 d
 template <uint32_t F>
 MRT_DFN float biased_pdf_value(const DScene& S, f3 origin, f3 dir, float time) {
     const MRT_CONST_AS mrt_node* bl = const_ptr(S.bleaf);
-    if (!S.blist) {
+    // one leaf (also a list of one, as the Cornell box's and book2's biased lists are,
+    // scene.cpp:326-329, 456-459): (0 + v) / 1 == v for the pdf values v >= +0 leaves return;
+    // one 64-B scalar load, no loop of dependent kind / field loads
+    if (!S.blist || S.nbleaf == 1) {
         const mrt_node n = ld_node(bl);
         return leaf_pdf_value<F>(S, n, origin, dir, time);
     }
@@ -429,9 +432,11 @@ struct PendRay {
 
 // trace_segment up to the next ray's constructor arguments.  Returns true when the path has
 // ended (radiance in *L); otherwise *pr holds the next ray's arguments.
-template <uint32_t F, uint32_t LK>
+// `flush` runs once the hit is known, before the material is read (the path loop issues the
+// previous path's radiance store there).
+template <uint32_t F, uint32_t LK, typename FLUSH>
 MRT_DFN bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev,
-                                            const LStack& Ls, f3* L, PendRay* pr, PhaseClock& ph) {
+                                            const LStack& Ls, f3* L, PendRay* pr, PhaseClock& ph, FLUSH&& flush) {
     ps.rays++;
     HitRec rec;
     Ray& r = ps.r;
@@ -440,6 +445,7 @@ MRT_DFN bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, c
     else if constexpr ((F & FT_LIN) != 0) hit = scene_hit_lin<F>(S, r, 0.001f, rec, Ls, ps.rng, ph);
     else hit = scene_hit<F>(S, r, 0.001f, rec, ps.rng, Ls);
     PH_MARK(ph, 1);
+    flush();
     BSTAT(0);
     BSTATC(14, hit);
     if (!hit) {

@@ -53,6 +53,9 @@ inline uint32_t lin_sig_of(const LinOp* prog, uint32_t n) {
             ok = op == g.op[i] && (op == LOP_END || kind == g.kind[i]) &&
                  ((op != LOP_LIST && op != LOP_INST) || prog[i].skip == g.skip[i]);
         }
+        // the Cornell shape's box must be box.h's six rects (MRT_F_BOX6, set on upload): the
+        // tolerance-contract kernel walks it as one slab test with no fallback (cornell_fast_hit)
+        if (ok && id == SIG_CORNELL) ok = ((prog[8].code >> 16) & MRT_F_BOX6) != 0;
         if (ok) return id;
     }
     return SIG_NONE;
@@ -238,19 +241,80 @@ struct CornellRec {
     float closest, k, ns;
     uint32_t code, mat;  // code: 0 none; 1-3 world rect of axis code-1 (plane k); 4-6 box face of axis code-4; 7 sphere
 };
+// A rect op's words (its LinOp's mat and f[0..5]) loaded into SGPRs.  The walk loads all six rects'
+// words as one batch and takes them at one point (the asms, issued back to back after the loads): one
+// scalar-cache round trip for the walls -- the compiler otherwise loaded each op's fields in two
+// dependent rounds, the material lazily inside a branch on the hit (12 round trips for the walls).
+struct CornellRect {
+    uint32_t mat, b0, b1, b2, b3, k, ns;
+};
+MRT_DFN CornellRect cornell_load(const MRT_CONST_AS LinOp& o) {
+    const MRT_CONST_AS uint32_t* q = reinterpret_cast<const MRT_CONST_AS uint32_t*>(&o);
+    return CornellRect{q[3], q[4], q[5], q[6], q[7], q[8], q[9]};
+}
+MRT_DFN void cornell_take1(CornellRect& d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+s"(d.mat), "+s"(d.b0), "+s"(d.b1), "+s"(d.b2), "+s"(d.b3), "+s"(d.k), "+s"(d.ns));
+#else
+    (void)d;
+#endif
+}
+// translate(rotate_y(box)): rotate_y's (sin, cos), translate's offset (op 7), the box's planes
+// and material (op 8); the sphere's centre, radius and material (op 17)
+struct CornellBox {
+    uint32_t s, c, o0, o1, o2, lo0, lo1, lo2, hi0, hi1, hi2, mat;
+};
+struct CornellSphere {
+    uint32_t c0, c1, c2, rad, mat;
+};
+MRT_DFN CornellBox cornell_load_box(const MRT_CONST_AS LinOp& io, const MRT_CONST_AS LinOp& bo) {
+    const MRT_CONST_AS uint32_t* qi = reinterpret_cast<const MRT_CONST_AS uint32_t*>(&io);
+    const MRT_CONST_AS uint32_t* qb = reinterpret_cast<const MRT_CONST_AS uint32_t*>(&bo);
+    return CornellBox{qi[10], qi[11], qi[12], qi[13], qi[14], qb[10], qb[11], qb[12], qb[13], qb[14], qb[15], qb[3]};
+}
+MRT_DFN CornellSphere cornell_load_sphere(const MRT_CONST_AS LinOp& so) {
+    const MRT_CONST_AS uint32_t* q = reinterpret_cast<const MRT_CONST_AS uint32_t*>(&so);
+    return CornellSphere{q[4], q[5], q[6], q[12], q[3]};
+}
+MRT_DFN void cornell_take1(CornellBox& d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+s"(d.s), "+s"(d.c), "+s"(d.o0), "+s"(d.o1), "+s"(d.o2), "+s"(d.mat));
+    asm volatile("" : "+s"(d.lo0), "+s"(d.lo1), "+s"(d.lo2), "+s"(d.hi0), "+s"(d.hi1), "+s"(d.hi2));
+#else
+    (void)d;
+#endif
+}
+MRT_DFN void cornell_take1(CornellSphere& d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+s"(d.c0), "+s"(d.c1), "+s"(d.c2), "+s"(d.rad), "+s"(d.mat));
+#else
+    (void)d;
+#endif
+}
+template <typename... D>
+MRT_DFN void cornell_take(D&... d) {
+    (cornell_take1(d), ...);
+}
 template <uint32_t F, uint32_t PC>
-MRT_DFN void cornell_rect(const MRT_CONST_AS LinOp* prog, const Ray& r, float tmin, CornellRec& w) {
+MRT_DFN void cornell_rect(const CornellRect& d, const Ray& r, float tmin, CornellRec& w) {
     constexpr uint32_t KIND = kSigs[SIG_CORNELL].kind[PC];
     static_assert(kSigs[SIG_CORNELL].op[PC] == LOP_PRIM && KIND != MRT_K_SPHERE, "Cornell shape: world rect");
     constexpr uint32_t AX = KIND == MRT_K_XY ? 2u : KIND == MRT_K_XZ ? 1u : 0u;
-    const MRT_CONST_AS LinOp& o = prog[PC];
+    LinOp o;
+    o.code = 0;  // (lin_prim_t reads the flags only under the exact contract's guards)
+    o.f[0] = __uint_as_float(d.b0);
+    o.f[1] = __uint_as_float(d.b1);
+    o.f[2] = __uint_as_float(d.b2);
+    o.f[3] = __uint_as_float(d.b3);
+    o.f[4] = __uint_as_float(d.k);
+    o.f[5] = __uint_as_float(d.ns);
     float t;
     const bool h = lin_prim_t<F, KIND>(o, r, tmin, w.closest, &t);
     w.closest = h ? t : w.closest;
     w.code = h ? 1u + AX : w.code;
     w.k = h ? o.f[4] : w.k;
     w.ns = h ? o.f[5] : w.ns;
-    w.mat = h ? o.mat : w.mat;
+    w.mat = h ? d.mat : w.mat;
 }
 template <uint32_t F>
 MRT_DFN bool cornell_fast_hit(const MRT_CONST_AS LinOp* prog, const Ray& r, float tmin, HitRec& rec) {
@@ -259,23 +323,30 @@ MRT_DFN bool cornell_fast_hit(const MRT_CONST_AS LinOp* prog, const Ray& r, floa
                       G.op[17] == LOP_PRIM && G.kind[17] == MRT_K_SPHERE,
                   "Cornell shape: translate(rotate_y(box)) at op 7, its six rects under op 8, the sphere at op 17");
     CornellRec w{FLT_MAX_, 0.0f, 0.0f, 0u, 0u};
-    cornell_rect<F, 1>(prog, r, tmin, w);
-    cornell_rect<F, 2>(prog, r, tmin, w);
-    cornell_rect<F, 3>(prog, r, tmin, w);
-    cornell_rect<F, 4>(prog, r, tmin, w);
-    cornell_rect<F, 5>(prog, r, tmin, w);
-    cornell_rect<F, 6>(prog, r, tmin, w);
+    // the six rects' words in one batch of scalar loads, one wait
+    CornellRect d1 = cornell_load(prog[1]), d2 = cornell_load(prog[2]), d3 = cornell_load(prog[3]);
+    CornellRect d4 = cornell_load(prog[4]), d5 = cornell_load(prog[5]), d6 = cornell_load(prog[6]);
+    CornellBox db = cornell_load_box(prog[7], prog[8]);
+    CornellSphere dsp = cornell_load_sphere(prog[17]);
+    cornell_take(d1, d2, d3, d4, d5, d6, db, dsp);
+    cornell_rect<F, 1>(d1, r, tmin, w);
+    cornell_rect<F, 2>(d2, r, tmin, w);
+    cornell_rect<F, 3>(d3, r, tmin, w);
+    cornell_rect<F, 4>(d4, r, tmin, w);
+    cornell_rect<F, 5>(d5, r, tmin, w);
+    cornell_rect<F, 6>(d6, r, tmin, w);
     // the box in its own frame: o' = R(o - offset), d' = R d, R = rotate_y's (s, c)
-    const MRT_CONST_AS LinOp& io = prog[7];
-    const MRT_CONST_AS LinOp& bo = prog[8];
-    const float s = io.f[6], c = io.f[7];
-    const float mx = r.o.x - io.f[8], my = r.o.y - io.f[9], mz = r.o.z - io.f[10];
+    const float s = __uint_as_float(db.s), c = __uint_as_float(db.c);
+    const float off0 = __uint_as_float(db.o0), off1 = __uint_as_float(db.o1), off2 = __uint_as_float(db.o2);
+    const float lo0 = __uint_as_float(db.lo0), lo1 = __uint_as_float(db.lo1), lo2 = __uint_as_float(db.lo2);
+    const float hi0 = __uint_as_float(db.hi0), hi1 = __uint_as_float(db.hi1), hi2 = __uint_as_float(db.hi2);
+    const float mx = r.o.x - off0, my = r.o.y - off1, mz = r.o.z - off2;
     const float ox = c * mx - s * mz, oz = c * mz + s * mx;
     const float dx = c * r.d.x - s * r.d.z, dz = c * r.d.z + s * r.d.x;
     const float ix = recip_nr(dx), iz = recip_nr(dz);
-    const float t0x = (bo.f[6] - ox) * ix, t1x = (bo.f[9] - ox) * ix;
-    const float t0y = (bo.f[7] - my) * r.inv.y, t1y = (bo.f[10] - my) * r.inv.y;
-    const float t0z = (bo.f[8] - oz) * iz, t1z = (bo.f[11] - oz) * iz;
+    const float t0x = (lo0 - ox) * ix, t1x = (hi0 - ox) * ix;
+    const float t0y = (lo1 - my) * r.inv.y, t1y = (hi1 - my) * r.inv.y;
+    const float t0z = (lo2 - oz) * iz, t1z = (hi2 - oz) * iz;
     const float nx = fminf(t0x, t1x), ny = fminf(t0y, t1y), nz = fminf(t0z, t1z);
     const float tn = fmaxf(fmaxf(nx, ny), nz);
     const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
@@ -286,15 +357,20 @@ MRT_DFN bool cornell_fast_hit(const MRT_CONST_AS LinOp* prog, const Ray& r, floa
     w.closest = hb ? tn : w.closest;
     w.code = hb ? 4u + bax : w.code;
     w.ns = hb ? (bd > 0.0f ? -1.0f : 1.0f) : w.ns;
-    w.mat = hb ? bo.mat : w.mat;
+    w.mat = hb ? db.mat : w.mat;
     // the sphere (op 17)
+    LinOp so;
+    so.code = 0;  // (a static sphere: F has no FT_MOVING)
+    so.f[0] = __uint_as_float(dsp.c0);
+    so.f[1] = __uint_as_float(dsp.c1);
+    so.f[2] = __uint_as_float(dsp.c2);
+    so.f[8] = __uint_as_float(dsp.rad);
     {
-        const MRT_CONST_AS LinOp& so = prog[17];
         float t;
         const bool h = lin_prim_t<F, MRT_K_SPHERE>(so, r, tmin, w.closest, &t);
         w.closest = h ? t : w.closest;
         w.code = h ? 7u : w.code;
-        w.mat = h ? so.mat : w.mat;
+        w.mat = h ? dsp.mat : w.mat;
     }
     if (w.code == 0u) return false;
     rec.t = w.closest;
@@ -311,36 +387,36 @@ MRT_DFN bool cornell_fast_hit(const MRT_CONST_AS LinOp* prog, const Ray& r, floa
         // from there re-enters the box at t > tmin: +0.35% rays (measured).
         const float t = w.closest;
         float px = ox + t * dx, py = my + t * r.d.y, pz = oz + t * dz;
-        const float pl = w.code == 4u ? (w.ns < 0.0f ? bo.f[6] : bo.f[9])
-                       : w.code == 5u ? (w.ns < 0.0f ? bo.f[7] : bo.f[10])
-                                      : (w.ns < 0.0f ? bo.f[8] : bo.f[11]);
+        const float pl = w.code == 4u ? (w.ns < 0.0f ? lo0 : hi0)
+                       : w.code == 5u ? (w.ns < 0.0f ? lo1 : hi1)
+                                      : (w.ns < 0.0f ? lo2 : hi2);
         px = w.code == 4u ? pl : px;
         py = w.code == 5u ? pl : py;
         pz = w.code == 6u ? pl : pz;
-        p = f3{(c * px + s * pz) + io.f[8], py + io.f[9], (c * pz - s * px) + io.f[10]};
+        p = f3{(c * px + s * pz) + off0, py + off1, (c * pz - s * px) + off2};
     }
     rec.p = p;
     const uint32_t a = w.code >= 4u ? w.code - 4u : w.code - 1u;
     const float lx = a == 0u ? w.ns : 0.0f, ly = a == 1u ? w.ns : 0.0f, lz = a == 2u ? w.ns : 0.0f;
     f3 n{lx, ly, lz};
     if (w.code >= 4u) n = f3{c * lx + s * lz, ly, c * lz - s * lx};  // unrotate_rec's normal
-    if (w.code == 7u) {
-        const MRT_CONST_AS LinOp& so = prog[17];
-        n = divf(sub(p, f3{so.f[0], so.f[1], so.f[2]}), so.f[8]);
-    }
+    if (w.code == 7u) n = divf(sub(p, f3{so.f[0], so.f[1], so.f[2]}), so.f[8]);
     rec.n = n;
     return true;
 }
+
+// the kernels that walk the Cornell shape by cornell_fast_hit (the host sizes LDS by it)
+template <uint32_t F>
+static constexpr uint32_t kBox6Walk = (MRT_FAST_BOX && MRT_SIG_OF(F) == SIG_CORNELL && !(F & (FT_UV | FT_MOVING))) ? 1u : 0u;
 
 // scene_object::hit for a program of shape SIG (same contract as scene_hit_lin)
 template <uint32_t F>
 MRT_DFN bool scene_hit_sig(const DScene& S, Ray& r, float tmin, HitRec& rec, const LStack& L) {
     constexpr uint32_t SIG = MRT_SIG_OF(F);
     constexpr bool INST = (F & FT_INST) != 0;
-    if constexpr (MRT_FAST_BOX && SIG == SIG_CORNELL && !(F & (FT_UV | FT_MOVING))) {
-        const MRT_CONST_AS LinOp* prog = const_ptr(S.prog);
-        if (LOP_FLAGS(prog[8]) & MRT_F_BOX6) return cornell_fast_hit<F>(prog, r, tmin, rec);  // uniform
-    }
+    if constexpr (kBox6Walk<F>) {  // (the shape implies MRT_F_BOX6 on op 8: lin_sig_of)
+        return cornell_fast_hit<F>(const_ptr(S.prog), r, tmin, rec);
+    } else {
     if (INST) lin_save_ray(L, r);
     const MRT_CONST_AS LinOp* prog = const_ptr(S.prog);
     SigState w;
@@ -383,6 +459,7 @@ MRT_DFN bool scene_hit_sig(const DScene& S, Ray& r, float tmin, HitRec& rec, con
         }
     }
     return true;
+    }
 }
 
 }  // namespace mrtd

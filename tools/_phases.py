@@ -17,7 +17,7 @@ lib().mrt_debug_phases(out, 1)
 img, rays = r.render(d)
 lib().mrt_debug_phases(out, 1)
 v = np.array(list(out), dtype=np.float64)
-names = ["loop+pool", "hit:record", "shade:pdf+lev", "write+bottom", "new path", "fold", "shade:mat+dir", "-", "hit:list/inst", "hit:prim", "hit:volume", "hit:bvh"][:NPH]
+names = ["loop+pool", "hit:record", "shade:pdf+lev", "write+bottom", "new path", "fold", "shade:mat+dir", "-", "make_ray|hit:list/inst", "hit:prim", "hit:volume", "hit:bvh"][:NPH]
 print(f"scene {scene} {w}x{h}x{spp}: rays {rays}")
 for n, x in zip(names, v):
     print(f"  {n:12s} {100 * x / v.sum():6.2f}%")

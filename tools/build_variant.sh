@@ -14,7 +14,10 @@ mkdir -p exp/obj_$tag
 BASE="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-fast-math -fno-slp-vectorize -w -mllvm -disable-promote-alloca-to-vector -mllvm -structurizecfg-skip-uniform-regions -DMRT_EXPERIMENTS"
 /opt/rocm/bin/hipcc $BASE -DMRT_TABLE_FAST=1 $flags -c miniraytracer_amd/csrc/mrt_kernels.hip -o exp/obj_$tag/mrt_kernels_fast.o
 EX=build/obj/mrt_kernels_exact.o
-if [ -n "${EXACT_FLAGS:-}" ]; then
+# host defines (MRT_NPART, MRT_BATCH, ...) change PathParams / the claim protocol: the exact TU must
+# be built with them too, or the exact kernel reads a foreign parameter layout (a GPU memory fault)
+EXACT_FLAGS="${EXACT_FLAGS:-} ${HOST_FLAGS:-}"
+if [ -n "${EXACT_FLAGS// /}" ]; then
   /opt/rocm/bin/hipcc $BASE -ffp-contract=off -DMRT_FAST=0 $EXACT_FLAGS -c miniraytracer_amd/csrc/mrt_kernels.hip -o exp/obj_$tag/mrt_kernels_exact.o
   EX=exp/obj_$tag/mrt_kernels_exact.o
 fi
