@@ -113,7 +113,8 @@ template <uint32_t F> struct PathLevLds {
 #endif
 template <uint32_t F> struct PathQ {
     static constexpr bool on = MRT_PATHQ && (F & FT_MESH) == 0 && !TreeOf<F>::on;
-    static constexpr uint32_t words = on ? 12u : 0u;  // LDS words per lane slot: o, dir, time, PCG state + inc, index
+    // LDS words per lane slot: o, dir, time, PCG state + inc, index (12); + the wave's claim state
+    static constexpr uint32_t words = on ? 13u : 0u;
 };
 template <uint32_t F>
 __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per_eu(MRT_OCC(F)))) MRT_PATH_KERNEL(PathParams P) {
@@ -162,16 +163,45 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
     // the opening atomics are a visible share; in long launches the static batch of a wave that
     // starts late in a pipelined step delays that launch's end).
     auto umin64 = [](uint64_t a, uint64_t b) -> uint64_t { return a < b ? a : b; };
+    // wave-uniform values kept in SGPRs (the compiler otherwise held the pool bounds in VGPRs and
+    // spilled them to scratch, reloaded every claim)
+    auto uni64 = [](uint64_t x) -> uint64_t {
+        return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32)) << 32) |
+               (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+    };
     const uint32_t wpb = blockDim.x >> 6;  // waves per workgroup
     uint32_t part = blockIdx.x % MRT_NPART;  // wave-uniform: the partition claims come from
     uint32_t part_tries = 0;                 // partitions found handed out
     bool in_tail = false;                    // the partition's last paths: small claims
     uint64_t pool_next = 0, pool_end = 0;    // wave-uniform: the wave's claimed, not yet taken paths
     if (P.static_first) {
-        pool_next = umin64(P.part_base[part] + ((uint64_t)(blockIdx.x / MRT_NPART) * wpb + wave) * MRT_BATCH, P.part_base[part + 1]);
-        pool_end = umin64(pool_next + MRT_BATCH, P.part_base[part + 1]);
+        pool_next = uni64(umin64(P.part_base[part] + ((uint64_t)(blockIdx.x / MRT_NPART) * wpb + wave) * MRT_BATCH, P.part_base[part + 1]));
+        pool_end = uni64(umin64(pool_next + MRT_BATCH, P.part_base[part + 1]));
     }
     bool exhausted = false;  // no paths left in the pool nor in any partition
+    // Queue kernels keep the claim state (pool bounds, partition) in LDS between claims -- it is
+    // touched once per 64 path starts -- so it holds no registers across the path loop (held in
+    // registers it cost VGPR spills to scratch: 1.2 GB/launch of extra HBM writes on C2).
+    uint32_t* const Lc = reinterpret_cast<uint32_t*>(Lq + 12u * 64u);
+    auto cold_store = [&]() {
+        if (lane == 0) {
+            Lc[0] = (uint32_t)pool_next;
+            Lc[1] = (uint32_t)(pool_next >> 32);
+            Lc[2] = (uint32_t)pool_end;
+            Lc[3] = (uint32_t)(pool_end >> 32);
+            Lc[4] = part | (part_tries << 8) | ((uint32_t)in_tail << 16);
+        }
+    };
+    auto cold_load = [&]() {
+        auto rd = [&](uint32_t k) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)Lc[k]); };
+        pool_next = (uint64_t)rd(0) | ((uint64_t)rd(1) << 32);
+        pool_end = (uint64_t)rd(2) | ((uint64_t)rd(3) << 32);
+        const uint32_t w = rd(4);
+        part = w & 0xFFu;
+        part_tries = (w >> 8) & 0xFFu;
+        in_tail = ((w >> 16) & 1u) != 0;
+    };
+    if constexpr (PathQ<F>::on) cold_store();
     uint32_t done_rays = 0;
     PhaseClock ph{};
 #ifdef MRT_PHASES
@@ -372,7 +402,9 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                         q_head = q_n = 0;
                         if (!exhausted) {
                             uint64_t i = 0;
+                            cold_load();
                             claim(64u, lane, true, &i);
+                            cold_store();
                             const bool valid = i < P.n_paths;
                             if (valid) {
                                 BSTAT(10);

@@ -237,6 +237,9 @@ struct SigWalk {
 //     face's outward normal rotated back (scene_object.cpp:85-93).  Differs from the reference's
 //     per-face tests and frame round trip by rounding only.
 // Walls and sphere are lin_prim_t's tests in op order (ties to the later op, as closest narrowing).
+#ifndef MRT_CORNELL_BATCHES
+#define MRT_CORNELL_BATCHES 2
+#endif
 struct CornellRec {
     float closest, k, ns;
     uint32_t code, mat;  // code: 0 none; 1-3 world rect of axis code-1 (plane k); 4-6 box face of axis code-4; 7 sphere
@@ -326,6 +329,18 @@ MRT_DFN bool cornell_fast_hit(const MRT_CONST_AS LinOp* prog, const Ray& r, floa
     // the six rects' words in one batch of scalar loads, one wait
     CornellRect d1 = cornell_load(prog[1]), d2 = cornell_load(prog[2]), d3 = cornell_load(prog[3]);
     CornellRect d4 = cornell_load(prog[4]), d5 = cornell_load(prog[5]), d6 = cornell_load(prog[6]);
+#if MRT_CORNELL_BATCHES == 2  // walls, then box + sphere (fewer SGPRs live at once, one more wait)
+    cornell_take(d1, d2, d3, d4, d5, d6);
+    cornell_rect<F, 1>(d1, r, tmin, w);
+    cornell_rect<F, 2>(d2, r, tmin, w);
+    cornell_rect<F, 3>(d3, r, tmin, w);
+    cornell_rect<F, 4>(d4, r, tmin, w);
+    cornell_rect<F, 5>(d5, r, tmin, w);
+    cornell_rect<F, 6>(d6, r, tmin, w);
+    CornellBox db = cornell_load_box(prog[7], prog[8]);
+    CornellSphere dsp = cornell_load_sphere(prog[17]);
+    cornell_take(db, dsp);
+#else
     CornellBox db = cornell_load_box(prog[7], prog[8]);
     CornellSphere dsp = cornell_load_sphere(prog[17]);
     cornell_take(d1, d2, d3, d4, d5, d6, db, dsp);
@@ -335,6 +350,7 @@ MRT_DFN bool cornell_fast_hit(const MRT_CONST_AS LinOp* prog, const Ray& r, floa
     cornell_rect<F, 4>(d4, r, tmin, w);
     cornell_rect<F, 5>(d5, r, tmin, w);
     cornell_rect<F, 6>(d6, r, tmin, w);
+#endif
     // the box in its own frame: o' = R(o - offset), d' = R d, R = rotate_y's (s, c)
     const float s = __uint_as_float(db.s), c = __uint_as_float(db.c);
     const float off0 = __uint_as_float(db.o0), off1 = __uint_as_float(db.o1), off2 = __uint_as_float(db.o2);
