@@ -259,10 +259,19 @@ def main():
             with torch.cuda.stream(streams[j]):
                 rnds[j].render_device(d, outs[j].data_ptr(), rays.data_ptr(), streams[j].cuda_stream)
         torch.cuda.synchronize(dev)
+        tw = time.perf_counter()
         for _ in range(args.warmup):
             step(d)
         drain()
         torch.cuda.synchronize(dev)
+        # clock settle, untimed: a fresh box's GPU ramps its clock over the first few hundred ms
+        # of load (measured: a first C2 run's steps 11.7 ms against 10.0 ms once warm), so
+        # warmup continues until ~0.5 s of GPU work has run, whatever W is
+        # (local renders, no collective: ranks may run different counts before the barrier)
+        while time.perf_counter() - tw < 0.5:
+            with torch.cuda.stream(streams[0]):
+                rnds[0].render_device(d, outs[0].data_ptr(), rays.data_ptr(), streams[0].cuda_stream)
+            torch.cuda.synchronize(dev)
         rays.zero_()
         if world > 1:
             dist.barrier()
