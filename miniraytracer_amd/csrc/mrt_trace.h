@@ -315,19 +315,27 @@ MRT_DFN bool tri_hit(const DScene& S, uint32_t i, const Ray& r, float tmin, floa
         sign = det < 0.0f ? -1.0f : 1.0f;
         det = sign * det;
     }
-    if (det < 0.00001f) return false;
+    // Branch-free: every value is computed whatever the early tests say and the outcome is one
+    // predicate (the reference's early returns only skip work whose result is unused, so the
+    // results are the same bits); a wave's lanes rarely all fail a test, and the nested
+    // branches cost more in exec-mask bookkeeping than they saved (room + mesh kernels)
+    const bool ok_det = !(det < 0.00001f);
     f3 tvec = sub(r.o, m);
     float uu = dot(tvec, pvec) * sign;
     f3 qvec = cross(tvec, u);
     float vv = dot(r.d, qvec) * sign;
-    if ((uu < 0) | (uu > det) | (vv < 0) | ((uu + vv) > det)) return false;
+    const bool ok_uv = !((uu < 0) | (uu > det) | (vv < 0) | ((uu + vv) > det));
+#if MRT_FAST_DIV && defined(__HIP_DEVICE_COMPILE__)
+    float invDet = __builtin_amdgcn_rcpf(det);
+#else
     float invDet = 1 / det;
+#endif
     float t = (dot(v, qvec) * invDet) * sign;
-    if ((t < tmin) | (t > tmax)) return false;
+    const bool ok_t = !((t < tmin) | (t > tmax));
     *tout = t;
     *uout = uu * invDet;
     *vout = vv * invDet;
-    return true;
+    return ok_det & ok_uv & ok_t;
 }
 
 // pod_bvh::hit (triangle.h:171-221): depth-first, closer child first (node_order & dirMask); the
