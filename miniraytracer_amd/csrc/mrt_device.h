@@ -87,6 +87,10 @@ __host__ static inline bool signbit(double x) { return std::signbit(x); }
 #ifndef MRT_FWD_FOLD
 #define MRT_FWD_FOLD MRT_FAST
 #endif
+// slab tests as one fma per plane (aabb_hit), tolerance contract only
+#ifndef MRT_FAST_SLAB
+#define MRT_FAST_SLAB MRT_FAST
+#endif
 
 namespace mrtd {
 
@@ -384,8 +388,16 @@ MRT_DFN f3 eval(const Ray& r, float t) { return add(r.o, fmul(t, r.d)); }
 
 // aabb::hit, active SSE branch (aabb.h:49-76)
 MRT_DFN bool aabb_hit(const float* bmin, const float* bmax, const Ray& r, float tmin, float tmax) {
+#if MRT_FAST_SLAB
+    // tolerance contract: (b - o) * inv as fma(b, inv, -(o * inv)); the products o * inv are shared
+    // by every box a walk step tests with the same ray (one multiply-add per slab instead of two)
+    const float nox = -(r.o.x * r.inv.x), noy = -(r.o.y * r.inv.y), noz = -(r.o.z * r.inv.z);
+    float t0x = __builtin_fmaf(bmin[0], r.inv.x, nox), t0y = __builtin_fmaf(bmin[1], r.inv.y, noy), t0z = __builtin_fmaf(bmin[2], r.inv.z, noz);
+    float t1x = __builtin_fmaf(bmax[0], r.inv.x, nox), t1y = __builtin_fmaf(bmax[1], r.inv.y, noy), t1z = __builtin_fmaf(bmax[2], r.inv.z, noz);
+#else
     float t0x = (bmin[0] - r.o.x) * r.inv.x, t0y = (bmin[1] - r.o.y) * r.inv.y, t0z = (bmin[2] - r.o.z) * r.inv.z;
     float t1x = (bmax[0] - r.o.x) * r.inv.x, t1y = (bmax[1] - r.o.y) * r.inv.y, t1z = (bmax[2] - r.o.z) * r.inv.z;
+#endif
     // A nice ray (|inv| <= 2^26, |o| <= 2^60) with a box of finite coordinates gets no NaN slab
     // values, and (bmin - o) * inv <= (bmax - o) * inv exactly when inv >= 0: the blendv swap is a
     // min/max, and maxps/minps (NaN-asymmetric) are plain max/min.  The result is a comparison, so
