@@ -686,6 +686,7 @@ mrt_status mrt_internal_scene_tables(const mrt_scene_view* v, SceneTables* T) {
     T->features = scene_features(v, nodes, absorbed);
     const char* no_sig = getenv("MRT_NO_SIG");  // test hook: run the interpreter on known shapes too
     if (lin) T->features |= FT_LIN;
+    if (lin) cornell_room_fill(lc.prog.data(), (uint32_t)lc.prog.size());  // (Cornell shape: the room into the END op)
     if (lin && !(no_sig && *no_sig && *no_sig != '0')) T->features |= MRT_SIG_BITS(lin_sig_of(lc.prog.data(), (uint32_t)lc.prog.size()));
     T->nbleaf = blist ? nodes[v->biased].b : 1u;
     T->blist = blist;

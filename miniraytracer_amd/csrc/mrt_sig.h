@@ -42,6 +42,68 @@ static constexpr LinSig kSigs[SIG_COUNT] = {
 };
 // clang-format on
 
+// host: the Cornell shape's room -- ops 1, 2, 4, 5, 6 (two yz, two xz, one xy rect) one-sided rects
+// facing INTO one box and spanning its faces (scene.cpp:311-318; op 3 is the light) -- written into
+// the program's END op: f[0..5] the box's min / max corners, f[6..11] the material of face
+// 2*axis + side (side 1: the max plane), node = the mask of the faces present.  The tolerance
+// contract's Cornell walk tests the room as ONE slab test: a ray inside (or entering) the box hits
+// the face it leaves through; a face seen from outside is back-facing.  Returns false (no room) if
+// the rects do not form such a box.
+inline bool cornell_room_fill(LinOp* prog, uint32_t n) {
+    if (n != kSigs[SIG_CORNELL].n) return false;
+    static const uint32_t ops[5] = {1, 2, 4, 5, 6};
+    float lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
+    bool has[3][2] = {{false, false}, {false, false}, {false, false}};
+    uint32_t mats[6] = {0, 0, 0, 0, 0, 0}, mask = 0;
+    // in-plane axes of a rect of axis a (mrt_lin.h lin_prim_t): f[0..1] along b, f[2..3] along c
+    auto in_plane = [](uint32_t a, uint32_t* b, uint32_t* c) { *b = a == 0 ? 1u : 0u; *c = a == 2 ? 1u : 2u; };
+    for (uint32_t j = 0; j < 5; j++) {
+        const LinOp& o = prog[ops[j]];
+        const uint32_t kind = (o.code >> 8) & 0xFFu;
+        if ((o.code & 0xFFu) != LOP_PRIM || (kind != MRT_K_XY && kind != MRT_K_XZ && kind != MRT_K_YZ)) return false;
+        if (((o.code >> 16) & (MRT_F_NEEDUV | MRT_F_SLOWDIV)) != 0) return false;
+        const uint32_t a = kind == MRT_K_YZ ? 0u : kind == MRT_K_XZ ? 1u : 2u;
+        const uint32_t side = o.f[5] > 0.0f ? 0u : 1u;  // a normal along +axis faces into a box from its min plane
+        if (o.f[5] != (side ? -1.0f : 1.0f) || has[a][side]) return false;
+        has[a][side] = true;
+        (side ? hi : lo)[a] = o.f[4];
+        mats[a * 2 + side] = o.mat;
+        mask |= 1u << (a * 2 + side);
+    }
+    // the box's extent along every axis: the face planes there, and the in-plane bounds of the
+    // faces that span it, must all agree
+    float blo[3], bhi[3];
+    bool set[3] = {false, false, false};
+    auto agree = [&](uint32_t a, float l, float h) {
+        if (!set[a]) { blo[a] = l; bhi[a] = h; set[a] = true; return true; }
+        return blo[a] == l && bhi[a] == h;
+    };
+    for (uint32_t j = 0; j < 5; j++) {
+        const LinOp& o = prog[ops[j]];
+        const uint32_t kind = (o.code >> 8) & 0xFFu;
+        const uint32_t a = kind == MRT_K_YZ ? 0u : kind == MRT_K_XZ ? 1u : 2u;
+        uint32_t b, c;
+        in_plane(a, &b, &c);
+        if (!agree(b, o.f[0], o.f[1]) || !agree(c, o.f[2], o.f[3])) return false;
+    }
+    for (uint32_t a = 0; a < 3; a++) {
+        if (!set[a] || !(blo[a] < bhi[a])) return false;
+        if ((has[a][0] && lo[a] != blo[a]) || (has[a][1] && hi[a] != bhi[a])) return false;
+    }
+    LinOp& e = prog[n - 1];  // the END op: nothing else reads its fields
+    for (uint32_t a = 0; a < 3; a++) {
+        e.f[a] = blo[a];
+        e.f[3 + a] = bhi[a];
+    }
+    for (uint32_t k = 0; k < 6; k++) {
+        float fm;
+        __builtin_memcpy(&fm, &mats[k], 4);
+        e.f[6 + k] = fm;
+    }
+    e.node = mask;
+    return true;
+}
+
 // host: the shape id of a compiled program (SIG_NONE if it matches no entry)
 inline uint32_t lin_sig_of(const LinOp* prog, uint32_t n) {
     for (uint32_t id = 1; id < SIG_COUNT; id++) {
@@ -55,7 +117,7 @@ inline uint32_t lin_sig_of(const LinOp* prog, uint32_t n) {
         }
         // the Cornell shape's box must be box.h's six rects (MRT_F_BOX6, set on upload): the
         // tolerance-contract kernel walks it as one slab test with no fallback (cornell_fast_hit)
-        if (ok && id == SIG_CORNELL) ok = ((prog[8].code >> 16) & MRT_F_BOX6) != 0;
+        if (ok && id == SIG_CORNELL) ok = ((prog[8].code >> 16) & MRT_F_BOX6) != 0 && prog[n - 1].node != 0;  // + cornell_room_fill
         if (ok) return id;
     }
     return SIG_NONE;
@@ -240,6 +302,15 @@ struct SigWalk {
 #ifndef MRT_CORNELL_BATCHES
 #define MRT_CORNELL_BATCHES 2
 #endif
+// x, y or z by a per-lane axis index, as selects (a select chain on one index was turned into a
+// per-lane lookup table in scratch memory)
+MRT_DFN float sel3(uint32_t a, float x, float y, float z) {
+    float v = a == 1u ? y : x;
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(v));
+#endif
+    return a == 2u ? z : v;
+}
 struct CornellRec {
     float closest, k, ns;
     uint32_t code, mat;  // code: 0 none; 1-3 world rect of axis code-1 (plane k); 4-6 box face of axis code-4; 7 sphere
@@ -294,6 +365,55 @@ MRT_DFN void cornell_take1(CornellSphere& d) {
     (void)d;
 #endif
 }
+// the room (cornell_room_fill): box corners, face materials, face mask -- from the END op
+struct CornellRoom {
+    uint32_t lo0, lo1, lo2, hi0, hi1, hi2, m0, m1, m2, m3, m4, m5, mask;
+};
+MRT_DFN CornellRoom cornell_load_room(const MRT_CONST_AS LinOp& e) {
+    const MRT_CONST_AS uint32_t* q = reinterpret_cast<const MRT_CONST_AS uint32_t*>(&e);
+    return CornellRoom{q[4], q[5], q[6], q[7], q[8], q[9], q[10], q[11], q[12], q[13], q[14], q[15], q[1]};
+}
+MRT_DFN void cornell_take1(CornellRoom& d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+s"(d.lo0), "+s"(d.lo1), "+s"(d.lo2), "+s"(d.hi0), "+s"(d.hi1), "+s"(d.hi2), "+s"(d.mask));
+    asm volatile("" : "+s"(d.m0), "+s"(d.m1), "+s"(d.m2), "+s"(d.m3), "+s"(d.m4), "+s"(d.m5));
+#else
+    (void)d;
+#endif
+}
+// The room's walls (ops 1, 2, 4, 5, 6) as one slab test: a ray that meets the box leaves it
+// through the face of its smallest far-plane distance; that face, if the room has it, is the
+// wall hit (front-facing: the walls face inward; any face the ray crosses going in is back-facing
+// and missed, rect.cpp:26-30).  Differs from the five rect tests by rounding at the room's edges.
+template <uint32_t F>
+MRT_DFN void cornell_room(const CornellRoom& d, const Ray& r, float tmin, CornellRec& w) {
+    const float lo0 = __uint_as_float(d.lo0), lo1 = __uint_as_float(d.lo1), lo2 = __uint_as_float(d.lo2);
+    const float hi0 = __uint_as_float(d.hi0), hi1 = __uint_as_float(d.hi1), hi2 = __uint_as_float(d.hi2);
+    const float t0x = (lo0 - r.o.x) * r.inv.x, t1x = (hi0 - r.o.x) * r.inv.x;
+    const float t0y = (lo1 - r.o.y) * r.inv.y, t1y = (hi1 - r.o.y) * r.inv.y;
+    const float t0z = (lo2 - r.o.z) * r.inv.z, t1z = (hi2 - r.o.z) * r.inv.z;
+    const float fx = fmaxf(t0x, t1x), fy = fmaxf(t0y, t1y), fz = fmaxf(t0z, t1z);
+    const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+    const float tf = fminf(fminf(fx, fy), fz);
+    // the exit face: its axis (ties to the later axis: z, then y, as the later rects win), and its
+    // side (the max plane when the ray goes up that axis)
+    const uint32_t a = tf == fz ? 2u : (tf == fy ? 1u : 0u);
+    const float da = sel3(a, r.d.x, r.d.y, r.d.z);
+    const uint32_t side = da > 0.0f ? 1u : 0u;
+    const uint32_t face = a * 2u + side;
+    const bool h = (tn <= tf) & (((d.mask >> face) & 1u) != 0u) & (tf >= tmin) & (tf <= w.closest);
+    // plane and material of the face by selects (a chain of compares with one index became a
+    // per-lane lookup table in scratch memory)
+    const bool up = side != 0u;
+    const float k = up ? sel3(a, hi0, hi1, hi2) : sel3(a, lo0, lo1, lo2);
+    const uint32_t m = __float_as_uint(up ? sel3(a, __uint_as_float(d.m1), __uint_as_float(d.m3), __uint_as_float(d.m5))
+                                          : sel3(a, __uint_as_float(d.m0), __uint_as_float(d.m2), __uint_as_float(d.m4)));
+    w.closest = h ? tf : w.closest;
+    w.code = h ? 1u + a : w.code;
+    w.k = h ? k : w.k;
+    w.ns = h ? (side ? -1.0f : 1.0f) : w.ns;
+    w.mat = h ? m : w.mat;
+}
 template <typename... D>
 MRT_DFN void cornell_take(D&... d) {
     (cornell_take1(d), ...);
@@ -326,31 +446,17 @@ MRT_DFN bool cornell_fast_hit(const MRT_CONST_AS LinOp* prog, const Ray& r, floa
                       G.op[17] == LOP_PRIM && G.kind[17] == MRT_K_SPHERE,
                   "Cornell shape: translate(rotate_y(box)) at op 7, its six rects under op 8, the sphere at op 17");
     CornellRec w{FLT_MAX_, 0.0f, 0.0f, 0u, 0u};
-    // the six rects' words in one batch of scalar loads, one wait
-    CornellRect d1 = cornell_load(prog[1]), d2 = cornell_load(prog[2]), d3 = cornell_load(prog[3]);
-    CornellRect d4 = cornell_load(prog[4]), d5 = cornell_load(prog[5]), d6 = cornell_load(prog[6]);
-#if MRT_CORNELL_BATCHES == 2  // walls, then box + sphere (fewer SGPRs live at once, one more wait)
-    cornell_take(d1, d2, d3, d4, d5, d6);
-    cornell_rect<F, 1>(d1, r, tmin, w);
-    cornell_rect<F, 2>(d2, r, tmin, w);
+    // the room's walls as one slab test (ops 1, 2, 4, 5, 6; cornell_room_fill), then the light
+    // (op 3), the box and the sphere: their words in two batches of scalar loads
+    static_assert(G.op[G.n - 1] == LOP_END, "the room is kept in the END op");
+    CornellRoom dr = cornell_load_room(prog[G.n - 1]);
+    CornellRect d3 = cornell_load(prog[3]);
+    cornell_take(dr, d3);
+    cornell_room<F>(dr, r, tmin, w);
     cornell_rect<F, 3>(d3, r, tmin, w);
-    cornell_rect<F, 4>(d4, r, tmin, w);
-    cornell_rect<F, 5>(d5, r, tmin, w);
-    cornell_rect<F, 6>(d6, r, tmin, w);
     CornellBox db = cornell_load_box(prog[7], prog[8]);
     CornellSphere dsp = cornell_load_sphere(prog[17]);
     cornell_take(db, dsp);
-#else
-    CornellBox db = cornell_load_box(prog[7], prog[8]);
-    CornellSphere dsp = cornell_load_sphere(prog[17]);
-    cornell_take(d1, d2, d3, d4, d5, d6, db, dsp);
-    cornell_rect<F, 1>(d1, r, tmin, w);
-    cornell_rect<F, 2>(d2, r, tmin, w);
-    cornell_rect<F, 3>(d3, r, tmin, w);
-    cornell_rect<F, 4>(d4, r, tmin, w);
-    cornell_rect<F, 5>(d5, r, tmin, w);
-    cornell_rect<F, 6>(d6, r, tmin, w);
-#endif
     // the box in its own frame: o' = R(o - offset), d' = R d, R = rotate_y's (s, c)
     const float s = __uint_as_float(db.s), c = __uint_as_float(db.c);
     const float off0 = __uint_as_float(db.o0), off1 = __uint_as_float(db.o1), off2 = __uint_as_float(db.o2);
@@ -369,7 +475,7 @@ MRT_DFN bool cornell_fast_hit(const MRT_CONST_AS LinOp* prog, const Ray& r, floa
     const bool hb = (tn <= tf) & (tn >= tmin) & (tn <= w.closest);
     // the entry face: its axis, and its outward normal's sign (against the ray's direction there)
     const uint32_t bax = tn == nx ? 0u : (tn == ny ? 1u : 2u);
-    const float bd = bax == 0u ? dx : (bax == 1u ? r.d.y : dz);
+    const float bd = sel3(bax, dx, r.d.y, dz);
     w.closest = hb ? tn : w.closest;
     w.code = hb ? 4u + bax : w.code;
     w.ns = hb ? (bd > 0.0f ? -1.0f : 1.0f) : w.ns;
