@@ -87,6 +87,10 @@ __host__ static inline bool signbit(double x) { return std::signbit(x); }
 #ifndef MRT_FWD_FOLD
 #define MRT_FWD_FOLD MRT_FAST
 #endif
+// the Cornell room's five walls as one slab test (mrt_sig.h cornell_room), tolerance contract only
+#ifndef MRT_FAST_ROOM
+#define MRT_FAST_ROOM MRT_FAST
+#endif
 // slab tests as one fma per plane (aabb_hit), tolerance contract only
 #ifndef MRT_FAST_SLAB
 #define MRT_FAST_SLAB MRT_FAST

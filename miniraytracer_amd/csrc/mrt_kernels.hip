@@ -495,7 +495,16 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                 w.hdone = false;
                 const MRT_CONST_AS LinOp& lo = prog[0];
                 const bool in = !(LOP_FLAGS(lo) & MRT_F_HASBOX) || lin_box(lo, w.cur, 0.001f, w.closest);
+#if MRT_FAST_ROOM
+                // tolerance contract: the room's five walls as one slab test (cornell_room_fill; the
+                // box test of the root list only skips work), then the light (op 3)
+                (void)in;
+                static_assert(kSigs[SIG_ROOM_MESH].op[kSigs[SIG_ROOM_MESH].n - 1] == LOP_END, "room in the END op");
+                room_walls_op(prog[kSigs[SIG_ROOM_MESH].n - 1], w.cur, 0.001f, w);
+                W::template run<3, 4>(S, prog, 0.001f, w, true, rec, Ls);
+#else
                 W::template run<1, kMeshPC>(S, prog, 0.001f, w, in, rec, Ls);
+#endif
                 const mrt_node mn = ld_node(const_ptr(S.nodes) + prog[kMeshPC].node);
                 const MRT_CONST_AS mrt_mesh_node& rt = const_ptr(S.mnodes)[mn.a];
                 const bool enter = in && aabb_hit(f3{rt.bmin[0], rt.bmin[1], rt.bmin[2]}, f3{rt.bmax[0], rt.bmax[1], rt.bmax[2]}, ps.r,

@@ -42,19 +42,21 @@ static constexpr LinSig kSigs[SIG_COUNT] = {
 };
 // clang-format on
 
-// host: the Cornell shape's room -- ops 1, 2, 4, 5, 6 (two yz, two xz, one xy rect) one-sided rects
+// host: the Cornell shapes' room (scene 5, and the room + mesh scenes 8 / 9, scene.cpp:489-495) --
+// ops 1, 2, 4, 5, 6 (two yz, two xz, one xy rect) one-sided rects
 // facing INTO one box and spanning its faces (scene.cpp:311-318; op 3 is the light) -- written into
 // the program's END op: f[0..5] the box's min / max corners, f[6..11] the material of face
-// 2*axis + side (side 1: the max plane), node = the mask of the faces present.  The tolerance
+// 2*axis + side (side 1: the max plane), node = the mask of the faces present, skip = the op index
+// of each face (4 bits per face).  The tolerance
 // contract's Cornell walk tests the room as ONE slab test: a ray inside (or entering) the box hits
 // the face it leaves through; a face seen from outside is back-facing.  Returns false (no room) if
 // the rects do not form such a box.
 inline bool cornell_room_fill(LinOp* prog, uint32_t n) {
-    if (n != kSigs[SIG_CORNELL].n) return false;
+    if (n != kSigs[SIG_CORNELL].n && n != kSigs[SIG_ROOM_MESH].n) return false;
     static const uint32_t ops[5] = {1, 2, 4, 5, 6};
     float lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
     bool has[3][2] = {{false, false}, {false, false}, {false, false}};
-    uint32_t mats[6] = {0, 0, 0, 0, 0, 0}, mask = 0;
+    uint32_t mats[6] = {0, 0, 0, 0, 0, 0}, mask = 0, face_ops = 0;
     // in-plane axes of a rect of axis a (mrt_lin.h lin_prim_t): f[0..1] along b, f[2..3] along c
     auto in_plane = [](uint32_t a, uint32_t* b, uint32_t* c) { *b = a == 0 ? 1u : 0u; *c = a == 2 ? 1u : 2u; };
     for (uint32_t j = 0; j < 5; j++) {
@@ -69,6 +71,7 @@ inline bool cornell_room_fill(LinOp* prog, uint32_t n) {
         (side ? hi : lo)[a] = o.f[4];
         mats[a * 2 + side] = o.mat;
         mask |= 1u << (a * 2 + side);
+        face_ops |= ops[j] << (4 * (a * 2 + side));
     }
     // the box's extent along every axis: the face planes there, and the in-plane bounds of the
     // faces that span it, must all agree
@@ -101,6 +104,7 @@ inline bool cornell_room_fill(LinOp* prog, uint32_t n) {
         e.f[6 + k] = fm;
     }
     e.node = mask;
+    e.skip = face_ops;  // op index of face k in bits 4k..4k+3
     return true;
 }
 
@@ -118,6 +122,7 @@ inline uint32_t lin_sig_of(const LinOp* prog, uint32_t n) {
         // the Cornell shape's box must be box.h's six rects (MRT_F_BOX6, set on upload): the
         // tolerance-contract kernel walks it as one slab test with no fallback (cornell_fast_hit)
         if (ok && id == SIG_CORNELL) ok = ((prog[8].code >> 16) & MRT_F_BOX6) != 0 && prog[n - 1].node != 0;  // + cornell_room_fill
+        if (ok && id == SIG_ROOM_MESH) ok = prog[n - 1].node != 0;  // the room (cornell_room_fill)
         if (ok) return id;
     }
     return SIG_NONE;
@@ -413,6 +418,25 @@ MRT_DFN void cornell_room(const CornellRoom& d, const Ray& r, float tmin, Cornel
     w.k = h ? k : w.k;
     w.ns = h ? (side ? -1.0f : 1.0f) : w.ns;
     w.mat = h ? m : w.mat;
+}
+// The room + mesh walk's walls (scenes 8 / 9, tolerance build): the room's slab test as above,
+// the hit face's op index as the hit op (the record is then derived op by op, SigWalk::derive)
+MRT_DFN void room_walls_op(const MRT_CONST_AS LinOp& e, const Ray& r, float tmin, SigState& w) {
+    CornellRoom d = cornell_load_room(e);
+    uint32_t face_ops = e.skip;
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+s"(face_ops));
+#endif
+    cornell_take1(d);
+    CornellRec c{w.closest, 0.0f, 0.0f, 0u, 0u};
+    cornell_room<0u>(d, r, tmin, c);
+    if (c.code != 0u) {  // per lane: the exit face's axis from the code, its side from the sign
+        const uint32_t face = (c.code - 1u) * 2u + (c.ns < 0.0f ? 1u : 0u);
+        w.closest = c.closest;
+        w.hnode = (face_ops >> (4u * face)) & 15u;
+        w.hinst = MRT_NONE;
+        w.hdone = false;
+    }
 }
 template <typename... D>
 MRT_DFN void cornell_take(D&... d) {
