@@ -125,3 +125,14 @@ def test_cpu_backend_preview_shows_finished_tiles(mrt):
         shown = np.any(snap != 0, axis=2)
         assert k in (0, 64)
         assert np.array_equal(snap[shown], img[shown])
+
+
+@pytest.mark.parametrize("sid,shape", [(5, 1), (8, 2), (9, 2), (0, 0), (7, 0)])
+def test_walk_shape_recognised_on_upload(mrt, sid, shape):
+    """The scene tables built on upload (shared by both backends) give the Cornell box its walk shape
+    only when its box is box.h's six rects and its five walls form one inward-facing room
+    (mrt_sig.h lin_sig_of / cornell_room_fill: the tolerance contract tests both as slab tests), and
+    the room + mesh scenes theirs; other scenes run the interpreter (shape 0)."""
+    sc = mrt.select_scene(sid, 1.0)
+    r = mrt.Renderer(sc, "cpu")
+    assert (r.kernel_info()["features"] >> 16) & 0xFF == shape
