@@ -75,10 +75,9 @@ extern "C" int mrt_debug_bstats(unsigned long long* out, int reset) {
 }
 #endif
 // resumable mesh walk (room + mesh kernels): the walk loop returns the wave to shading / new rays
-// once at most MRT_WALK_MIN lanes still walk and at least MRT_WALK_OTHER lanes have other work
-#ifndef MRT_WALK_MIN
-#define MRT_WALK_MIN 32u
-#endif
+// once at most P.walk_min lanes still walk (set on upload from the mesh BVH's size: 32, or 40 for
+// BVHs of >= 2048 inner nodes -- measured: bunny, 2937 inner nodes, best at 40 (+4% over 32);
+// teapot, ~1045, at 28-32 (40: -3%)) and at least MRT_WALK_OTHER lanes have other work
 #ifndef MRT_WALK_OTHER
 #define MRT_WALK_OTHER 16u
 #endif
@@ -523,7 +522,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                     if (st == 1u) w.hnode = kMeshPC;  // w.closest = the hit's t, w.hdone set
                     phase = st != 0u ? PH_DONE : PH_WALK;
                 }
-                if ((uint32_t)__popcll(__ballot(phase == PH_WALK)) <= MRT_WALK_MIN &&
+                if ((uint32_t)__popcll(__ballot(phase == PH_WALK)) <= P.walk_min &&
                     (uint32_t)__popcll(__ballot(phase == PH_DONE || (!active && !exhausted))) >= MRT_WALK_OTHER)
                     break;  // others can shade / start rays: done lanes, or idle lanes with paths left
             }

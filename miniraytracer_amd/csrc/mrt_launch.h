@@ -39,6 +39,7 @@ struct PathParams {
     float4* __restrict__ lev;             // fold levels, lane-major: [slot][lev_rows]
     uint32_t lev_rows;                    // levels per lane (max_bounces, at least 1)
     uint32_t lds_frames, lds_rays, lds_mesh, lds_save;  // LDS stack slots / words per lane
+    uint32_t walk_min;                    // resumable mesh walk: yield once at most this many lanes walk
     const float4* tree_src;               // TreeOf<F>::on kernels: BvhWide nodes copied to LDS at start
     uint32_t tree_n;                      // how many (the first tree_n of the breadth-first array)
 };

@@ -226,6 +226,7 @@ struct mrt_scene {
     unsigned long long* d_rays = nullptr;
     uint32_t features = 0, variant = 0;
     uint32_t lds_frames = 0, lds_rays = 0, lds_mesh = 0, lds_save = 0;
+    uint32_t walk_min = 32;  // resumable mesh walk threshold (PathParams::walk_min)
     PathLaunch pl[2];            // [0] exact contract, [1] tolerance contract (MRT_RF_FAST)
     size_t max_threads = 0;  // largest path-kernel grid in threads (per-lane level rows)
     std::vector<hipEvent_t> ev;  // [2*k]: start/stop of path-kernel launch k of the last render
@@ -765,6 +766,8 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     s->lds_rays = lin_kernel ? 0 : (uint32_t)T.max_rays;
     s->lds_mesh = (uint32_t)T.max_mesh;
     s->lds_save = (lin_kernel && (kVariants[s->variant] & FT_INST)) ? 15u : 0u;
+    // resumable mesh walk: deeper pod_bvh trees keep the wave walking longer
+    s->walk_min = T.wide.size() >= 2048 ? 40u : 32u;  // inner nodes: bunny 2937, teapot ~1045
     const std::vector<BvhWide>& bwide = T.bwide;
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
@@ -1016,6 +1019,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.lds_rays = s->lds_rays;
         P.lds_mesh = s->lds_mesh;
         P.lds_save = PL.lds_save;
+        P.walk_min = s->walk_min;
         P.tree_src = reinterpret_cast<const float4*>(s->S.bwide);
         P.tree_n = PL.tree_n;
         P.pixels = s->d_pixels;
