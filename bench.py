@@ -59,6 +59,8 @@ def parse():
                     help="single-GPU rehearsal: render only rank --emulate-rank's share of an N-rank job "
                          "(no collectives); used to predict per-rank step time at N GPUs")
     ap.add_argument("--emulate-rank", type=int, default=0)
+    ap.add_argument("--chunk-samples", type=int, default=0,
+                    help="samples per path-kernel launch (0: the library's choice)")
     ap.add_argument("--pipeline", type=int, default=2,
                     help="render contexts used round-robin on their own HIP streams: step i+1's launch "
                          "fills the CUs freed by step i's tail instead of waiting for it")
@@ -205,7 +207,7 @@ def main():
         d_rank, d_world = args.emulate_rank, args.emulate_world
     def desc_of(numerics):
         return m.render_desc(args.width, args.height, args.samples, depth=args.depth, tile_size=args.tile_size,
-                             rank=d_rank, world=d_world, numerics=numerics)
+                             rank=d_rank, world=d_world, numerics=numerics, chunk_samples=args.chunk_samples)
 
     desc = desc_of(args.numerics)
     for r in rnds:
