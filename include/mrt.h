@@ -152,7 +152,6 @@ mrt_status mrt_kernel_ms(mrt_scene* s, float* path_ms, uint32_t* launches);
  * workgroups, threads per workgroup and the BVH nodes each workgroup keeps in LDS. */
 typedef struct mrt_kernel_info {
     uint32_t features, kernel_features, lds_bytes, grid, prog_ops, vgprs, wg, tree_nodes;
-    uint32_t run_k;  /* samples per sample run of a tolerance-contract mode-0 render (0: per-path radiance + fold) */
 } mrt_kernel_info;
 mrt_status mrt_scene_kernel_info(const mrt_scene* s, mrt_kernel_info* out);
 

@@ -113,8 +113,7 @@ template <uint32_t F> struct PathLevLds {
 template <uint32_t F> struct PathQ {
     static constexpr bool on = MRT_PATHQ && (F & FT_MESH) == 0 && !TreeOf<F>::on;
     // LDS words per lane slot: o, dir, time, PCG state + inc, index (12); + the wave's claim state
-    // (1); + the sample-run slots (MRT_RUN_SLOTS x 5 words: partial b xyz, run index, counters)
-    static constexpr uint32_t words = on ? 13u + (MRT_RUN_SLOTS * 5u + 63u) / 64u : 0u;
+    static constexpr uint32_t words = on ? 13u : 0u;
 };
 template <uint32_t F>
 __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per_eu(MRT_OCC(F)))) MRT_PATH_KERNEL(PathParams P) {
@@ -175,8 +174,8 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
     bool in_tail = false;                    // the partition's last paths: small claims
     uint64_t pool_next = 0, pool_end = 0;    // wave-uniform: the wave's claimed, not yet taken paths
     if (P.static_first) {
-        pool_next = uni64(umin64(P.part_base[part] + ((uint64_t)(blockIdx.x / MRT_NPART) * wpb + wave) * P.batch, P.part_base[part + 1]));
-        pool_end = uni64(umin64(pool_next + P.batch, P.part_base[part + 1]));
+        pool_next = uni64(umin64(P.part_base[part] + ((uint64_t)(blockIdx.x / MRT_NPART) * wpb + wave) * MRT_BATCH, P.part_base[part + 1]));
+        pool_end = uni64(umin64(pool_next + MRT_BATCH, P.part_base[part + 1]));
     }
     bool exhausted = false;  // no paths left in the pool nor in any partition
     // Queue kernels keep the claim state (pool bounds, partition) in LDS between claims -- it is
@@ -212,17 +211,12 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
     // work_queue.cpp:158-166).  start(u, v) begins a lane's path at camera coordinates (u, v) with
     // its PCG stream seeded from the path key.
     // path index -> its camera coordinates (u, v) and its PCG stream seeded from the path key
-    // i = hi * npix + lp; the double estimate is off by at most one either way
-    auto split = [&](uint32_t i, uint32_t* hi, uint32_t* lo) {
+    auto path_key = [&](uint32_t i, Pcg& rng, float* uo, float* vo) {
+        // i = sl * npix + lp; the double estimate is off by at most one either way
         uint32_t sl = (uint32_t)((double)i * P.inv_npix);
         uint32_t lp = i - sl * P.npix;
         if ((int32_t)lp < 0) { sl--; lp += P.npix; }
         if (lp >= P.npix) { sl++; lp -= P.npix; }
-        *hi = sl;
-        *lo = lp;
-    };
-    // sample s0 + sl of local pixel lp
-    auto path_key_at = [&](uint32_t sl, uint32_t lp, Pcg& rng, float* uo, float* vo) {
         const uint32_t s = P.s0 + sl;
         const uint2 xy = P.pixels[lp];
         const uint32_t x = xy.x, y = xy.y;
@@ -241,11 +235,6 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
         *uo = u;
         *vo = v;
     };
-    auto path_key = [&](uint32_t i, Pcg& rng, float* uo, float* vo) {
-        uint32_t sl, lp;
-        split(i, &sl, &lp);
-        path_key_at(sl, lp, rng, uo, vo);
-    };
     // the next c path indices of the wave's pool, the lane of rank r taking index *i (>= n_paths:
     // none); the pool refilled by one atomic per claim (work_queue::getWork, work_queue.cpp:158-166)
     auto claim = [&](uint32_t c, uint32_t r, bool want, uint64_t* i) {
@@ -254,7 +243,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
         if (have < c) {
             while (part_tries < MRT_NPART) {  // wave-uniform
                 const uint64_t pe = P.part_base[part + 1], p0 = P.part_dyn[part];
-                const uint32_t batch = in_tail ? P.tail_batch : P.batch;
+                const uint32_t batch = in_tail ? MRT_TAIL_BATCH : MRT_BATCH;
                 if (lane == 0) {
                     nb = p0 + atomicAdd(P.counter + part * MRT_COUNTER_STRIDE, (unsigned long long)batch);
                     // every 32nd claim: a system-scope store to host memory, read by mrt_progress
@@ -355,44 +344,6 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
         f3 st_v{0.0f, 0.0f, 0.0f};
         uint32_t st_off = 0;  // byte offset of the path's radiance (a launch chunk is < 4 GiB)
         bool st_pend = false;
-        // Sample runs (P.run_k != 0, PathParams): the wave's run slots in LDS after the claim state,
-        // SoA: partial b (x, y, z), run index u, counters (samples started | done << 8 | NaN
-        // doublings << 16 | samples in the run << 24; kRunFree = no run)
-        constexpr uint32_t kRunFree = 0xFFFFFFFFu;
-        float* const Rx = Lq + 13u * 64u;
-        float* const Ry = Rx + MRT_RUN_SLOTS;
-        float* const Rz = Ry + MRT_RUN_SLOTS;
-        uint32_t* const Ru = reinterpret_cast<uint32_t*>(Rz + MRT_RUN_SLOTS);
-        uint32_t* const Rc = Ru + MRT_RUN_SLOTS;
-        const bool runs = PathQ<F>::on && P.run_k != 0u;  // (the host sets run_k for PathQ kernels only)
-        if (runs) {
-            Rc[lane] = kRunFree;
-            if (lane + 64u < MRT_RUN_SLOTS) Rc[lane + 64u] = kRunFree;
-        }
-        // a run's sample ended with radiance L: draw()'s per-sample step (main.cpp:161-167) on the
-        // run's affine partial -- col -> 2^k col + b; a non-finite sample doubles both -- and the
-        // partial out once the run's last sample is in (its samples run one after another, so the
-        // sum is in sample order whichever lanes traced them)
-        auto run_add = [&](uint32_t sl, f3 L) {
-            uint32_t cn = Rc[sl];
-            f3 b{Rx[sl], Ry[sl], Rz[sl]};
-            if (finite3(L)) {
-                b = add(b, L);
-            } else {
-                b = add(b, b);
-                cn += 1u << 16;
-            }
-            cn += 1u << 8;
-            if (((cn >> 8) & 0x7Fu) == ((cn >> 24) & 0x7Fu)) {
-                P.runs_out[Ru[sl]] = make_float4(b.x, b.y, b.z, (float)((cn >> 16) & 0xFFu));
-                Rc[sl] = kRunFree;
-            } else {
-                Rx[sl] = b.x;
-                Ry[sl] = b.y;
-                Rz[sl] = b.z;
-                Rc[sl] = cn;
-            }
-        };
         for (;;) {
             bool want_ray = false;
             if (active) {
@@ -409,14 +360,9 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                 });
                 PH_MARK(ph, 2);
                 if (ended) {
-                    const f3 Lp = end_path(ps, lev, L);
-                    if (runs) {
-                        run_add(idx, Lp);
-                    } else {
-                        st_v = Lp;
-                        st_off = idx * 12u;
-                        st_pend = true;
-                    }
+                    st_v = end_path(ps, lev, L);
+                    st_off = idx * 12u;
+                    st_pend = true;
                     if (P.path_rays) P.path_rays[idx] = ps.rays;
                     done_rays += ps.rays;
                     active = false;
@@ -453,72 +399,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                         q_head += c;
                     } else {
                         q_head = q_n = 0;
-                        if (!exhausted && runs) {
-                            // sample runs: runs from the pool into free slots (two claims: slots
-                            // 0-63, 64-..), then the next sample of up to 64 runs with none in
-                            // flight, one start per lane at full width
-                            const uint32_t sA = lane, sB = lane + 64u;
-                            const bool hasB = sB < MRT_RUN_SLOTS;
-                            cold_load();
-                            bool dry = part_tries >= MRT_NPART && pool_next >= pool_end;
-                            for (uint32_t h = 0; h < 2u; h++) {
-                                const uint32_t sl = h ? sB : sA;
-                                const bool fr = (h == 0u || hasB) && Rc[sl] == kRunFree;
-                                const uint64_t mf = __ballot(fr);
-                                if (mf && !dry) {
-                                    uint64_t i = 0;
-                                    claim((uint32_t)__popcll(mf), fr ? rank_below(mf) : 0u, fr, &i);
-                                    dry = exhausted;
-                                    if (fr && i < P.n_paths) {
-                                        uint32_t rc, lp;
-                                        split((uint32_t)i, &rc, &lp);
-                                        Ru[sl] = (uint32_t)i;
-                                        Rx[sl] = 0.0f;
-                                        Ry[sl] = 0.0f;
-                                        Rz[sl] = 0.0f;
-                                        Rc[sl] = (rc + 1u == P.run_c ? P.run_last : P.run_k) << 24;
-                                    }
-                                }
-                            }
-                            cold_store();
-                            auto startable = [](uint32_t cn) {
-                                return cn != kRunFree && (cn & 0x7Fu) == ((cn >> 8) & 0x7Fu) && (cn & 0x7Fu) < ((cn >> 24) & 0x7Fu);
-                            };
-                            const bool stA = startable(Rc[sA]), stB = hasB && startable(Rc[sB]);
-                            const uint64_t mA = __ballot(stA), mB = __ballot(stB);
-                            const uint32_t nA = (uint32_t)__popcll(mA);
-                            // the slots to start, in slot order, listed in the queue's index row
-                            uint32_t* const list = reinterpret_cast<uint32_t*>(Lq + 704);
-                            if (stA) list[rank_below(mA)] = sA;
-                            if (stB && nA + rank_below(mB) < 64u) list[nA + rank_below(mB)] = sB;
-                            const uint32_t nq = min(nA + (uint32_t)__popcll(mB), 64u);
-                            if (lane < nq) {
-                                const uint32_t sl = list[lane];
-                                const uint32_t cn = Rc[sl];
-                                uint32_t rc, lp;
-                                split(Ru[sl], &rc, &lp);
-                                Pcg rng;
-                                float u, v, time;
-                                f3 o, dir;
-                                path_key_at(rc * P.run_k + (cn & 0x7Fu), lp, rng, &u, &v);
-                                camera_ray_args(S, rng, u, v, &o, &dir, &time);
-                                float* q = Lq + lane;
-                                q[0] = o.x; q[64] = o.y; q[128] = o.z;
-                                q[192] = dir.x; q[256] = dir.y; q[320] = dir.z;
-                                q[384] = time;
-                                q[448] = __uint_as_float((uint32_t)rng.state);
-                                q[512] = __uint_as_float((uint32_t)(rng.state >> 32));
-                                q[576] = __uint_as_float((uint32_t)rng.inc);
-                                q[640] = __uint_as_float((uint32_t)(rng.inc >> 32));
-                                Rc[sl] = cn + 1u;  // (q[704] = sl already)
-                            }
-                            q_n = nq;
-                            auto left = [](uint32_t cn) { return cn != kRunFree && (cn & 0x7Fu) < ((cn >> 24) & 0x7Fu); };
-                            exhausted = dry && !__any(left(Rc[sA]) || (hasB && left(Rc[sB])));
-                            const uint32_t r2 = rank - avail;
-                            if (!active && r2 < q_n) pop(r2);
-                            q_head = min(c - avail, q_n);
-                        } else if (!exhausted) {
+                        if (!exhausted) {
                             uint64_t i = 0;
                             cold_load();
                             claim(64u, lane, true, &i);

@@ -42,16 +42,6 @@ struct PathParams {
     uint32_t walk_min;                    // resumable mesh walk: yield once at most this many lanes walk
     const float4* tree_src;               // TreeOf<F>::on kernels: BvhWide nodes copied to LDS at start
     uint32_t tree_n;                      // how many (the first tree_n of the breadth-first array)
-    uint32_t batch, tail_batch;           // work units per claim (MRT_BATCH / MRT_TAIL_BATCH paths, or runs)
-    // Sample runs (PathQ kernels, mode 0 without path debug; 0 = off): the work unit is a RUN of
-    // run_k consecutive samples of one local pixel, u = c * npix + lp covering samples
-    // s0 + c*run_k ..; a run's samples are traced one after another (never two in flight) and
-    // summed in sample order in the wave's LDS, so no per-path radiance reaches HBM: each run
-    // stores one affine partial (b, k) with col -> 2^k col + b (main.cpp:161-167's NaN doubling)
-    uint32_t run_k;
-    uint32_t run_c;                       // runs per pixel in this launch: ceil(chunk samples / run_k)
-    uint32_t run_last;                    // samples in a pixel's last run (1..run_k)
-    float4* __restrict__ runs_out;        // n_paths (= npix * run_c units) partials, [c][lp]
 };
 
 typedef void (*path_kernel_t)(PathParams);
@@ -68,19 +58,6 @@ typedef void (*path_kernel_t)(PathParams);
 #endif
 // one claim must cover a whole wave's idle lanes (the pool hands out at most 64 at once)
 static_assert(MRT_TAIL_BATCH >= 64u && MRT_BATCH >= MRT_TAIL_BATCH, "claims must be at least a wave wide");
-// sample runs: samples per run, run slots per wave (LDS), runs per claim (a claim may cover fewer
-// slots than are free: the rest wait for the next refill)
-#ifndef MRT_RUN_K
-#define MRT_RUN_K 16u
-#endif
-#define MRT_RUN_SLOTS 112u
-#ifndef MRT_RUN_BATCH
-#define MRT_RUN_BATCH 32u
-#endif
-#ifndef MRT_RUN_TAIL_BATCH
-#define MRT_RUN_TAIL_BATCH 8u
-#endif
-static_assert(MRT_RUN_K >= 1u && MRT_RUN_K <= 127u, "run counters are 7-bit fields");
 
 // kernel variants by scene features (the first instantiated superset is launched); FT_LIN
 // variants need the scene's linear hit program (mrt_lin.h), FT_ALL runs any graph.  The same list

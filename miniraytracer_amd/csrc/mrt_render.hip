@@ -78,32 +78,6 @@ __global__ void __launch_bounds__(256) mrt_fold_kernel(const float* __restrict__
     acc[lp] = make_float4(c.x, c.y, c.z, 0.0f);
 }
 
-// Sample runs (run mode, PathParams::run_k): each pixel's runs of consecutive samples arrive as
-// affine partials (b, k): col -> 2^k col + b (the NaN doubling of main.cpp:161-167 inside a run);
-// applied in run order -- draw()'s sequential sum, grouped by run (the tolerance contract only).
-#define FOLD_RUNS_DEPTH 8
-__global__ void __launch_bounds__(256) mrt_fold_runs_kernel(const float4* __restrict__ runs, float4* __restrict__ acc, uint32_t npix,
-                                                           uint32_t run_c) {
-    const uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
-    if (lp >= npix) return;
-    const float4 a = acc[lp];
-    f3 c{a.x, a.y, a.z};
-    auto apply = [&](float4 r) {
-        for (uint32_t d = (uint32_t)r.w; d > 0u; d--) c = add(c, c);
-        c = add(c, f3{r.x, r.y, r.z});
-    };
-    uint32_t k = 0;
-    for (; k + FOLD_RUNS_DEPTH <= run_c; k += FOLD_RUNS_DEPTH) {
-        float4 r[FOLD_RUNS_DEPTH];
-#pragma unroll
-        for (int j = 0; j < FOLD_RUNS_DEPTH; j++) r[j] = runs[(size_t)(k + j) * npix + lp];
-#pragma unroll
-        for (int j = 0; j < FOLD_RUNS_DEPTH; j++) apply(r[j]);
-    }
-    for (; k < run_c; k++) apply(runs[(size_t)k * npix + lp]);
-    acc[lp] = make_float4(c.x, c.y, c.z, 0.0f);
-}
-
 __global__ void __launch_bounds__(256) mrt_final_kernel(const float4* __restrict__ acc, float4* __restrict__ out, uint32_t npix, uint32_t ns,
                                                        uint32_t mode, float max_lum) {
     uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
@@ -213,7 +187,6 @@ struct mrt_scene {
     float2* d_sdist = nullptr;
     uint32_t sdist_sq = 0;
     float* d_rad = nullptr;
-    float4* d_runs = nullptr;  // sample-run partials (run mode): npix * runs per pixel
     uint32_t* d_path_rays = nullptr;
     float4* d_acc = nullptr;
     float4* d_lev = nullptr;
@@ -258,7 +231,7 @@ struct mrt_scene {
     size_t max_threads = 0;  // largest path-kernel grid in threads (per-lane level rows)
     std::vector<hipEvent_t> ev;  // [2*k]: start/stop of path-kernel launch k of the last render
     uint32_t n_launch = 0;
-    size_t runs_cap = 0, rad_cap = 0, acc_cap = 0, lev_cap = 0, px_cap = 0, pr_cap = 0, sd_cap = 0, out_cap = 0;
+    size_t rad_cap = 0, acc_cap = 0, lev_cap = 0, px_cap = 0, pr_cap = 0, sd_cap = 0, out_cap = 0;
     uint64_t last_paths = 0;
     uint32_t last_numerics = 0;
     uint32_t prog_ops = 0;  // linear hit program length (0: generic machine)
@@ -864,7 +837,7 @@ extern "C" void mrt_scene_free(mrt_scene* s) {
     if (s->h_prev) (void)hipHostFree(s->h_prev);
     if (s->h_seq) (void)hipHostFree(s->h_seq);
     if (s->ev_done) (void)hipEventDestroy(s->ev_done);
-    for (void* p : {(void*)s->d_counters, (void*)s->d_pixels, (void*)s->d_sdist, (void*)s->d_rad, (void*)s->d_runs, (void*)s->d_path_rays, (void*)s->d_acc,
+    for (void* p : {(void*)s->d_counters, (void*)s->d_pixels, (void*)s->d_sdist, (void*)s->d_rad, (void*)s->d_path_rays, (void*)s->d_acc,
                     (void*)s->d_lev, (void*)s->d_out, (void*)s->d_prev})
         if (p) (void)hipFree(p);
     delete s;
@@ -877,19 +850,6 @@ static uint32_t auto_chunk(uint32_t npix, uint32_t ns) {
     size_t c = per_sample ? budget / per_sample : ns;
     if (c < 1) c = 1;
     return (uint32_t)std::min<size_t>(c, ns);
-}
-
-// sample runs (PathParams::run_k): the tolerance build of a kernel with a path-start queue, draw()
-// accumulation (mode 0), no per-path debug output
-static uint32_t run_k_of(const mrt_scene* s, const mrt_render_desc* d) {
-    if (!(d->flags & MRT_RF_FAST) || d->mode != 0 || (d->flags & MRT_RF_PATH_DEBUG)) return 0;
-    if (!kernel_table_fast().pq[s->variant]) return 0;
-    uint32_t k = MRT_RUN_K;
-#ifdef MRT_EXPERIMENTS
-    if (const char* e = getenv("MRT_RUN_K"))  // experiment hook (0 = off)
-        if (*e) k = std::min<uint32_t>((uint32_t)atoi(e), 127u);
-#endif
-    return k;
 }
 
 static bool same_layout(const mrt_render_desc& a, const mrt_render_desc& b) {
@@ -958,11 +918,7 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
     if (chunk != s->chunk && (st = quiesce(s))) return st;  // the fold of a running render reads `chunk` rows
     s->chunk = chunk;
     size_t paths = (size_t)s->npix * s->chunk;
-    if (const uint32_t rk = run_k_of(s, d)) {  // run partials, not per-path radiance
-        if ((st = grow(s, (void**)&s->d_runs, &s->runs_cap, (size_t)s->npix * ((s->chunk + rk - 1) / rk) * 16))) return st;
-    } else if ((st = grow(s, (void**)&s->d_rad, &s->rad_cap, paths * 12))) {
-        return st;
-    }
+    if ((st = grow(s, (void**)&s->d_rad, &s->rad_cap, paths * 12))) return st;
     if ((st = grow(s, (void**)&s->d_acc, &s->acc_cap, (size_t)s->npix * 16))) return st;
     if ((st = grow(s, (void**)&s->d_out, &s->out_cap, (size_t)s->npix * 16 + 16))) return st;
     if (d->flags & MRT_RF_PREVIEW) {
@@ -1033,14 +989,12 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
     uint32_t ns = d->sqrt_samples * d->sqrt_samples;
     HIPCHK(hipMemsetAsync(s->d_acc, 0, (size_t)s->npix * 16, q));
     const uint32_t launches = (ns + s->chunk - 1) / s->chunk;
-    const uint32_t run_k = run_k_of(s, d);
     HIPCHK(hipMemsetAsync(s->d_counters, 0, (size_t)launches * MRT_NPART * MRT_COUNTER_STRIDE * 8, q));
     HIPCHK(hipMemsetAsync(s->d_counter + 4, 0, 8, q));  // cancel flag
     {
         std::lock_guard<std::mutex> lk(s->prog_mu);
         for (uint32_t k = 0; k < launches; k++) {
-            const uint32_t nsl = std::min(ns, (k + 1) * s->chunk) - k * s->chunk;  // work units: paths or runs
-            s->chunk_paths[k] = (uint64_t)s->npix * (run_k ? (nsl + run_k - 1) / run_k : nsl);
+            s->chunk_paths[k] = (uint64_t)s->npix * (std::min(ns, (k + 1) * s->chunk) - k * s->chunk);
             for (uint32_t j = 0; j < MRT_NPART; j++) {
                 __atomic_store_n(&s->h_prog[(size_t)k * MRT_NPART + j], (uint64_t)0, __ATOMIC_RELAXED);
                 s->h_seen[(size_t)k * MRT_NPART + j] = 0;
@@ -1080,21 +1034,15 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.sq = d->sqrt_samples;
         P.ns = ns;
         P.s0 = s0;
-        P.run_k = run_k;
-        P.run_c = run_k ? (s1 - s0 + run_k - 1) / run_k : 0u;
-        P.run_last = run_k ? (s1 - s0) - (P.run_c - 1) * run_k : 0u;
-        P.runs_out = s->d_runs;
-        P.batch = run_k ? MRT_RUN_BATCH : MRT_BATCH;
-        P.tail_batch = run_k ? MRT_RUN_TAIL_BATCH : MRT_TAIL_BATCH;
-        P.n_paths = s->npix * (run_k ? P.run_c : s1 - s0);  // work units
-        P.tail_zone = (uint32_t)std::min<uint64_t>((uint64_t)PL.grid * (PL.wg / 64u) * 2 * P.batch, P.n_paths);  // ~2 big claims per wave
-        P.static_first = (uint64_t)P.n_paths < (uint64_t)PL.grid * (PL.wg / 64u) * P.batch * 64u;
+        P.n_paths = s->npix * (s1 - s0);
+        P.tail_zone = (uint32_t)std::min<uint64_t>((uint64_t)PL.grid * (PL.wg / 64u) * 2 * MRT_BATCH, P.n_paths);  // ~2 big claims per wave
+        P.static_first = (uint64_t)P.n_paths < (uint64_t)PL.grid * (PL.wg / 64u) * MRT_BATCH * 64u;
         // MRT_NPART contiguous work partitions, one counter each; the waves of partition k (workgroups
         // b with b % MRT_NPART == k) take its first batches statically when P.static_first
         for (uint32_t k = 0; k <= MRT_NPART; k++) P.part_base[k] = (uint64_t)P.n_paths * k / MRT_NPART;
         for (uint32_t k = 0; k < MRT_NPART; k++) {
             const uint64_t waves_k = (uint64_t)((PL.grid - k + MRT_NPART - 1) / MRT_NPART) * (PL.wg / 64u);
-            P.part_dyn[k] = P.part_base[k] + (P.static_first ? waves_k * P.batch : 0);
+            P.part_dyn[k] = P.part_base[k] + (P.static_first ? waves_k * MRT_BATCH : 0);
         }
         P.seed = d->seed;
         P.max_bounces = d->max_bounces;
@@ -1112,10 +1060,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         HIPCHK(hipEventRecord(s->ev[2 * s->n_launch + 1], q));
         s->n_launch++;
         uint32_t blocks = (s->npix + 255) / 256;
-        if (run_k)
-            hipLaunchKernelGGL(mrt_fold_runs_kernel, dim3(blocks), dim3(256), 0, q, s->d_runs, s->d_acc, s->npix, P.run_c);
-        else
-            hipLaunchKernelGGL(mrt_fold_kernel, dim3(blocks), dim3(256), 0, q, s->d_rad, s->d_acc, s->npix, s0, s1, d->mode, d->max_luminance);
+        hipLaunchKernelGGL(mrt_fold_kernel, dim3(blocks), dim3(256), 0, q, s->d_rad, s->d_acc, s->npix, s0, s1, d->mode, d->max_luminance);
         HIPCHK(hipGetLastError());
         if (preview) {  // the image after s1 samples, copied under the sequence lock
             hipLaunchKernelGGL(mrt_final_kernel, dim3(blocks), dim3(256), 0, q, s->d_acc, s->d_prev, s->npix, s1, d->mode, d->max_luminance);
@@ -1271,9 +1216,6 @@ extern "C" mrt_status mrt_scene_kernel_info(const mrt_scene* s, mrt_kernel_info*
     out->vgprs = L.vgprs;
     out->wg = L.wg;
     out->tree_nodes = L.tree_n;
-    mrt_render_desc fd{};
-    fd.flags = MRT_RF_FAST;
-    out->run_k = run_k_of(s, &fd);
     return MRT_OK;
 }
 
