@@ -61,6 +61,9 @@ def parse():
     ap.add_argument("--emulate-rank", type=int, default=0)
     ap.add_argument("--chunk-samples", type=int, default=0,
                     help="samples per path-kernel launch (0: the library's choice)")
+    ap.add_argument("--fold", choices=["auto", "lean", "full"], default="auto",
+                    help="mode-0 fold kernel: lean (MRT_RF_FOLD_BEHIND, runs beside the other context's "
+                         "path kernel), full (after it); auto = lean when --pipeline > 1")
     ap.add_argument("--pipeline", type=int, default=2,
                     help="render contexts used round-robin on their own HIP streams: step i+1's launch "
                          "fills the CUs freed by step i's tail instead of waiting for it")
@@ -200,6 +203,7 @@ def main():
     # scene build + upload + workspace: outside the timed region (main.cpp:309 precedes 375)
     scene = m.select_scene(args.scene, args.width / args.height)
     npipe = max(1, args.pipeline)
+    lean_fold = args.fold == "lean" or (args.fold == "auto" and npipe > 1)
     rnds = [m.Renderer(scene, device=local) for _ in range(npipe)]
     rnd = rnds[0]
     d_rank, d_world = rank, world
@@ -207,7 +211,8 @@ def main():
         d_rank, d_world = args.emulate_rank, args.emulate_world
     def desc_of(numerics):
         return m.render_desc(args.width, args.height, args.samples, depth=args.depth, tile_size=args.tile_size,
-                             rank=d_rank, world=d_world, numerics=numerics, chunk_samples=args.chunk_samples)
+                             rank=d_rank, world=d_world, numerics=numerics, chunk_samples=args.chunk_samples,
+                             flags=m._lib.RF_FOLD_BEHIND if lean_fold else 0)
 
     desc = desc_of(args.numerics)
     for r in rnds:
@@ -362,7 +367,7 @@ def main():
                                    f"{desc.sqrt_samples ** 2} spp, depth {args.depth}, draw() accumulation",
                        "scene": args.scene, "width": args.width, "height": args.height,
                        "spp": desc.sqrt_samples ** 2, "depth": args.depth, "parallelism": f"tiles{world}",
-                       "tile_size": args.tile_size, "pipeline": npipe, "numerics": args.numerics,
+                       "tile_size": args.tile_size, "pipeline": npipe, "fold": "lean" if lean_fold else "full", "numerics": args.numerics,
                        **({"emulated_share": f"rank {d_rank} of {d_world}"} if d_world != world else {}),
                        "rays_per_step": nrays // args.steps},
             "roofline": roofline,

@@ -114,6 +114,10 @@ typedef struct mrt_render_desc {
                                   mode 0: the mean of the samples so far) is copied to pinned host
                                   memory in stream order (G_linearBackBuffer as the UI thread reads
                                   it every 33 ms, main.cpp:387-444) */
+#define MRT_RF_FOLD_BEHIND 0x8u /* mode 0: fold with a kernel lean enough (8 VGPRs) to run beside
+                                   another context's persistent path kernel instead of after it --
+                                   for callers that pipeline renders on several streams; slower
+                                   when nothing else runs (same bits either way) */
 
 void mrt_default_render_desc(const mrt_params* p, mrt_render_desc* d);
 

@@ -17,6 +17,7 @@ MRT_NONE = 0xFFFFFFFF
 RF_PATH_DEBUG = 0x1
 RF_FAST = 0x2  # tolerance numerics contract (include/mrt.h MRT_RF_FAST)
 RF_PREVIEW = 0x4  # keep a progressive preview for mrt_preview (include/mrt.h MRT_RF_PREVIEW)
+RF_FOLD_BEHIND = 0x8  # mode-0 fold that runs beside another context's path kernel (include/mrt.h)
 DEVICE_CPU = -1  # mrt_scene_upload device of the CPU backend (include/mrt.h MRT_DEVICE_CPU)
 
 

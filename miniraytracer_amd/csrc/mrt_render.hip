@@ -78,6 +78,33 @@ __global__ void __launch_bounds__(256) mrt_fold_kernel(const float* __restrict__
     acc[lp] = make_float4(c.x, c.y, c.z, 0.0f);
 }
 
+// draw()'s fold (mode 0) in 8 VGPRs: the persistent path kernel fills 7 waves per SIMD with 72
+// VGPRs each (504 of 512), so only a kernel this lean fits the 8th wave slot beside it -- the fold
+// of one render then runs under the next render's path kernel (bench.py --pipeline, two contexts
+// on two streams) instead of after it.  Buffer loads (a scalar resource + one 32-bit VGPR offset;
+// a launch chunk's radiance is < 4 GiB, mrt_prepare) keep it at 8 VGPRs: the offset, the acc
+// offset, c and one sample, so one 12-B load is in flight per lane.  (Staging rows in LDS with
+// buffer loads to LDS was tried: the compiler then reserves 97 VGPRs for the kernel.)  The same
+// operations in the same order as mrt_fold_kernel (bit-identical).
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(8)))
+mrt_fold_lean_kernel(const float* __restrict__ rad, float4* __restrict__ acc, uint32_t npix, uint32_t n) {
+    const uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
+    if (lp >= npix) return;
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rad), 0, 0xFFFFFFFFu, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(acc, 0, 0xFFFFFFFFu, 0x00020000);
+    const auto a = __builtin_amdgcn_raw_buffer_load_b96(ra, lp * 16u, 0, 0);
+    f3 c{__uint_as_float(a[0]), __uint_as_float(a[1]), __uint_as_float(a[2])};
+    const uint32_t stride = npix * 12u;
+    uint32_t off = lp * 12u;
+    for (uint32_t s = 0; s < n; s++, off += stride) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b96(rr, off, 0, 2 /* nt */);
+        c = fold_sample(c, f3{__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2])}, s, 0u, 0.0f);
+    }
+    using u3 = decltype(a);
+    const u3 o = {__float_as_uint(c.x), __float_as_uint(c.y), __float_as_uint(c.z)};
+    __builtin_amdgcn_raw_buffer_store_b96(o, ra, lp * 16u, 0, 0);
+}
+
 __global__ void __launch_bounds__(256) mrt_final_kernel(const float4* __restrict__ acc, float4* __restrict__ out, uint32_t npix, uint32_t ns,
                                                        uint32_t mode, float max_lum) {
     uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1060,7 +1087,10 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         HIPCHK(hipEventRecord(s->ev[2 * s->n_launch + 1], q));
         s->n_launch++;
         uint32_t blocks = (s->npix + 255) / 256;
-        hipLaunchKernelGGL(mrt_fold_kernel, dim3(blocks), dim3(256), 0, q, s->d_rad, s->d_acc, s->npix, s0, s1, d->mode, d->max_luminance);
+        if ((d->flags & MRT_RF_FOLD_BEHIND) && d->mode == 0)
+            hipLaunchKernelGGL(mrt_fold_lean_kernel, dim3(blocks), dim3(256), 0, q, s->d_rad, s->d_acc, s->npix, s1 - s0);
+        else
+            hipLaunchKernelGGL(mrt_fold_kernel, dim3(blocks), dim3(256), 0, q, s->d_rad, s->d_acc, s->npix, s0, s1, d->mode, d->max_luminance);
         HIPCHK(hipGetLastError());
         if (preview) {  // the image after s1 samples, copied under the sequence lock
             hipLaunchKernelGGL(mrt_final_kernel, dim3(blocks), dim3(256), 0, q, s->d_acc, s->d_prev, s->npix, s1, d->mode, d->max_luminance);

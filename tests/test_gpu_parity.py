@@ -362,6 +362,40 @@ def test_concurrent_contexts_on_two_streams(gpu):
         c.close()
 
 
+@pytest.mark.parametrize("numerics,chunk", [("exact", 0), ("fast", 0), ("fast", 24)])
+def test_lean_fold_equals_fold(gpu, numerics, chunk):
+    """MRT_RF_FOLD_BEHIND (the 8-VGPR mode-0 fold bench.py --pipeline uses) performs the same adds
+    in the same order as the full fold: same image bits, alone and with two contexts on two streams."""
+    import torch
+    w, h, spp = 96, 80, 64
+    sc, r0 = renderer(gpu, 5, w, h)
+    ref, rays1 = r0.render(gpu.render_desc(w, h, spp, numerics=numerics, chunk_samples=chunk))
+    d = gpu.render_desc(w, h, spp, numerics=numerics, chunk_samples=chunk, flags=gpu._lib.RF_FOLD_BEHIND)
+    img, rays = r0.render(d)
+    assert rays == rays1
+    assert np.array_equal(img[..., :3].view(np.uint32), ref[..., :3].view(np.uint32))
+    ctx = [gpu.Renderer(sc, 0) for _ in range(2)]
+    for c in ctx:
+        c.prepare(d)
+    px = gpu.local_pixels(d)
+    dev = torch.device("cuda", 0)
+    outs = [torch.zeros((len(px), 4), dtype=torch.float32, device=dev) for _ in range(2)]
+    rays_d = torch.zeros(1, dtype=torch.int64, device=dev)
+    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    torch.cuda.synchronize(dev)
+    for _ in range(3):
+        for c, o, s in zip(ctx, outs, streams):
+            c.render_device(d, o.data_ptr(), rays_d.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize(dev)
+    assert int(rays_d.item()) == 6 * rays1
+    for o in outs:
+        im = np.zeros((w * h, 4), dtype=np.float32)
+        im[px] = o.cpu().numpy()
+        assert np.array_equal(im.reshape(h, w, 4)[..., :3].view(np.uint32), ref[..., :3].view(np.uint32))
+    for c in ctx:
+        c.close()
+
+
 # Tolerance of the small shipped fixtures.  The difference between two renders on the same path
 # streams comes only from paths that diverge (a rounding difference sends them elsewhere); its
 # per-pixel RMSE shrinks like 1/sqrt(spp) (SURVEY 8(d), calibration).  The north-star bar is
