@@ -64,6 +64,15 @@ def test_default_render_desc_carries_numerics(mrt):
         assert (d.sqrt_samples, d.flags & mrt._lib.RF_FAST) == (4, flag)
 
 
+def test_render_flags_match_header(mrt):
+    """The ctypes mirror's MRT_RF_* bits are the header's (include/mrt.h)."""
+    hdr = open(os.path.join(os.path.dirname(__file__), "..", "include", "mrt.h")).read()
+    bits = {m.group(1): int(m.group(2), 16) for m in re.finditer(r"#define MRT_RF_(\w+) (0x[0-9a-fA-F]+)u", hdr)}
+    assert set(bits) == {"PATH_DEBUG", "FAST", "PREVIEW", "FOLD_BEHIND"}
+    for name, v in bits.items():
+        assert getattr(mrt._lib, "RF_" + name) == v, name
+
+
 def reference_tiles(W, H, ts):
     """work_queue::work_queue (work_queue.cpp:64-128), restated in numpy-free Python."""
     xc, yc = (W + ts - 1) // ts, (H + ts - 1) // ts
