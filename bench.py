@@ -205,12 +205,18 @@ def main():
     # scene build + upload + workspace: outside the timed region (main.cpp:309 precedes 375)
     scene = m.select_scene(args.scene, args.width / args.height)
     npipe = max(1, args.pipeline)
-    lean_fold = args.fold == "lean" or (args.fold == "auto" and npipe > 1)
     rnds = [m.Renderer(scene, device=local) for _ in range(npipe)]
     rnd = rnds[0]
     d_rank, d_world = rank, world
     if world == 1 and args.emulate_world > 1:
         d_rank, d_world = args.emulate_rank, args.emulate_world
+    # The lean fold keeps one load in flight per lane, so beside the other contexts' path kernels it
+    # needs ~ns load round trips whatever the pixel count: it wins while the rank's path kernel is
+    # long (C2 per-rank share, lean vs full, ms/step: 1 rank 8.36 / 8.59, 2: 4.16 / 4.30, 4: 2.19 /
+    # 2.16, 8: 1.19 / 1.15; tools/_fold_world.sh) -- auto: lean from ~96 M paths per rank
+    n_paths_local = len(m.local_pixels(m.render_desc(args.width, args.height, args.samples, tile_size=args.tile_size,
+                                                     rank=d_rank, world=d_world))) * (int(np.sqrt(np.float32(args.samples))) ** 2)
+    lean_fold = args.fold == "lean" or (args.fold == "auto" and npipe > 1 and n_paths_local >= 96_000_000)
     def desc_of(numerics):
         return m.render_desc(args.width, args.height, args.samples, depth=args.depth, tile_size=args.tile_size,
                              rank=d_rank, world=d_world, numerics=numerics, chunk_samples=args.chunk_samples,
