@@ -2,7 +2,10 @@
 
 Bar: bit-exact.  Per-path radiance, per-path ray counts, total ray count (the Mrays/s numerator,
 main.cpp:68) and the accumulated image must equal the reference's own trace() (stream-matched
-fixtures) and the C restatement, float bits included."""
+fixtures) and the C restatement, float bits included.  The stream fixtures come from the reference
+built exact: its own sources with -ffp-contract=off and its transcendentals from the project's
+include/mrt_mathfn.h ("reference + project libm").  The independent check against
+the reference AS SHIPPED (FMA, glibc libm) is the tolerance suite below (shipped_stream_*)."""
 import os
 import threading
 
