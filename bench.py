@@ -61,14 +61,15 @@ def parse():
     ap.add_argument("--emulate-rank", type=int, default=0)
     ap.add_argument("--chunk-samples", type=int, default=0,
                     help="samples per path-kernel launch (0: the library's choice)")
-    ap.add_argument("--fold", choices=["auto", "lean", "full"], default="auto",
-                    help="mode-0 fold kernel: lean (MRT_RF_FOLD_BEHIND, runs beside the other context's "
-                         "path kernel), full (after it); auto = lean when --pipeline > 1")
+    ap.add_argument("--fold", choices=["auto", "lean", "full"], default="full",
+                    help="mode-0 fold kernel: full (after its render's path kernel; the default), lean "
+                         "(MRT_RF_FOLD_BEHIND, beside the other contexts' path kernels: 8.35-8.45 ms per "
+                         "C2 step in most runs but 9.8-10.1 in about one of five, against a steady 8.62 "
+                         "for full), auto = lean from ~96 M paths per rank")
     ap.add_argument("--pipeline", type=int, default=3,
                     help="render contexts used round-robin on their own HIP streams: step i+1's launch "
-                         "fills the CUs freed by step i's tail instead of waiting for it, and step i's "
-                         "(lean) fold runs beside the next steps' path kernels (C2 per step, lean fold: "
-                         "8.60 / 8.46 / 8.56 ms at 2 / 3 / 4 contexts; full fold at 2: 8.66)")
+                         "fills the CUs freed by step i's tail instead of waiting for it (C2 per step, full "
+                         "fold: 8.66 / 8.61 ms at 2 / 3 contexts)")
     ap.add_argument("--verify", action="store_true",
                     help="after timing, rank 0 checks the assembled framebuffer of the last step against a "
                          "single-context full render, bit for bit")
