@@ -8,9 +8,14 @@ to rank 0 over RCCL and scattered into the full framebuffer.  The image is fixed
 (strong scaling); tile k of the work_queue order belongs to rank k % N.
 
 Prints ONE JSON line (rank 0).  `value` = total rays traced by all ranks / max-over-ranks wall
-time of the K timed steps.  `roofline` prices the dominant kernel (mrt_path_kernel) by the
-algorithmic bytes per ray of SURVEY.md 8(d) over its HIP-event-measured duration.  `cpu_baseline`
-times the reference itself (oracle/_ref/mrt_ref, as shipped) on a bounded sample on this host.
+time of the K timed steps.  `roofline` bounds the dominant kernel (mrt_path_kernel) by what limits
+it, VALU issue: its VALU wave-instructions per launch (rocprofv3 SQ_INSTS_VALU per ray, committed
+under profiles/, times the launch's rays) over its HIP-event-measured duration, against the issue
+peak of 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction; beside it the measured HBM bytes
+(hbm_frac) and the reference-equivalent bytes of SURVEY.md 8(d) (ref_equiv: served by caches, not
+a ceiling).  `parity` compares the last timed step's image with the reference as shipped on the
+same per-path streams (tests/golden fixture), after the timed region.  `cpu_baseline` times the
+reference itself (oracle/_ref/mrt_ref, as shipped) on a bounded sample on this host.
 """
 import argparse
 import json
@@ -25,12 +30,19 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "Mrays/sec (primary+secondary), Cornell box 32-bounce; per-pixel RMSE vs CPU"
-# algorithmic bytes per ray: sum over the reference's tests per ray of the compact
-# FP32 payload each test reads (aabb 24-32 B, rect 24 B, sphere 16 B, triangle 36 B, instance 20 B)
+# reference-equivalent bytes per ray: sum over the reference's tests per ray of the
+# compact FP32 payload each test reads (aabb 24-32 B, rect 24 B, sphere 16 B, triangle 36 B,
+# instance 20 B).  The scenes are cache-resident and the tolerance kernels replace most of those
+# tests (the Cornell slab walks), so this is a reference-work rate, not an HBM ceiling.
 B_RAY = {5: 256.0, 9: 434.0, 8: 1251.0, 7: 780.0, 0: 976.0}
-HBM_PEAK_GBS = 8000.0
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD per 2 cycles
+# (MI355X_MICROARCH.md: 32 lanes/cycle), at the 2.4 GHz peak engine clock
+N_SIMD = 1024
+CLOCK_PEAK_GHZ = 2.4
+VALU_PEAK_G = N_SIMD * CLOCK_PEAK_GHZ / 2.0  # G wave-instructions/s
 WORKLOAD = {5: "C2 cornell_box", 9: "C3 wt_teapot in cornell box", 8: "C4 bunny", 7: "C5 book2 final scene",
-            0: "C1 random spheres"}  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+            0: "C1 random spheres"}
 
 
 def parse():
@@ -73,7 +85,13 @@ def parse():
     ap.add_argument("--verify", action="store_true",
                     help="after timing, rank 0 checks the assembled framebuffer of the last step against a "
                          "single-context full render, bit for bit")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_cornell_c2.json"))
+    ap.add_argument("--pmc-json", default=None,
+                    help="per-ray PMC figures of the workload (default: profiles/pmc_s<scene>_<W>x<H>.json, "
+                         "written by tools/pmc_summary.py --bench-file)")
+    ap.add_argument("--no-other-walk", action="store_true",
+                    help="skip timing the general hit walk (MRT_NO_SIG=1: the linear-program interpreter) "
+                         "beside a shape-specialised one")
+    ap.add_argument("--no-parity", action="store_true")
     return ap.parse_args()
 
 
@@ -127,36 +145,91 @@ def cpu_baseline(args):
             "sample": sample + f", C restatement oracle/liboracle.so, {rays} rays in {dt:.2f} s"}
 
 
-def roofline_counters(args, k_ms):
-    """Counter-derived figures of the dominant kernel from the committed rocprofv3 PMC summary of
-    the same workload (profiles/pmc_cornell_c2.json -> profiles/<tag>_pmc.json, tools/pmc_summary.py):
-    measured HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md), VALU issue
-    busy and VALU lane utilisation.  hbm_frac prices the measured bytes over the live kernel time."""
-    if not os.path.exists(args.pmc_json):
-        return {}
-    pmc = json.load(open(args.pmc_json))
-    if pmc.get("config") != [args.scene, args.width, args.height, args.samples, args.depth]:
-        return {}
-    e = pmc.get("by_numerics", {}).get(args.numerics)
-    if not e:
-        return {}
-    out = {"traffic": e.get("hbm_bytes_per_launch"), "pmc_source": pmc.get("source")}
-    if out["traffic"]:
-        out["hbm_frac"] = round(out["traffic"] / (k_ms * 1e-3) / (HBM_PEAK_GBS * 1e9), 5)
-    for k in ("valu_busy", "valu_lane_util"):
-        if e.get(k) is not None:
-            out[k] = round(e[k], 4)
+def pmc_path(args):
+    return args.pmc_json or os.path.join(ROOT, "profiles", f"pmc_s{args.scene}_{args.width}x{args.height}.json")
+
+
+def roofline(args, k_ms, rays_per_launch, numerics, kinfo):
+    """Roofline of the dominant kernel from the live HIP-event kernel time and this launch's rays,
+    priced by the committed rocprofv3 per-ray counters of the same workload (profiles/pmc_*.json,
+    tools/pmc_summary.py): VALU wave-instructions per ray -> VALU issue rate vs its peak (the bound:
+    C2's path kernel issues VALU on ~3/4 of SIMD cycles), HBM bytes per ray (2*FETCH_SIZE +
+    WRITE_SIZE, MI355X_MICROARCH.md) -> hbm_frac.  Per-ray figures, so a rank's share (world > 1)
+    is priced by its own rays; they do not depend on spp."""
+    k_s = k_ms * 1e-3
+    out = {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_G, 1), "unit": "G VALU wave-instr/s", "frac": None,
+           "traffic": None, "kernel": "mrt_path_kernel" + ("_fast" if numerics == "fast" else ""), "kernel_ms": round(k_ms, 3),
+           "rays_per_launch": int(rays_per_launch),
+           **{k: kinfo[k] for k in ("grid", "wg", "lds_bytes", "vgprs", "tree_nodes")}}
+    b_ray = B_RAY.get(args.scene)
+    if b_ray is not None:
+        gbs = rays_per_launch * b_ray / k_s / 1e9
+        out["ref_equiv"] = {"bytes_per_ray": b_ray, "GBps": round(gbs, 1), "vs_hbm_peak": round(gbs / HBM_PEAK_GBS, 4),
+                            "note": "reference-equivalent bytes (SURVEY 8(d) B_ray): what the reference's tests read per ray; "
+                                    "cache-served here, not an HBM ceiling"}
+    p = pmc_path(args)
+    if not os.path.exists(p):
+        out["note"] = f"no PMC profile {os.path.relpath(p, ROOT)} for this workload: frac unmeasured"
+        return out
+    pmc = json.load(open(p))
+    cfg = pmc.get("config") or []
+    e = pmc.get("by_numerics", {}).get(numerics)
+    if cfg[:3] != [args.scene, args.width, args.height] or (len(cfg) > 4 and cfg[4] != args.depth) or not e:
+        out["note"] = f"{os.path.relpath(p, ROOT)} is for config {cfg}: frac unmeasured"
+        return out
+    out["pmc_source"] = pmc.get("source")
+    vpr = e.get("valu_insts_per_ray")
+    if vpr:
+        ach = vpr * rays_per_launch / k_s / 1e9
+        out["achieved"] = round(ach, 1)
+        out["frac"] = round(ach / VALU_PEAK_G, 4)
+        out["valu_insts_per_ray"] = round(vpr, 3)
+    if e.get("valu_lane_util") is not None:
+        out["valu_lane_util"] = round(e["valu_lane_util"], 4)
+        if out["frac"] is not None:
+            out["lane_frac"] = round(out["frac"] * e["valu_lane_util"], 4)  # of the lane-throughput peak
+    if e.get("valu_busy") is not None:
+        out["valu_busy_pmc"] = round(e["valu_busy"], 4)  # the profiler's own issue-cycle fraction
+    bpr = e.get("hbm_bytes_per_ray")
+    if bpr:
+        out["traffic"] = round(bpr * rays_per_launch)
+        out["hbm_GBps"] = round(out["traffic"] / k_s / 1e9, 1)
+        out["hbm_peak"] = HBM_PEAK_GBS
+        out["hbm_frac"] = round(out["hbm_GBps"] / HBM_PEAK_GBS, 5)
     return out
+
+
+def visible_gpus():
+    """GPUs this process may use, counted without any HIP call: KFD topology nodes with SIMDs
+    (sysfs), narrowed by HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES."""
+    n = 0
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        for d in os.listdir(base):
+            try:
+                props = dict(line.split()[:2] for line in open(os.path.join(base, d, "properties")) if line.strip())
+            except (OSError, ValueError):
+                continue
+            if int(props.get("simd_count", "0")) > 0:
+                n += 1
+    except OSError:
+        pass
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
 
 
 def launch_ranks(args):
     """`bench.py --gpus N` without a launcher: start N rank processes of this script (one per GPU,
     RANK/LOCAL_RANK/WORLD_SIZE set, rendezvous on 127.0.0.1), like main() spawns one thread per
-    worker (main.cpp:376-382).  This parent never touches the GPU or imports the package."""
+    worker (main.cpp:376-382).  This parent makes no HIP call (GPUs counted from sysfs) and does
+    not import torch or the package; if any rank fails, the others are stopped and its exit code
+    returned (instead of the rest waiting in a collective until a timeout)."""
     import socket
-    import torch  # device_count() does not initialise HIP
     same = bool(os.environ.get("MRT_SAME_GPU"))
-    ndev = torch.cuda.device_count()
+    ndev = visible_gpus()
     if args.gpus > ndev and not same:
         print(f"bench.py: --gpus {args.gpus} but {ndev} GPU(s) visible (set MRT_SAME_GPU=1 to rehearse "
               f"several ranks on one GPU)", file=sys.stderr)
@@ -171,8 +244,25 @@ def launch_ranks(args):
                    LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
     rc = 0
-    for p in procs:
-        rc = max(rc, p.wait())
+    while procs:
+        time.sleep(0.2)
+        for p in list(procs):
+            r = p.poll()
+            if r is None:
+                continue
+            procs.remove(p)
+            if r != 0:
+                rc = rc or r
+                for q in procs:  # a failed rank: the others would block in a collective
+                    q.terminate()
+                for q in procs:
+                    try:
+                        q.wait(timeout=20)
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+                        q.wait()
+                procs = []
+                break
     return rc
 
 
@@ -241,6 +331,7 @@ def main():
 
     pending = [None]
     it = [0]
+    ctx = [rnds]  # the render contexts measure() uses (the other-walk timing swaps in its own)
 
     def step(d):
         # step i renders with context i % npipe on its stream; nothing orders it after step i-1's
@@ -248,7 +339,7 @@ def main():
         j = it[0] % npipe
         it[0] += 1
         with torch.cuda.stream(streams[j]):
-            rnds[j].render_device(d, outs[j].data_ptr(), rays.data_ptr(), streams[j].cuda_stream)
+            ctx[0][j].render_device(d, outs[j].data_ptr(), rays.data_ptr(), streams[j].cuda_stream)
             if world > 1:
                 # the one RCCL collective of the data path (tile shards -> rank 0), overlapped with
                 # the next render: finish the previous step's gather, then start this one's
@@ -273,7 +364,7 @@ def main():
         # first touch, first launch on its stream) are paid before the warmup steps
         for j in range(npipe):
             with torch.cuda.stream(streams[j]):
-                rnds[j].render_device(d, outs[j].data_ptr(), rays.data_ptr(), streams[j].cuda_stream)
+                ctx[0][j].render_device(d, outs[j].data_ptr(), rays.data_ptr(), streams[j].cuda_stream)
         torch.cuda.synchronize(dev)
         tw = time.perf_counter()
         for _ in range(args.warmup):
@@ -286,7 +377,7 @@ def main():
         # (local renders, no collective: ranks may run different counts before the barrier)
         while time.perf_counter() - tw < 0.5:
             with torch.cuda.stream(streams[0]):
-                rnds[0].render_device(d, outs[0].data_ptr(), rays.data_ptr(), streams[0].cuda_stream)
+                ctx[0][0].render_device(d, outs[0].data_ptr(), rays.data_ptr(), streams[0].cuda_stream)
             torch.cuda.synchronize(dev)
         rays.zero_()
         if world > 1:
@@ -311,52 +402,89 @@ def main():
     desc = desc_of(args.numerics)
     secs, nrays, rays_per_step_local = measure(desc)
 
+    def last_image():
+        """The assembled framebuffer of the last timed step (rank 0; None elsewhere)."""
+        if world > 1:
+            return tg.full.view(args.height, args.width, 4).cpu().numpy() if rank == 0 else None
+        full = np.zeros((args.width * args.height, 4), dtype=np.float32)
+        full[px] = outs[(it[0] - 1) % npipe].cpu().numpy()
+        return full.reshape(args.height, args.width, 4)
+
+    # parity of the timed render (after the timed region): the last step's image against the
+    # reference as shipped on the same per-path streams, when a fixture of this exact config exists
+    fixture = None
+    if not args.no_parity and d_world == world:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from fixture_cmp import compare, fixture_for
+        fixture = fixture_for(args.scene, args.width, args.height, desc.sqrt_samples ** 2, args.depth)
+
+    def parity(nrays_total):
+        if fixture is None or rank != 0:
+            return None
+        r = compare(last_image(), nrays_total // max(args.steps, 1), fixture)
+        return {k: (round(v, 7) if isinstance(v, float) else v) for k, v in r.items()}
+
+    par = parity(nrays)
+
     verified = None
     if args.verify and d_world == world and rank == 0:
-        img = tg.full.view(args.height, args.width, 4) if world > 1 else None
-        if world == 1:
-            full = np.zeros((args.width * args.height, 4), dtype=np.float32)
-            full[px] = outs[(it[0] - 1) % npipe].cpu().numpy()
-            img = full.reshape(args.height, args.width, 4)
+        img = last_image()
         ref, ref_rays = m.Renderer(scene, device=local).render(
             m.render_desc(args.width, args.height, args.samples, depth=args.depth, tile_size=args.tile_size,
                           numerics=args.numerics))
-        got = img[..., :3] if isinstance(img, np.ndarray) else img[..., :3].cpu().numpy()
-        verified = bool(np.array_equal(got.view(np.uint32), ref[..., :3].view(np.uint32))
+        verified = bool(np.array_equal(img[..., :3].view(np.uint32), ref[..., :3].view(np.uint32))
                         and nrays == ref_rays * args.steps)
 
-    # dominant kernel: mrt_path_kernel, HIP events recorded on the launch stream (3 extra renders)
-    def kernel_ms(d):
+    # dominant kernel: mrt_path_kernel, HIP events recorded on the launch stream (extra renders)
+    def kernel_ms(d, r=None):
+        r = r or rnd
         kms = []
         for _ in range(max(args.kernel_reps, 1)):
-            rnd.render_device(d, out.data_ptr(), rays.data_ptr(), stream.cuda_stream)
-            ms, launches = rnd.kernel_ms()
+            r.render_device(d, out.data_ptr(), rays.data_ptr(), stream.cuda_stream)
+            ms, launches = r.kernel_ms()
             kms.append(ms / max(launches, 1))
         return float(np.mean(kms)), max(launches, 1)
 
     k_ms, launches = kernel_ms(desc)
-    b_ray = B_RAY.get(args.scene)
-    roofline = None
-    if b_ray is not None:
-        bytes_per_launch = rays_per_step_local / launches * b_ray
-        achieved = bytes_per_launch / (k_ms * 1e-3) / 1e9
-        roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                    "kernel": "mrt_path_kernel" + ("_fast" if args.numerics == "fast" else ""),
-                    "kernel_ms": round(k_ms, 3), "bytes_per_ray": b_ray,
-                    **{k: rnd.kernel_info()[k] for k in ("grid", "wg", "lds_bytes", "vgprs", "tree_nodes")}}
-        roofline.update(roofline_counters(args, k_ms))
+    roof = roofline(args, k_ms, rays_per_step_local / launches, args.numerics, rnd.kernel_info())
 
     # the other numerics contract, same protocol (reported beside the headline, never as `value`)
     other = None
     if not args.no_compare_numerics:
         alt = "exact" if args.numerics == "fast" else "fast"
         a_secs, a_rays, a_local = measure(desc_of(alt))
+        a_par = parity(a_rays)
         a_kms, a_launches = kernel_ms(desc_of(alt))
+        a_roof = roofline(args, a_kms, a_local / a_launches, alt, rnd.kernel_info())
         other = {"numerics": alt, "value": round(a_rays / a_secs / 1e6, 2), "ms_per_step": round(a_secs / args.steps * 1e3, 3),
-                 "kernel_ms": round(a_kms, 3)}
-        if b_ray is not None:
-            other["roofline_frac"] = round(a_local / a_launches * b_ray / (a_kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+                 "kernel_ms": round(a_kms, 3), "roofline_frac": a_roof["frac"], "valu_lane_util": a_roof.get("valu_lane_util"),
+                 "hbm_frac": a_roof.get("hbm_frac"), "parity": a_par}
+
+    # the general hit walk on the same workload: the shape-specialised walks (mrt_sig.h, e.g. the
+    # Cornell box's slab tests) fire only for known program shapes; this times the linear-program
+    # interpreter every other scene graph of that kind runs (MRT_NO_SIG=1 at scene upload)
+    other_walk = None
+    if not args.no_other_walk and (rnd.kernel_info()["kernel_features"] >> 16) != 0:
+        os.environ["MRT_NO_SIG"] = "1"
+        try:
+            gen = [m.Renderer(scene, device=local) for _ in range(npipe)]
+        finally:
+            del os.environ["MRT_NO_SIG"]
+        for r in gen:
+            r.prepare(desc)
+        ctx[0] = gen
+        g_secs, g_rays, g_local = measure(desc)
+        g_par = parity(g_rays)
+        ctx[0] = rnds
+        g_kms, g_launches = kernel_ms(desc, gen[0])
+        g_roof = roofline(args, g_kms, g_local / g_launches, args.numerics, gen[0].kernel_info())
+        other_walk = {"walk": "linear-program interpreter (MRT_NO_SIG=1)", "numerics": args.numerics,
+                      "kernel_features": gen[0].kernel_info()["kernel_features"],
+                      "value": round(g_rays / g_secs / 1e6, 2), "ms_per_step": round(g_secs / args.steps * 1e3, 3),
+                      "kernel_ms": round(g_kms, 3), "vgprs": g_roof["vgprs"], "parity": g_par,
+                      "note": "VALU per ray differs from the specialised walk: no PMC for it, frac not priced"}
+        for r in gen:
+            r.close()
 
     if rank == 0:
         res = {
@@ -379,9 +507,11 @@ def main():
                        "tile_size": args.tile_size, "pipeline": npipe, "fold": "lean" if lean_fold else "full", "numerics": args.numerics,
                        **({"emulated_share": f"rank {d_rank} of {d_world}"} if d_world != world else {}),
                        "rays_per_step": nrays // args.steps},
-            "roofline": roofline,
+            "roofline": roof,
+            "parity": par,
             "cpu_baseline": None,
             "other_numerics": other,
+            "other_walk": other_walk,
         }
         if verified is not None:
             res["verify_bit_exact"] = verified

@@ -54,6 +54,10 @@ typedef struct mrt_params {
     uint32_t gpus;            /* -gpus: GPUs to shard the work_queue tiles over (0 = every visible GPU) */
     uint32_t numerics;        /* -numerics: 0 exact contract, 1 tolerance contract (MRT_RF_FAST) */
     uint32_t backend;         /* -backend: 0 GPU (default), 1 CPU (MRT_DEVICE_CPU, -threads workers, exact) */
+    uint32_t order;           /* -order: 0 = per-path stream keys (the GPU's; any thread / GPU count gives
+                                 the same image), 1 = the reference's RNG order (one PCG stream per worker
+                                 thread, work_queue order; CPU backend only, MRT_RF_REF_ORDER).  Default:
+                                 1 with -backend cpu, 0 otherwise */
 } mrt_params;
 
 void mrt_default_params(mrt_params* p);
@@ -75,9 +79,9 @@ void mrt_free_string(char* s);
 mrt_status mrt_pack_obj(const char* obj_path, const char* out_path);
 void mrt_scene_blob_free(mrt_scene_blob* blob);
 /* The (initstate, initseq) main() hands its worker threads (main.cpp:357-361): drawn from the main
- * thread's PCG after select_scene consumed what it needs.  Only the reference's own deterministic
- * mode (-threads 1) depends on them: the CPU backend's ref-order renders and the oracle's
- * reference-RNG-order restatement use them; the GPU path keys its streams per path instead. */
+ * thread's PCG after select_scene consumed what it needs.  Only renders in the reference's own RNG
+ * order depend on them (the CPU backend's MRT_RF_REF_ORDER renders, via mrt_set_worker_seeds, and
+ * the oracle's restatement); the GPU path keys its streams per path instead. */
 mrt_status mrt_worker_seeds(const mrt_scene_blob* blob, uint32_t n_threads, uint64_t* initstate, uint64_t* initseq);
 
 /* ---- device -------------------------------------------------------------------------------- */
@@ -90,6 +94,9 @@ typedef struct mrt_scene mrt_scene;
 #define MRT_DEVICE_CPU (-1)
 mrt_status mrt_scene_upload(int device, const mrt_scene_view* view, mrt_scene** out);
 void mrt_scene_free(mrt_scene* scene);
+/* CPU backend only: the drawArgs (initstate, initseq) of each worker thread (main.cpp:127-135,
+ * 357-366; from mrt_worker_seeds) for renders with MRT_RF_REF_ORDER, which run n_threads workers. */
+mrt_status mrt_set_worker_seeds(mrt_scene* s, uint32_t n_threads, const uint64_t* initstate, const uint64_t* initseq);
 
 typedef struct mrt_render_desc {
     uint32_t width, height;
@@ -118,6 +125,13 @@ typedef struct mrt_render_desc {
                                    another context's persistent path kernel instead of after it --
                                    for callers that pipeline renders on several streams; slower
                                    when nothing else runs (same bits either way) */
+#define MRT_RF_REF_ORDER 0x10u  /* CPU backend: the reference's own RNG order -- worker i draws from
+                                   one PCG stream seeded by mrt_set_worker_seeds' i-th pair; mode 0 =
+                                   draw() over work_queue_seq (tile -> pixel -> sample), mode 1 =
+                                   draw2() over work_queue_dynamic ((tile, sample) items,
+                                   work_queue.cpp:133-166).  One thread reproduces the reference's
+                                   -threads 1 run bit for bit (its deterministic mode,
+                                   cmdline_parser.h:15); world must be 1 */
 
 void mrt_default_render_desc(const mrt_params* p, mrt_render_desc* d);
 

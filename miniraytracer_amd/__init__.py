@@ -90,16 +90,19 @@ NUMERICS = ("exact", "fast")
 
 
 def render_desc(width, height, samples, depth=32, max_luminance=1000.0, mode=0, seed=MAIN_SEED, tile_size=32,
-                rank=0, world=1, chunk_samples=0, flags=0, numerics="exact", threads=0, preview=False):
+                rank=0, world=1, chunk_samples=0, flags=0, numerics="exact", threads=0, preview=False, ref_order=False):
     """Render description; `samples` is floored to a perfect square like main.cpp:319-320.
     numerics: "exact" (bit-for-bit the reference built exact) or "fast" (tolerance contract:
-    per-pixel RMSE < 1e-3 vs the reference as shipped; MRT_RF_FAST)."""
+    per-pixel RMSE < 1e-3 vs the reference as shipped; MRT_RF_FAST).  ref_order (CPU backend): the
+    reference's own RNG order, one stream per worker thread (Renderer.set_worker_seeds)."""
     if numerics not in NUMERICS:
         raise ValueError(f"numerics must be one of {NUMERICS}")
     if numerics == "fast":
         flags |= _lib.RF_FAST
     if preview:
         flags |= _lib.RF_PREVIEW
+    if ref_order:
+        flags |= _lib.RF_REF_ORDER
     sq = int(np.sqrt(np.float32(samples)))
     return MrtRenderDesc(width, height, sq, depth, max_luminance, mode, seed, tile_size, rank, world,
                          chunk_samples, flags, threads)
@@ -145,6 +148,13 @@ class Renderer:
         check(lib().mrt_render(self._h, C.byref(desc), img.ctypes.data, C.byref(rays), C.byref(cancel) if cancel is not None else None),
               "mrt_render")
         return img, rays.value
+
+    def set_worker_seeds(self, seeds):
+        """CPU backend: the (initstate, initseq) of each worker thread (main.cpp:357-366, e.g.
+        scene.worker_seeds(n)) for renders in the reference's RNG order (render_desc(ref_order=True))."""
+        a = np.array([s[0] for s in seeds], dtype=np.uint64)
+        b = np.array([s[1] for s in seeds], dtype=np.uint64)
+        check(lib().mrt_set_worker_seeds(self._h, len(seeds), a.ctypes.data, b.ctypes.data), "mrt_set_worker_seeds")
 
     def prepare(self, desc):
         check(lib().mrt_prepare(self._h, C.byref(desc)), "mrt_prepare")

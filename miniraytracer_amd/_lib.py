@@ -18,6 +18,7 @@ RF_PATH_DEBUG = 0x1
 RF_FAST = 0x2  # tolerance numerics contract (include/mrt.h MRT_RF_FAST)
 RF_PREVIEW = 0x4  # keep a progressive preview for mrt_preview (include/mrt.h MRT_RF_PREVIEW)
 RF_FOLD_BEHIND = 0x8  # mode-0 fold that runs beside another context's path kernel (include/mrt.h)
+RF_REF_ORDER = 0x10  # CPU backend: the reference's own RNG order (worker streams, work_queue order)
 DEVICE_CPU = -1  # mrt_scene_upload device of the CPU backend (include/mrt.h MRT_DEVICE_CPU)
 
 
@@ -29,7 +30,7 @@ class MrtParams(C.Structure):
                 ("num_threads", C.c_uint32), ("max_bounces", C.c_uint32),
                 ("scene_select", C.c_uint32), ("threading_mode", C.c_uint32),
                 ("max_luminance", C.c_float), ("delay", C.c_uint32), ("seed", C.c_uint64),
-                ("gpus", C.c_uint32), ("numerics", C.c_uint32), ("backend", C.c_uint32)]
+                ("gpus", C.c_uint32), ("numerics", C.c_uint32), ("backend", C.c_uint32), ("order", C.c_uint32)]
 
 
 class MrtRenderDesc(C.Structure):
@@ -124,6 +125,8 @@ def lib():
     L.mrt_kernel_ms.restype = st
     L.mrt_worker_seeds.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
     L.mrt_worker_seeds.restype = st
+    L.mrt_set_worker_seeds.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
+    L.mrt_set_worker_seeds.restype = st
     L.mrt_pack_obj.argtypes = [C.c_char_p, C.c_char_p]
     L.mrt_pack_obj.restype = st
     L.mrt_tonemap_argb.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
@@ -148,5 +151,5 @@ EXPORTS = [
     "mrt_scene_upload", "mrt_scene_free", "mrt_default_render_desc", "mrt_local_pixels",
     "mrt_render", "mrt_render_device", "mrt_prepare", "mrt_render_debug", "mrt_progress",
     "mrt_tonemap_argb", "mrt_strerror", "mrt_last_error", "mrt_kernel_ms", "mrt_pack_obj",
-    "mrt_scene_kernel_info", "mrt_preview", "mrt_lum_max_device", "mrt_tonemap_device", "mrt_worker_seeds",
+    "mrt_scene_kernel_info", "mrt_preview", "mrt_lum_max_device", "mrt_tonemap_device", "mrt_worker_seeds", "mrt_set_worker_seeds",
 ]

@@ -57,6 +57,17 @@ int main(int argc, char** argv) {
         descs[r].world = (uint32_t)world;
         if (!cpu && (st = mrt_prepare(scenes[r], &descs[r]))) return fail("prepare", st);
     }
+    if (descs[0].flags & MRT_RF_REF_ORDER) {  // main.cpp:338-366: the workers' (initstate, initseq)
+        if (!cpu) {
+            fprintf(stderr, "-order ref: the reference's per-thread RNG order runs on the CPU backend only (-backend cpu)\n");
+            return 1;
+        }
+        const uint32_t n = p.num_threads ? p.num_threads : std::max(1u, std::thread::hardware_concurrency());
+        std::vector<uint64_t> is(n), iq(n);
+        if ((st = mrt_worker_seeds(blob, n, is.data(), iq.data()))) return fail("worker_seeds", st);
+        if ((st = mrt_set_worker_seeds(scenes[0], n, is.data(), iq.data()))) return fail("set_worker_seeds", st);
+        descs[0].threads = n;
+    }
     std::vector<float> img((size_t)p.buffer_width * p.buffer_height * 4, 0.0f);
     std::vector<uint64_t> rays(world, 0);
     std::vector<mrt_status> sts(world, MRT_OK);

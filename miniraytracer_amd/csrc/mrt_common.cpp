@@ -66,6 +66,7 @@ extern "C" void mrt_default_params(mrt_params* p) {
     p->gpus = 0;
     p->numerics = 1;  // tolerance contract (DESIGN.md "Numerics contracts"); -numerics exact for bit-exact
     p->backend = 0;
+    p->order = 0;
 }
 
 // ReadParameter (cmdline_parser.cpp:41-62): first occurrence wins, value range-checked, a bad
@@ -130,6 +131,9 @@ extern "C" mrt_status mrt_parse_argv(int argc, char** argv, mrt_params* out) {
                "  -backend  \t[gpu, cpu]\tRender on the MI355X(s) (default) or on the host CPU\n"
                "            \t\t\t(the same hot-path code, exact numerics, -threads workers)\n"
                "  -gpus     \t<value>\t\tNumber of GPUs to shard tiles over (0 selects all)\n"
+               "  -order    \t[ref, path]\tRNG order: ref = the reference's (one stream per worker thread,\n"
+               "            \t\t\twork_queue order; CPU backend default: -threads 1 reproduces the\n"
+               "            \t\t\treference's deterministic run), path = per-path stream keys (GPU)\n"
                "  -numerics \t[exact, fast]\tArithmetic contract (exact: bit-for-bit the reference built\n"
                "            \t\t\twithout contraction; fast: per-pixel RMSE < 1e-3, default)\n"
                "  -tilesize \t<value>\t\tSize of image tiles (GPUs own interleaved tiles)\n"
@@ -168,6 +172,13 @@ extern "C" mrt_status mrt_parse_argv(int argc, char** argv, mrt_params* out) {
         else printf("Warning: Invalid value for parameter '-backend', must be gpu or cpu.\n");
     }
     if (p.backend == 1) p.numerics = 0;  // the CPU backend runs the exact contract
+    p.order = p.backend == 1 ? 1u : 0u;  // the reference's own RNG order where it can run
+    if (int i = check_param(argc, argv, "-order")) {
+        const char* v = i + 1 < argc ? argv[i + 1] : "";
+        if (!strcmp(v, "ref")) p.order = 1;
+        else if (!strcmp(v, "path")) p.order = 0;
+        else printf("Warning: Invalid value for parameter '-order', must be ref or path.\n");
+    }
     if (out) *out = p;
     return MRT_OK;
 }
@@ -184,7 +195,7 @@ extern "C" void mrt_default_render_desc(const mrt_params* p, mrt_render_desc* d)
     d->tile_size = p->tile_size;
     d->rank = 0;
     d->world = 1;
-    d->flags = p->numerics ? MRT_RF_FAST : 0u;
+    d->flags = (p->numerics ? MRT_RF_FAST : 0u) | (p->order == 1 ? MRT_RF_REF_ORDER : 0u);
     d->threads = p->num_threads;
 }
 

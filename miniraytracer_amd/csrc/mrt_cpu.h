@@ -11,3 +11,4 @@ mrt_status mrt_cpu_render(mrt_cpu_scene* c, const mrt_render_desc* d, float* rgb
 mrt_status mrt_cpu_progress(mrt_cpu_scene* c, float* pct);
 mrt_status mrt_cpu_last_ms(mrt_cpu_scene* c, float* ms, uint32_t* threads);
 mrt_status mrt_cpu_preview(mrt_cpu_scene* c, float* rgb_out, uint32_t* samples_done);
+mrt_status mrt_cpu_set_worker_seeds(mrt_cpu_scene* c, uint32_t n, const uint64_t* initstate, const uint64_t* initseq);

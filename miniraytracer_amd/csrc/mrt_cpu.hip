@@ -17,6 +17,16 @@
 // order (draw(), main.cpp:138-188), folding them as they come (draw2()'s per-pixel running average
 // is the same fold with mode 1, main.cpp:205-231).  Path streams are keyed per (pixel, sample) as on
 // the GPU, so the image does not depend on the thread count.
+//
+// MRT_RF_REF_ORDER: the reference's own RNG order instead (its deterministic mode at -threads 1,
+// cmdline_parser.h:15): worker i draws every random number from ONE PCG stream seeded with the
+// (initstate, initseq) main() gives it (main.cpp:357-366, handed over by mrt_set_worker_seeds),
+// mode 0 = draw() over work_queue_seq (tile -> pixel -> sample, main.cpp:138-188,
+// work_queue.cpp:133-140), mode 1 = draw2() over work_queue_dynamic (item k -> tile k % n_tiles,
+// sample k / n_tiles; every pixel of the tile gets that sample, main.cpp:193-243,
+// work_queue.cpp:157-166).  At one thread the image and ray count equal the reference's
+// -threads 1 -mode 0|1 (tests/golden/refseq_*.npz); with more threads the result depends on
+// scheduling, as the reference's does.
 #define MRT_HOST_BACKEND 1
 #include <hip/hip_runtime.h>
 
@@ -54,7 +64,15 @@ struct mrt_cpu_scene {
     std::vector<uint32_t> fb_px;  // owned pixels, row-major
     uint32_t fb_w = 0, fb_h = 0, fb_ns = 0;
     std::atomic<uint32_t> tiles_done{0};
-    std::mutex fb_mu;  // render start / preview: the framebuffer's size and owner list
+    uint32_t n_tiles = 0;
+    // mrt_set_worker_seeds: (initstate, initseq) of each worker thread (MRT_RF_REF_ORDER renders)
+    std::vector<uint64_t> seed_state, seed_seq;
+    // MRT_RF_REF_ORDER mode 1: work items published per sample pass (mrt_preview: passes complete)
+    std::vector<uint32_t> pass_items;
+    uint32_t ref_mode1 = 0;
+    // the framebuffer's size, owner list and contents: workers publish a finished work item (a
+    // tile's pixels) under it, mrt_preview copies under it
+    std::mutex fb_mu;
 };
 
 // the two hot-path instantiations of the host backend: any linear hit program through the
@@ -150,6 +168,7 @@ static void render_tiles(mrt_cpu_scene* c, const mrt_render_desc* d, const std::
     for (uint32_t i = 0; i < sq; i++)
         for (uint32_t j = 0; j < sq; j++) sd[(size_t)i * sq + j] = make_float2(((float)i + 0.5f) / (float)sq, ((float)j + 0.5f) / (float)sq);
     uint64_t my_rays = 0;
+    std::vector<float> tb;  // the work item's pixels, published to the framebuffer when done
     for (;;) {
         if (cancel && *cancel) {  // G_isRunning (main.cpp:180)
             cancelled.store(true, std::memory_order_relaxed);
@@ -158,6 +177,8 @@ static void render_tiles(mrt_cpu_scene* c, const mrt_render_desc* d, const std::
         const uint32_t k = next.fetch_add(1, std::memory_order_relaxed);  // work_queue::getWork
         if (k >= tiles.size()) break;
         const mrt_tile& t = tiles[k];
+        const uint32_t tw = t.xmax - t.xmin;
+        tb.assign((size_t)tw * (t.ymax - t.ymin) * 4, 0.0f);
         for (uint32_t y = t.ymin; y < t.ymax; y++)
             for (uint32_t x = t.xmin; x < t.xmax; x++) {
                 const uint32_t pix = x + y * W;
@@ -176,16 +197,107 @@ static void render_tiles(mrt_cpu_scene* c, const mrt_render_desc* d, const std::
                     col = fold_sample(col, L, s, d->mode, d->max_luminance);
                 }
                 col = final_pixel(col, ns, d->mode, d->max_luminance);
-                float* o = c->fb.data() + (size_t)pix * 4;
+                float* o = tb.data() + ((size_t)(x - t.xmin) + (size_t)(y - t.ymin) * tw) * 4;
+                o[0] = col.x;
+                o[1] = col.y;
+                o[2] = col.z;
+            }
+        {
+            std::lock_guard<std::mutex> lk(c->fb_mu);
+            for (uint32_t y = t.ymin; y < t.ymax; y++)
+                memcpy(c->fb.data() + ((size_t)t.xmin + (size_t)y * W) * 4, tb.data() + (size_t)(y - t.ymin) * tw * 4, (size_t)tw * 16);
+        }
+        c->done.fetch_add((uint64_t)tw * (t.ymax - t.ymin) * ns, std::memory_order_relaxed);
+        c->tiles_done.fetch_add(1, std::memory_order_release);
+    }
+    rays_total.fetch_add(my_rays, std::memory_order_relaxed);
+}
+
+// MRT_RF_REF_ORDER: worker `wi` with its own continuing PCG stream (Init_Thread_RNG(initstate,
+// initseq), main.cpp:143 / 198), work items from the shared queue in the reference's order.
+template <uint32_t F>
+static void render_ref_order(mrt_cpu_scene* c, const mrt_render_desc* d, const std::vector<mrt_tile>& tiles, uint32_t wi,
+                             std::atomic<uint64_t>& next, std::atomic<uint64_t>& rays_total, const volatile int* cancel,
+                             std::atomic<bool>& cancelled) {
+    const DScene& S = c->S;
+    const uint32_t sq = d->sqrt_samples, ns = sq * sq, W = d->width;
+    const uint32_t rows = std::max<uint32_t>(d->max_bounces, 1);
+    Stacks st(c->T, rows);
+    const LStack Ls{st.frames.data(), st.rays.data(), st.mesh.data(), st.save.data(), 0u, nullptr, 0u};
+    const LevStore<0> lev{st.lev.data(), rows, 0u, 0u};
+    std::vector<float2> sd(ns);
+    for (uint32_t i = 0; i < sq; i++)
+        for (uint32_t j = 0; j < sq; j++) sd[(size_t)i * sq + j] = make_float2(((float)i + 0.5f) / (float)sq, ((float)j + 0.5f) / (float)sq);
+    Pcg rng;
+    pcg_seed(rng, c->seed_state[wi], c->seed_seq[wi]);
+    const uint64_t nt = tiles.size();
+    const uint64_t items = d->mode == 0 ? nt : nt * ns;  // work_queue_seq: tiles; work_queue_dynamic: (tile, sample)
+    uint64_t my_rays = 0;
+    // one path of the worker's stream: camera::get_ray then trace() (main.cpp:153-157, 208-210)
+    auto path = [&](uint32_t x, uint32_t y, uint32_t s) {
+        PathState ps;
+        ps.rng = rng;
+        const float u = ((float)x + sd[s].x) / (float)d->width, v = ((float)y + sd[s].y) / (float)d->height;
+        ps.r = camera_ray(S, ps.rng, u, v);
+        ps.depth = 0;
+        ps.nlev = 0;
+        ps.rays = 0;
+        const f3 L = trace_path<F>(S, ps, d->max_bounces, lev, Ls);
+        rng = ps.rng;
+        my_rays += ps.rays;
+        return L;
+    };
+    std::vector<float> tb;
+    for (;;) {
+        if (cancel && *cancel) {  // G_isRunning (main.cpp:180, 235)
+            cancelled.store(true, std::memory_order_relaxed);
+            break;
+        }
+        const uint64_t k = next.fetch_add(1, std::memory_order_relaxed);  // work_queue::getWork
+        if (k >= items) break;
+        const mrt_tile& t = tiles[k % nt];
+        const uint32_t s = d->mode == 0 ? 0u : (uint32_t)(k / nt);
+        const uint32_t tw = t.xmax - t.xmin, th = t.ymax - t.ymin;
+        tb.resize((size_t)tw * th * 4);
+        if (d->mode == 1) {  // draw2() folds into the buffer's running average: the tile's current values
+            std::lock_guard<std::mutex> lk(c->fb_mu);
+            for (uint32_t y = t.ymin; y < t.ymax; y++)
+                memcpy(tb.data() + (size_t)(y - t.ymin) * tw * 4, c->fb.data() + ((size_t)t.xmin + (size_t)y * W) * 4, (size_t)tw * 16);
+        }
+        for (uint32_t y = t.ymin; y < t.ymax; y++)
+            for (uint32_t x = t.xmin; x < t.xmax; x++) {
+                float* o = tb.data() + ((size_t)(x - t.xmin) + (size_t)(y - t.ymin) * tw) * 4;
+                f3 col;
+                if (d->mode == 0) {  // draw(): every sample of the pixel in order
+                    col = f3{0, 0, 0};
+                    for (uint32_t j = 0; j < ns; j++) col = fold_sample(col, path(x, y, j), j, 0u, d->max_luminance);
+                    col = final_pixel(col, ns, 0u, d->max_luminance);
+                } else {  // draw2(): sample s of the pixel into its running average
+                    col = fold_sample(f3{o[0], o[1], o[2]}, path(x, y, s), s, 1u, d->max_luminance);
+                }
                 o[0] = col.x;
                 o[1] = col.y;
                 o[2] = col.z;
                 o[3] = 0.0f;
             }
-        c->done.fetch_add((uint64_t)(t.xmax - t.xmin) * (t.ymax - t.ymin) * ns, std::memory_order_relaxed);
-        c->tiles_done.fetch_add(1, std::memory_order_release);
+        {
+            std::lock_guard<std::mutex> lk(c->fb_mu);
+            for (uint32_t y = t.ymin; y < t.ymax; y++)
+                memcpy(c->fb.data() + ((size_t)t.xmin + (size_t)y * W) * 4, tb.data() + (size_t)(y - t.ymin) * tw * 4, (size_t)tw * 16);
+            if (d->mode == 1) c->pass_items[s]++;
+        }
+        c->done.fetch_add((uint64_t)tw * th * (d->mode == 0 ? ns : 1u), std::memory_order_relaxed);
+        if (d->mode == 0) c->tiles_done.fetch_add(1, std::memory_order_release);
     }
     rays_total.fetch_add(my_rays, std::memory_order_relaxed);
+}
+
+mrt_status mrt_cpu_set_worker_seeds(mrt_cpu_scene* c, uint32_t n, const uint64_t* initstate, const uint64_t* initseq) {
+    if (!c || (n && (!initstate || !initseq))) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_set_worker_seeds: null");
+    std::lock_guard<std::mutex> lk(c->fb_mu);
+    c->seed_state.assign(initstate, initstate + n);
+    c->seed_seq.assign(initseq, initseq + n);
+    return MRT_OK;
 }
 
 mrt_status mrt_cpu_render(mrt_cpu_scene* c, const mrt_render_desc* d, float* rgb_out, uint64_t* rays_out, const volatile int* cancel) {
@@ -194,6 +306,13 @@ mrt_status mrt_cpu_render(mrt_cpu_scene* c, const mrt_render_desc* d, float* rgb
     if (d->flags & MRT_RF_FAST)
         return mrt_internal_fail(MRT_ERR_INVALID, "the CPU backend implements the exact numerics contract only");
     if (d->flags & MRT_RF_PATH_DEBUG) return mrt_internal_fail(MRT_ERR_INVALID, "MRT_RF_PATH_DEBUG is a GPU-backend render flag");
+    const bool ref_order = (d->flags & MRT_RF_REF_ORDER) != 0;
+    if (ref_order) {
+        if (d->world > 1) return mrt_internal_fail(MRT_ERR_INVALID, "MRT_RF_REF_ORDER renders the whole image (the reference has no ranks)");
+        if (c->seed_state.empty()) return mrt_internal_fail(MRT_ERR_INVALID, "MRT_RF_REF_ORDER needs mrt_set_worker_seeds first");
+        if (d->threads && d->threads != c->seed_state.size())
+            return mrt_internal_fail(MRT_ERR_INVALID, "MRT_RF_REF_ORDER: desc.threads must equal the worker seeds given");
+    }
     const auto t0 = std::chrono::steady_clock::now();
     const uint32_t world = d->world ? d->world : 1u, ns = d->sqrt_samples * d->sqrt_samples;
     std::vector<mrt_tile> tiles;  // this rank's tiles, in work_queue order
@@ -214,19 +333,28 @@ mrt_status mrt_cpu_render(mrt_cpu_scene* c, const mrt_render_desc* d, float* rgb
         c->fb_h = d->height;
         c->fb_ns = ns;
         c->tiles_done.store(0, std::memory_order_relaxed);
+        c->n_tiles = (uint32_t)tiles.size();
+        c->ref_mode1 = ref_order && d->mode == 1;
+        c->pass_items.assign(c->ref_mode1 ? ns : 0u, 0u);
     }
-    uint32_t n = d->threads ? d->threads : std::max(1u, std::thread::hardware_concurrency());
-    n = (uint32_t)std::min<size_t>(n, std::max<size_t>(tiles.size(), 1));
+    uint32_t n = ref_order ? (uint32_t)c->seed_state.size() : d->threads ? d->threads : std::max(1u, std::thread::hardware_concurrency());
+    if (!ref_order) n = (uint32_t)std::min<size_t>(n, std::max<size_t>(tiles.size(), 1));
     std::atomic<uint32_t> next{0};
+    std::atomic<uint64_t> next_item{0};
     std::atomic<uint64_t> rays{0};
     std::atomic<bool> cancelled{false};
-    auto work = [&]() {
-        if (c->feats & FT_LIN) render_tiles<F_LIN>(c, d, tiles, next, rgb_out, rays, cancel, cancelled);
-        else render_tiles<F_GEN>(c, d, tiles, next, rgb_out, rays, cancel, cancelled);
+    auto work = [&](uint32_t wi) {
+        if (ref_order) {
+            if (c->feats & FT_LIN) render_ref_order<F_LIN>(c, d, tiles, wi, next_item, rays, cancel, cancelled);
+            else render_ref_order<F_GEN>(c, d, tiles, wi, next_item, rays, cancel, cancelled);
+        } else {
+            if (c->feats & FT_LIN) render_tiles<F_LIN>(c, d, tiles, next, rgb_out, rays, cancel, cancelled);
+            else render_tiles<F_GEN>(c, d, tiles, next, rgb_out, rays, cancel, cancelled);
+        }
     };
     std::vector<std::thread> pool;
-    for (uint32_t i = 1; i < n; i++) pool.emplace_back(work);
-    work();
+    for (uint32_t i = 1; i < n; i++) pool.emplace_back(work, i);
+    work(0u);
     for (std::thread& t : pool) t.join();
     for (uint32_t p : c->fb_px) memcpy(rgb_out + (size_t)p * 4, c->fb.data() + (size_t)p * 4, 16);
     c->last_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -248,15 +376,22 @@ mrt_status mrt_cpu_last_ms(mrt_cpu_scene* c, float* ms, uint32_t* threads) {
     return MRT_OK;
 }
 
-// draw()'s framebuffer as the UI thread sees it (main.cpp:387-444): every finished tile's pixels
-// with all their samples, the others still black.  A pixel is written once, after its last sample,
-// as the reference's workers write G_linearBackBuffer.
+// The framebuffer as the UI thread sees it (main.cpp:387-444), copied under the lock the workers
+// publish finished work items with (never a half-written tile).  draw() (mode 0, and every
+// stream-keyed render): finished tiles with all their samples, the others black; samples_done = spp
+// once every tile is in, 0 before.  draw2() in the reference's order (MRT_RF_REF_ORDER, mode 1):
+// the running averages; samples_done = the leading sample passes every tile has published.
 mrt_status mrt_cpu_preview(mrt_cpu_scene* c, float* rgb_out, uint32_t* samples_done) {
     std::lock_guard<std::mutex> lk(c->fb_mu);
     *samples_done = 0;
     if (c->fb.empty()) return MRT_OK;
-    const uint32_t done = c->tiles_done.load(std::memory_order_acquire);
     for (uint32_t p : c->fb_px) memcpy(rgb_out + (size_t)p * 4, c->fb.data() + (size_t)p * 4, 16);
-    *samples_done = done ? c->fb_ns : 0u;
+    if (c->ref_mode1) {
+        uint32_t s = 0;
+        while (s < c->pass_items.size() && c->pass_items[s] == c->n_tiles) s++;
+        *samples_done = s;
+    } else {
+        *samples_done = c->tiles_done.load(std::memory_order_acquire) == c->n_tiles ? c->fb_ns : 0u;
+    }
     return MRT_OK;
 }

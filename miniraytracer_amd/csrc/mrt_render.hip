@@ -56,8 +56,13 @@ __global__ void __launch_bounds__(256) mrt_fold_kernel(const float* __restrict__
                                                       uint32_t s1, uint32_t mode, float max_lum) {
     uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
     if (lp >= npix) return;
-    float4 a = acc[lp];
-    f3 c{a.x, a.y, a.z};
+    // a render's first chunk starts from +0 without reading acc (no per-render clearing fill:
+    // folding +0 first gives the same bits as starting from a zeroed accumulator)
+    f3 c{0.0f, 0.0f, 0.0f};
+    if (s0 != 0) {
+        const float4 a = acc[lp];
+        c = f3{a.x, a.y, a.z};
+    }
     const float* q = rad + (size_t)lp * 3;
     const size_t stride = (size_t)npix * 3;
     uint32_t s = s0;
@@ -90,27 +95,40 @@ __global__ void __launch_bounds__(256) mrt_fold_kernel(const float* __restrict__
 #define MRT_FOLD_LEAN_WG 64  // one-wave groups take any single free wave slot (C2 step 8.44 -> 8.38 ms vs 256)
 #endif
 __global__ void __launch_bounds__(MRT_FOLD_LEAN_WG) __attribute__((amdgpu_num_vgpr(8)))
-mrt_fold_lean_kernel(const float* __restrict__ rad, float4* __restrict__ acc, uint32_t npix, uint32_t n) {
+mrt_fold_lean_kernel(const float* __restrict__ rad, float4* __restrict__ acc, uint32_t npix, uint32_t n, uint32_t first) {
     const uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
     if (lp >= npix) return;
     const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rad), 0, 0xFFFFFFFFu, 0x00020000);
     const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(acc, 0, 0xFFFFFFFFu, 0x00020000);
-    const auto a = __builtin_amdgcn_raw_buffer_load_b96(ra, lp * 16u, 0, 0);
-    f3 c{__uint_as_float(a[0]), __uint_as_float(a[1]), __uint_as_float(a[2])};
+    f3 c{0.0f, 0.0f, 0.0f};  // the render's first chunk: from +0 (as mrt_fold_kernel)
+    if (!first) {
+        const auto a = __builtin_amdgcn_raw_buffer_load_b96(ra, lp * 16u, 0, 0);
+        c = f3{__uint_as_float(a[0]), __uint_as_float(a[1]), __uint_as_float(a[2])};
+    }
     const uint32_t stride = npix * 12u;
     uint32_t off = lp * 12u;
     for (uint32_t s = 0; s < n; s++, off += stride) {
         const auto v = __builtin_amdgcn_raw_buffer_load_b96(rr, off, 0, 2 /* nt */);
         c = fold_sample(c, f3{__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2])}, s, 0u, 0.0f);
     }
-    using u3 = decltype(a);
+    using u3 = decltype(__builtin_amdgcn_raw_buffer_load_b96(ra, 0u, 0, 0));
     const u3 o = {__float_as_uint(c.x), __float_as_uint(c.y), __float_as_uint(c.z)};
     __builtin_amdgcn_raw_buffer_store_b96(o, ra, lp * 16u, 0, 0);
 }
 
+// Also resets what the render's path kernels consumed, for the context's next render, in stream
+// order after them: the work counters of its launches (word (k * MRT_NPART + part) *
+// MRT_COUNTER_STRIDE) and their progress snapshots in host memory -- instead of clearing fills
+// enqueued before each render (a blit kernel needs a free wave slot, which the persistent path
+// kernels of the other pipelined contexts hold: up to 49 ms waits in the bench trace).
 __global__ void __launch_bounds__(256) mrt_final_kernel(const float4* __restrict__ acc, float4* __restrict__ out, uint32_t npix, uint32_t ns,
-                                                       uint32_t mode, float max_lum) {
+                                                       uint32_t mode, float max_lum, unsigned long long* __restrict__ counters,
+                                                       unsigned long long* hprog, uint32_t nreset) {
     uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
+    if (lp < nreset) {
+        counters[(size_t)lp * MRT_COUNTER_STRIDE] = 0ull;
+        if (hprog) __hip_atomic_store(hprog + lp, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     if (lp >= npix) return;
     float4 a = acc[lp];
     const f3 c = final_pixel(f3{a.x, a.y, a.z}, ns, mode, max_lum);
@@ -788,6 +806,7 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     if ((st = dev_alloc(s, &p, 64))) { mrt_scene_free(s); return st; }
     s->d_counter = (uint64_t*)p;
     s->d_rays = (unsigned long long*)((char*)p + 16);
+    HIPCHK(hipMemset(p, 0, 64));  // the cancel flag (d_counter + 4) starts clear
     // kernel variant + LDS stacks sized from the scene graph (top frame lives in registers)
     s->features = T.features;
     s->variant = pick_variant(s->features);
@@ -978,7 +997,12 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
     if ((st = grow(s, (void**)&s->d_lev, &s->lev_cap, (size_t)s->lev_rows * s->max_threads * 16))) return st;
     uint32_t launches = (ns + s->chunk - 1) / s->chunk;
     const size_t cnt_words = (size_t)MRT_NPART * MRT_COUNTER_STRIDE;  // per launch
-    if ((st = grow(s, (void**)&s->d_counters, &s->cnt_cap, (size_t)launches * cnt_words * 8))) return st;
+    {
+        void* const before = s->d_counters;
+        if ((st = grow(s, (void**)&s->d_counters, &s->cnt_cap, (size_t)launches * cnt_words * 8))) return st;
+        // zeroed once at allocation; afterwards every render's final kernel leaves them zero
+        if (s->d_counters != before) HIPCHK(hipMemset(s->d_counters, 0, s->cnt_cap));
+    }
     if (!s->pstream) HIPCHK(hipStreamCreateWithFlags(&s->pstream, hipStreamNonBlocking));
     if (!s->ev_done) HIPCHK(hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming));
     {
@@ -989,6 +1013,7 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
             s->h_prog = nullptr;
             s->h_prog_cap = 0;
             HIPCHK(hipHostMalloc((void**)&s->h_prog, (size_t)launches * MRT_NPART * 8, hipHostMallocPortable | hipHostMallocCoherent));
+            memset(s->h_prog, 0, (size_t)launches * MRT_NPART * 8);  // later: reset by each render's final kernel
             s->h_prog_cap = launches;
         }
         if (s->h_seen.size() < (size_t)launches * MRT_NPART) s->h_seen.resize((size_t)launches * MRT_NPART, 0);
@@ -1017,18 +1042,18 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
     const PathLaunch& PL = s->pl[(d->flags & MRT_RF_FAST) ? 1 : 0];
     hipStream_t q = (hipStream_t)stream;
     uint32_t ns = d->sqrt_samples * d->sqrt_samples;
-    HIPCHK(hipMemsetAsync(s->d_acc, 0, (size_t)s->npix * 16, q));
+    // No clearing fills enqueued here: the first fold chunk starts from +0 instead of reading the
+    // accumulator, and the work counters and progress snapshots were left zero by the previous
+    // render's final kernel (stream order; zeroed at allocation before the first).  The cancel flag
+    // is clear unless a cancelled mrt_render set it, and that clears it again before returning.
     const uint32_t launches = (ns + s->chunk - 1) / s->chunk;
-    HIPCHK(hipMemsetAsync(s->d_counters, 0, (size_t)launches * MRT_NPART * MRT_COUNTER_STRIDE * 8, q));
-    HIPCHK(hipMemsetAsync(s->d_counter + 4, 0, 8, q));  // cancel flag
     {
         std::lock_guard<std::mutex> lk(s->prog_mu);
         for (uint32_t k = 0; k < launches; k++) {
             s->chunk_paths[k] = (uint64_t)s->npix * (std::min(ns, (k + 1) * s->chunk) - k * s->chunk);
-            for (uint32_t j = 0; j < MRT_NPART; j++) {
-                __atomic_store_n(&s->h_prog[(size_t)k * MRT_NPART + j], (uint64_t)0, __ATOMIC_RELAXED);
-                s->h_seen[(size_t)k * MRT_NPART + j] = 0;
-            }
+            // the host's running maxima only: a snapshot is read only once this render's launch k
+            // has started (its start event), i.e. after the previous render's final kernel reset it
+            for (uint32_t j = 0; j < MRT_NPART; j++) s->h_seen[(size_t)k * MRT_NPART + j] = 0;
         }
     }
     s->n_launch = 0;
@@ -1092,12 +1117,13 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         uint32_t blocks = (s->npix + 255) / 256;
         if ((d->flags & MRT_RF_FOLD_BEHIND) && d->mode == 0)
             hipLaunchKernelGGL(mrt_fold_lean_kernel, dim3((s->npix + MRT_FOLD_LEAN_WG - 1) / MRT_FOLD_LEAN_WG), dim3(MRT_FOLD_LEAN_WG), 0, q,
-                               s->d_rad, s->d_acc, s->npix, s1 - s0);
+                               s->d_rad, s->d_acc, s->npix, s1 - s0, (uint32_t)(s0 == 0));
         else
             hipLaunchKernelGGL(mrt_fold_kernel, dim3(blocks), dim3(256), 0, q, s->d_rad, s->d_acc, s->npix, s0, s1, d->mode, d->max_luminance);
         HIPCHK(hipGetLastError());
         if (preview) {  // the image after s1 samples, copied under the sequence lock
-            hipLaunchKernelGGL(mrt_final_kernel, dim3(blocks), dim3(256), 0, q, s->d_acc, s->d_prev, s->npix, s1, d->mode, d->max_luminance);
+            hipLaunchKernelGGL(mrt_final_kernel, dim3(blocks), dim3(256), 0, q, s->d_acc, s->d_prev, s->npix, s1, d->mode, d->max_luminance,
+                               (unsigned long long*)nullptr, (unsigned long long*)nullptr, 0u);
             HIPCHK(hipGetLastError());
             HIPCHK(hipStreamWriteValue32(q, s->h_seq, 2 * seq + 1, 0));
             HIPCHK(hipMemcpyAsync(s->h_prev, s->d_prev, (size_t)s->npix * 16, hipMemcpyDeviceToHost, q));
@@ -1107,8 +1133,10 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         }
         s->last_paths = P.n_paths;
     }
-    uint32_t blocks = (s->npix + 255) / 256;
-    hipLaunchKernelGGL(mrt_final_kernel, dim3(blocks), dim3(256), 0, q, s->d_acc, (float4*)d_local, s->npix, ns, d->mode, d->max_luminance);
+    const uint32_t nreset = launches * MRT_NPART;
+    const uint32_t blocks = (std::max(s->npix, nreset) + 255) / 256;
+    hipLaunchKernelGGL(mrt_final_kernel, dim3(blocks), dim3(256), 0, q, s->d_acc, (float4*)d_local, s->npix, ns, d->mode, d->max_luminance,
+                       (unsigned long long*)s->d_counters, (unsigned long long*)s->h_prog, nreset);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(s->ev_done, q));
     s->ev_done_pending = true;
@@ -1119,6 +1147,8 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
 extern "C" mrt_status mrt_render(mrt_scene* s, const mrt_render_desc* d, float* rgb_out, uint64_t* rays_out, const volatile int* cancel) {
     if (!s || !d || !rgb_out) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_render: null");
     if (s->cpu) return mrt_cpu_render(s->cpu, d, rgb_out, rays_out, cancel);
+    if (d->flags & MRT_RF_REF_ORDER)
+        return mrt_internal_fail(MRT_ERR_INVALID, "MRT_RF_REF_ORDER is a CPU-backend mode (the GPU keys its PCG streams per path)");
     s->n_chunks.store(0, std::memory_order_release);
     if (cancel && *cancel) return mrt_internal_fail(MRT_ERR_CANCELLED, "cancelled");
     mrt_render_desc dc = *d;  // a cancellable render runs as >= 16 launches; cancel lands between them
@@ -1149,6 +1179,7 @@ extern "C" mrt_status mrt_render(mrt_scene* s, const mrt_render_desc* d, float* 
         }
     }
     s->ev_done_pending = false;
+    if (cancelled) HIPCHK(hipMemset(s->d_counter + 4, 0, 8));  // the render is over: clear the flag for the next one
     std::vector<float> local((size_t)s->npix * 4);
     std::vector<uint32_t> px = mrt_internal_local_pixels(d);
     HIPCHK(hipMemcpy(local.data(), s->d_out, local.size() * 4, hipMemcpyDeviceToHost));
@@ -1227,6 +1258,14 @@ extern "C" mrt_status mrt_preview(mrt_scene* s, float* rgb_out, uint32_t* sample
         return MRT_OK;
     }
     return MRT_OK;  // the render outran every attempt: report nothing rather than a torn image
+}
+
+extern "C" mrt_status mrt_set_worker_seeds(mrt_scene* s, uint32_t n_threads, const uint64_t* initstate, const uint64_t* initseq) {
+    if (!s) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_set_worker_seeds: null");
+    if (!s->cpu)
+        return mrt_internal_fail(MRT_ERR_INVALID, "mrt_set_worker_seeds: the reference's per-thread RNG order is a CPU-backend mode "
+                                                  "(the GPU keys its PCG streams per path)");
+    return mrt_cpu_set_worker_seeds(s->cpu, n_threads, initstate, initseq);
 }
 
 extern "C" mrt_status mrt_scene_kernel_info(const mrt_scene* s, mrt_kernel_info* out) {

@@ -90,10 +90,11 @@ def test_cpu_backend_progress_cancel_and_gpu_only_calls(mrt):
 
 
 def test_cli_cpu_backend_writes_reference_image(mrt, tmp_path):
-    """bin/mrt -backend cpu: the reference's flags (-threads = CPU workers), image == fixture."""
+    """bin/mrt -backend cpu -order path: the reference's flags (-threads = CPU workers), per-path
+    stream keys (the GPU's), image == the stream-matched fixture."""
     g = golden_stream("stream_5.npz")
     out = tmp_path / "x.pfm"
-    p = subprocess.run([os.path.join(ROOT, "bin", "mrt"), "-backend", "cpu", "-threads", "3", "-scene", "5", "-width", str(g["w"]),
+    p = subprocess.run([os.path.join(ROOT, "bin", "mrt"), "-backend", "cpu", "-order", "path", "-threads", "3", "-scene", "5", "-width", str(g["w"]),
                         "-height", str(g["h"]), "-samples", str(g["spp"]), "-depth", str(g["depth"]), "-mode", str(g["mode"]),
                         "-tilesize", "8", "-o", str(out)], capture_output=True, text=True, timeout=120, check=True)
     assert "CPU, 3 threads" in p.stdout
@@ -136,3 +137,83 @@ def test_walk_shape_recognised_on_upload(mrt, sid, shape):
     sc = mrt.select_scene(sid, 1.0)
     r = mrt.Renderer(sc, "cpu")
     assert (r.kernel_info()["features"] >> 16) & 0xFF == shape
+
+
+REFSEQ = [(s, md) for s in (0, 5, 7, 8) for md in (0, 1)]
+
+
+def _refseq(sid, mode):
+    g = np.load(os.path.join(ROOT, "tests", "golden", f"refseq_{sid}_m{mode}.npz"))
+    _, w, h, spp, depth, ts, md, rays = (int(x) for x in g["meta"])
+    return g["image"], w, h, spp, depth, ts, rays
+
+
+@pytest.mark.parametrize("sid,mode", REFSEQ)
+def test_cpu_backend_reproduces_reference_threads1_run(mrt, sid, mode):
+    """The reference's OWN deterministic mode (cmdline_parser.h:15: "use mode=0 and threads=1 for a
+    deterministic runtime test") in the product: the CPU backend with MRT_RF_REF_ORDER and one worker
+    seeded as main() seeds it (main.cpp:357-366, mrt_set_worker_seeds) -- tiles in work_queue order,
+    pixel -> sample (draw, mode 0) or (tile, sample) items (draw2, mode 1) -- equals the exact
+    reference build's -threads 1 run (refseq_<sid>_m<mode>.npz): G_linearBackBuffer and G_rayCounter."""
+    ref, w, h, spp, depth, ts, rays = _refseq(sid, mode)
+    sc = mrt.select_scene(sid, w / h)
+    r = mrt.Renderer(sc, "cpu")
+    r.set_worker_seeds(sc.worker_seeds(1))
+    img, nr = r.render(mrt.render_desc(w, h, spp, depth=depth, mode=mode, tile_size=ts, threads=1, ref_order=True))
+    assert nr == rays
+    assert np.array_equal(img[..., :3].view(np.uint32), ref.view(np.uint32))
+    final, n = r.preview(w, h)
+    assert np.array_equal(final, img) and n == int(np.sqrt(np.float32(spp))) ** 2
+
+
+@pytest.mark.parametrize("sid,mode", [(5, 0), (5, 1), (7, 1), (8, 0)])
+def test_cli_cpu_backend_reproduces_reference_deterministic_run(mrt, tmp_path, sid, mode):
+    """bin/mrt -backend cpu -threads 1 -mode 0|1 (the reference's RNG order is the CPU backend's
+    default): the same image and ray count as the reference's own -threads 1 run."""
+    ref, w, h, spp, depth, ts, rays = _refseq(sid, mode)
+    out = tmp_path / "r.pfm"
+    p = subprocess.run([os.path.join(ROOT, "bin", "mrt"), "-backend", "cpu", "-threads", "1", "-mode", str(mode), "-scene", str(sid),
+                        "-width", str(w), "-height", str(h), "-samples", str(spp), "-depth", str(depth), "-tilesize", str(ts),
+                        "-o", str(out)], capture_output=True, text=True, timeout=300, check=True)
+    assert int(p.stdout.split("rays ")[-1].split()[0]) == rays
+    assert np.array_equal(mrt.read_pfm(str(out)).view(np.uint32), ref.view(np.uint32))
+
+
+def test_ref_order_guards(mrt):
+    """MRT_RF_REF_ORDER needs worker seeds and one rank; the GPU backend refuses it."""
+    sc = mrt.select_scene(5, 1.0)
+    r = mrt.Renderer(sc, "cpu")
+    d = mrt.render_desc(16, 16, 4, ref_order=True, threads=1)
+    with pytest.raises(mrt.MrtError, match="worker_seeds"):
+        r.render(d)
+    r.set_worker_seeds(sc.worker_seeds(2))
+    with pytest.raises(mrt.MrtError, match="threads"):
+        r.render(d)
+    with pytest.raises(mrt.MrtError, match="ranks"):
+        r.render(mrt.render_desc(16, 16, 4, ref_order=True, world=2, rank=1))
+    img, rays = r.render(mrt.render_desc(16, 16, 4, ref_order=True))  # threads 0: one per seed pair
+    assert rays > 0
+
+
+def test_ref_order_mode1_preview_counts_whole_passes(mrt):
+    """draw2() in the reference's order, previewed while it runs: samples_done counts the sample
+    passes every tile has published; after the render the preview is the image."""
+    sc = mrt.select_scene(5, 1.0)
+    r = mrt.Renderer(sc, "cpu")
+    r.set_worker_seeds(sc.worker_seeds(2))
+    d = mrt.render_desc(64, 64, 64, mode=1, tile_size=16, ref_order=True)
+    seen = []
+    done = threading.Event()
+
+    def poll():
+        while not done.is_set():
+            seen.append(r.preview(64, 64)[1])
+
+    t = threading.Thread(target=poll)
+    t.start()
+    img, _ = r.render(d)
+    done.set()
+    t.join()
+    final, n = r.preview(64, 64)
+    assert n == 64 and np.array_equal(final, img)
+    assert all(0 <= k <= 64 for k in seen) and seen == sorted(seen)

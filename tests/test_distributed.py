@@ -1,7 +1,10 @@
-"""World-size-2 gloo test of the multi-GPU path on CPU: tile ownership (tile k -> rank k % world),
-padded gather to rank 0 and scatter into the framebuffer reproduce the single-process image bit
-for bit.  The per-rank pixels are rendered by the C restatement (CPU stand-in for the GPU), so
-this covers the distribution logic of bench.py / miniraytracer_amd.dist without a GPU."""
+"""World-size-2/3 gloo test of the multi-GPU path on CPU: tile ownership (tile k -> rank k % world),
+each rank rendering ONLY its own tiles through the product's render path (the CPU backend behind the
+same C-ABI: mrt_render with rank / world in the desc, the hot-path code compiled for the host),
+padded gather to rank 0 and scatter into the framebuffer.  The assembled image must equal a
+one-rank render and the reference fixture (tests/golden/stream_5.npz) bit for bit, and the ray
+totals summed over ranks the reference's G_rayCounter.  Covers the distribution logic of bench.py /
+miniraytracer_amd.dist without a GPU; no oracle involved."""
 import os
 import socket
 
@@ -11,9 +14,11 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from conftest import ROOT
+from conftest import ROOT, golden_stream
 
-W, H, SPP = 50, 30, 4
+G = golden_stream("stream_5.npz")
+W, H, SPP, DEPTH = G["w"], G["h"], G["spp"], G["depth"]
+TILE = 8
 
 
 def _free_port():
@@ -30,12 +35,15 @@ def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import miniraytracer_amd as m
-    import oracle
     from miniraytracer_amd.dist import TileGather
     sc = m.select_scene(5, W / H)
-    img, rays, _, _ = oracle.render(sc, oracle.desc(W, H, SPP, threads=2))
-    tg = TileGather(W, H, SPP, 32, world, rank, torch.device("cpu"), tile_size=16)
-    local = torch.from_numpy(img.reshape(-1, 4)[tg.px[rank]].copy())
+    r = m.Renderer(sc, "cpu")
+    d = m.render_desc(W, H, SPP, depth=DEPTH, tile_size=TILE, rank=rank, world=world, threads=2)
+    img, rays = r.render(d)  # this rank's tiles only
+    px = m.local_pixels(d)
+    tg = TileGather(W, H, SPP, DEPTH, world, rank, torch.device("cpu"), tile_size=TILE)
+    assert np.array_equal(px, tg.px[rank])
+    local = torch.from_numpy(img.reshape(-1, 4)[px].copy())
     full = tg.gather(local)
     full = full.clone() if full is not None else None
     # overlapped form used by bench.py: start() copies the shard, finish() scatters on rank 0
@@ -43,10 +51,11 @@ def _worker(rank, world, port, q):
     full2 = tg.finish(h)
     if rank == 0:
         assert torch.equal(full, full2)
-    total = torch.tensor([len(tg.px[rank])], dtype=torch.int64)
-    dist.all_reduce(total)
+    total = torch.tensor([rays], dtype=torch.int64)
+    dist.all_reduce(total)  # the ray count's one all_reduce
     if rank == 0:
-        q.put((full.numpy().copy(), img, int(total.item())))
+        one, one_rays = r.render(m.render_desc(W, H, SPP, depth=DEPTH, tile_size=TILE, threads=2))
+        q.put((full.numpy().copy(), one, one_rays, int(total.item())))
     dist.destroy_process_group()
 
 
@@ -58,9 +67,10 @@ def test_gloo_tile_gather_reassembles_image(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    full, ref, total = q.get(timeout=300)
+    full, one, one_rays, total = q.get(timeout=300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    assert total == W * H
-    assert np.array_equal(full.view(np.uint32), ref.view(np.uint32))
+    assert total == one_rays == G["rays"]
+    assert np.array_equal(full.view(np.uint32), one.view(np.uint32))
+    assert np.array_equal(full[..., :3].view(np.uint32), G["image"].view(np.uint32))

@@ -334,6 +334,35 @@ def test_full_c2_within_tolerance_of_shipped_reference(gpu, numerics):
     assert abs(rays / float(g["rays"][0]) - 1) < 1e-4
 
 
+# Full-resolution fixtures of C3 / C4 / C5 (tools/make_golden.py FULLRES: the reference as shipped,
+# stream-matched, 1024 spp at the configs' own resolution).  Per-pixel RMSE over a band of rows and
+# a seeded sample of pixels (tests/fixture_cmp.py), 32x32-grid block means, channel means, rays.
+# Bars: per-pixel RMSE < 1e-3 (the north-star bar, at 1024 spp as for C2) -- except where stated;
+# measured values in profiles/r03_parity.json (tools/parity_record.py).
+FULL_RMSE = {(9, "exact"): 1e-3, (9, "fast"): 1e-3, (8, "exact"): 1e-3, (8, "fast"): 1e-3,
+             (7, "exact"): 1e-3, (7, "fast"): 1e-3}
+FULL_RAYS = {"exact": 1e-3, "fast": 5e-3}
+
+
+@pytest.mark.parametrize("numerics", ["exact", "fast"])
+@pytest.mark.parametrize("sid", [9, 8, 7])
+def test_full_resolution_within_tolerance_of_shipped_reference(gpu, sid, numerics):
+    """C3 (teapot in the Cornell room, 800x800), C4 (bunny, 1024x1024), C5 (book2, 2048x2048) at full
+    resolution, 1024 spp, against the reference as shipped on the same per-path streams."""
+    from fixture_cmp import GOLDEN, compare
+    path = os.path.join(GOLDEN, f"shipped_full_{sid}.npz")
+    g = np.load(path)
+    _, w, h, spp, depth = (int(x) for x in g["meta"])
+    _, r = renderer(gpu, sid, w, h)
+    img, rays = r.render(gpu.render_desc(w, h, spp, depth=depth, numerics=numerics))
+    c = compare(img, rays, path)
+    print(c)
+    assert c["rmse"] < FULL_RMSE[(sid, numerics)], c
+    assert c["block_rmse"] < 1e-4, c
+    assert c["mean_delta"] < 1e-4, c
+    assert abs(c["ray_ratio"] - 1) < FULL_RAYS[numerics], c
+
+
 def test_concurrent_contexts_on_two_streams(gpu):
     """bench.py --pipeline: render contexts of the same scene on two HIP streams, launched back to
     back without ordering, share one device ray counter (atomics) and overlap on the CUs; each

@@ -1,8 +1,10 @@
 """Host-side surface (CPU only): the C-ABI library loads and exports every declared symbol, the
 reference's flags parse the same way, work_queue tile order, per-rank ownership, tone map."""
 import ctypes
+import json
 import os
 import re
+import types
 
 import numpy as np
 
@@ -64,11 +66,23 @@ def test_default_render_desc_carries_numerics(mrt):
         assert (d.sqrt_samples, d.flags & mrt._lib.RF_FAST) == (4, flag)
 
 
+def test_order_flag_defaults(mrt):
+    """-order: the reference's RNG order is the CPU backend's default (its -threads 1 run is then
+    reproducible), per-path keys the GPU's; -order path / ref override; the desc carries it."""
+    cases = [(["-backend", "cpu"], 1), ([], 0), (["-backend", "cpu", "-order", "path"], 0), (["-order", "ref"], 1)]
+    for args, order in cases:
+        p = mrt.ParseArgv(["mrt"] + args)
+        assert p.order == order, args
+        d = mrt._lib.MrtRenderDesc()
+        mrt.lib().mrt_default_render_desc(ctypes.byref(p), ctypes.byref(d))
+        assert bool(d.flags & mrt._lib.RF_REF_ORDER) == bool(order)
+
+
 def test_render_flags_match_header(mrt):
     """The ctypes mirror's MRT_RF_* bits are the header's (include/mrt.h)."""
     hdr = open(os.path.join(os.path.dirname(__file__), "..", "include", "mrt.h")).read()
     bits = {m.group(1): int(m.group(2), 16) for m in re.finditer(r"#define MRT_RF_(\w+) (0x[0-9a-fA-F]+)u", hdr)}
-    assert set(bits) == {"PATH_DEBUG", "FAST", "PREVIEW", "FOLD_BEHIND"}
+    assert set(bits) == {"PATH_DEBUG", "FAST", "PREVIEW", "FOLD_BEHIND", "REF_ORDER"}
     for name, v in bits.items():
         assert getattr(mrt._lib, "RF_" + name) == v, name
 
@@ -180,3 +194,27 @@ def test_packed_mesh_equals_obj_parse(mrt, tmp_path):
     out = tmp_path / "bunny.mesh"
     assert mrt.lib().mrt_pack_obj(obj.encode(), str(out).encode()) == 0
     assert out.read_bytes() == open(os.path.join(ROOT, "assets", "bunny.mesh"), "rb").read()
+
+
+def test_bench_roofline_prices_pmc_per_ray(tmp_path):
+    """bench.py's roofline: VALU issue rate of the launch from the committed per-ray PMC figures and
+    the live kernel time, frac against 1024 SIMDs x 2.4 GHz / 2; a rank's share priced by its own
+    rays (world > 1); a PMC file of another workload is not used."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    pmc = tmp_path / "p.json"
+    pmc.write_text(json.dumps({"config": [5, 500, 500, 1024, 32], "source": "x",
+                               "by_numerics": {"fast": {"valu_insts_per_ray": 9.0, "hbm_bytes_per_ray": 7.0, "valu_lane_util": 0.6,
+                                                        "valu_busy": 0.7}}}))
+    args = types.SimpleNamespace(scene=5, width=500, height=500, depth=32, pmc_json=str(pmc))
+    ki = dict(grid=1, wg=64, lds_bytes=0, vgprs=72, tree_nodes=0)
+    r = bench.roofline(args, 8.0, 778e6, "fast", ki)
+    assert r["bound"] == "valu" and r["peak"] == pytest.approx(1228.8)
+    assert r["achieved"] == pytest.approx(9.0 * 778e6 / 8e-3 / 1e9, rel=1e-3)
+    assert 0 < r["frac"] <= 1 and r["traffic"] == round(7.0 * 778e6)
+    half = bench.roofline(args, 4.0, 389e6, "fast", ki)  # a rank's half: same rates
+    assert half["frac"] == pytest.approx(r["frac"], rel=1e-3) and half["hbm_frac"] == pytest.approx(r["hbm_frac"], rel=1e-3)
+    args.width = 640
+    assert bench.roofline(args, 8.0, 778e6, "fast", ki)["frac"] is None

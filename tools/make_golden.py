@@ -17,6 +17,9 @@ Fixtures (all small; data only -- inputs and expected outputs):
                           block means, channel means, ray count; and whole small images of scenes 5, 8, 9, 7
                           (SHIPPED_SMALL).
                           `--only-shipped-stream` regenerates just these two.
+  shipped_full_<id>.npz   the same at the full resolution of C3 / C4 / C5 (1024 spp): block means,
+                          channel means, a band of rows, a seeded pixel sample, ray total
+                          (`--only-fullres`; FULLRES)
   refseq_<id>_m<mode>.npz the exact reference build with -threads 1 (its own deterministic mode:
                           one worker PCG stream, work_queue tile order), image + G_rayCounter
                           (`--only-refseq`)
@@ -95,6 +98,41 @@ def shipped_stream(tmp):
         print("shipped stream small", sid, meta)
 
 
+# full-resolution tolerance fixtures of the BASELINE configs beyond C2 (C3 teapot-in-Cornell 800^2,
+# C4 bunny 1024^2, C5 book2 2048^2) at reduced spp: the reference AS SHIPPED, stream-matched.  The
+# whole float image is too large to commit (C5: 50 MB), so each keeps the size-independent parts:
+# a 32x32 grid of block means, the channel means, a band of full rows, a seeded random sample of
+# pixels (per-pixel RMSE estimated over band + sample), and the ray total.
+FULLRES = [(9, 800, 800, 1024), (8, 1024, 1024, 1024), (7, 2048, 2048, 1024)]
+FULLRES_SAMPLE = 49152  # random pixels kept per config (seeded, numpy PCG64)
+FULLRES_BAND = 16       # full rows kept, starting at H/2
+
+
+def fullres_reduce(im, sid, w, h, spp, rays):
+    """The committed parts of a full-resolution image (also used by the GPU test on its own image)."""
+    g = 32
+    bh, bw = h // g, w // g
+    rng = np.random.default_rng(1000 + sid)
+    idx = np.sort(rng.choice(w * h, size=FULLRES_SAMPLE, replace=False)).astype(np.int64)
+    r0 = h // 2
+    return dict(block_mean=im[:bh * g, :bw * g].reshape(g, bh, g, bw, 3).mean(axis=(1, 3), dtype=np.float64),
+                mean=im.reshape(-1, 3).mean(axis=0, dtype=np.float64), band=im[r0:r0 + FULLRES_BAND].copy(),
+                band_rows=np.array([r0, r0 + FULLRES_BAND]), sample_idx=idx, sample=im.reshape(-1, 3)[idx].copy(),
+                rays=np.array([rays], dtype=np.int64), meta=np.array([sid, w, h, spp, 32], dtype=np.int64))
+
+
+def fullres(tmp, only=None, threads=8):
+    img = os.path.join(tmp, "fr.pfm")
+    for sid, w, h, spp in FULLRES:
+        if only is not None and sid not in only:
+            continue
+        meta = json.loads(run(SHIPPED, ["--h-mode", "stream", "-width", w, "-height", h, "-samples", spp, "-depth", 32,
+                                        "--h-threads", threads, "--h-out", img] + scene_args(sid)))
+        np.savez_compressed(os.path.join(OUT, f"shipped_full_{sid}.npz"),
+                            **fullres_reduce(read_pfm(img, w, h), sid, w, h, spp, meta["rays"]))
+        print("shipped full", sid, w, h, spp, meta, flush=True)
+
+
 # the reference's own deterministic mode: -threads 1, one worker stream, work_queue tile order
 # (scene id, width, height, samples, depth, tile size); both -mode 0 (draw) and -mode 1 (draw2)
 REFSEQ_CASES = [(0, 60, 30, 16, 8, 16), (5, 48, 40, 16, 32, 16), (7, 40, 40, 4, 32, 16), (8, 40, 40, 9, 32, 16)]
@@ -117,6 +155,11 @@ def main():
     if "--only-refseq" in sys.argv:
         with tempfile.TemporaryDirectory() as tmp:
             refseq(tmp)
+        return
+    if "--only-fullres" in sys.argv:
+        only = [int(a) for a in os.environ.get("MRT_FULLRES_SCENES", "").split(",") if a]
+        with tempfile.TemporaryDirectory() as tmp:
+            fullres(tmp, only or None, int(os.environ.get("MRT_FULLRES_THREADS", "8")))
         return
     if "--only-shipped-stream" in sys.argv:
         with tempfile.TemporaryDirectory() as tmp:

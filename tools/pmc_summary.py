@@ -4,8 +4,9 @@
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
   profiles/<tag>_pmc.json           per-launch counters of every mrt_path_kernel build (exact /
                                     fast) + derived metrics, per-dispatch wave check
-  profiles/pmc_<name>.json          (--bench-file) what bench.py reads for roofline.traffic /
-                                    hbm_frac / valu_busy / valu_lane_util, keyed by workload config
+  profiles/pmc_s<scene>_<W>x<H>.json  what bench.py reads for its roofline (per-ray VALU
+                                    wave-instructions and HBM bytes, lane utilisation, issue busy),
+                                    keyed by the workload config of the profiled bench run
 
 HBM bytes follow MI355X_MICROARCH.md "HBM": FETCH_SIZE / WRITE_SIZE are in KiB and come from
 separate passes; on gfx950 FETCH_SIZE reports half the bytes of wide coalesced reads, so it is
@@ -15,7 +16,10 @@ MI355X_MICROARCH.md "DVFS give-back"): an issue-slot estimate (transcendental / 
 occupy more than 2 cycles, so it is a lower bound).  Lane utilisation = SQ_THREAD_CYCLES_VALU /
 (64 SQ_ACTIVE_INST_VALU).
 
-Usage: pmc_summary.py <tag> [--prof DIR] [--bench-file NAME --config "S W H SPP DEPTH"]
+The workload config is read from the profiled bench run's own JSON line (trace.log), so a
+profile is labelled with what actually ran.
+
+Usage: pmc_summary.py <tag> [--prof DIR] [--no-bench-file]
 """
 import argparse
 import collections
@@ -58,8 +62,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
     ap.add_argument("--prof", default=os.path.join(ROOT, "gpurun_out", "prof"))
-    ap.add_argument("--bench-file", default=None)
-    ap.add_argument("--config", default="5 500 500 1024 32")
+    ap.add_argument("--no-bench-file", action="store_true")
     a = ap.parse_args()
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
@@ -73,14 +76,18 @@ def main():
     sqp = os.path.join(a.prof, "sq", "run_counter_collection.csv")
     sqd = per_dispatch(sqp) if os.path.exists(sqp) else {}
     sq, _, _ = mean_by_kernel(sqd)
-    res = {"workload_config": [int(x) for x in a.config.split()], "kernels": {}, "sq_wave_check": []}
-    # rays of one launch: the bench line of the trace pass (one launch per step at these sizes)
-    rays_per_launch = None
+    # workload and rays of one launch: the bench line of the trace pass (one launch per step at
+    # these sizes, --pipeline 1)
+    rays_per_launch, cfg = None, None
     tl = os.path.join(a.prof, "trace.log")
-    if os.path.exists(tl):
-        for line in open(tl):
-            if line.startswith("{") and '"rays_per_step"' in line:
-                rays_per_launch = json.loads(line)["config"]["rays_per_step"]
+    for line in open(tl):
+        if line.startswith("{") and '"rays_per_step"' in line:
+            c = json.loads(line)["config"]
+            rays_per_launch = c["rays_per_step"]
+            cfg = [c["scene"], c["width"], c["height"], c["spp"], c["depth"]]
+    if cfg is None:
+        raise SystemExit(f"{tl}: no bench line (the trace pass failed?)")
+    res = {"workload_config": cfg, "kernels": {}, "sq_wave_check": []}
     for did, (k, c, m) in sorted(sqd.items(), key=lambda t: int(t[0])):
         try:
             grid_waves = int(m["Grid_Size"]) // 64
@@ -93,6 +100,9 @@ def main():
         e = {"launches": n_f[k], "dispatch": meta[k], "rays_per_launch": rays_per_launch, "FETCH_SIZE_KiB": fetch[k].get("FETCH_SIZE"),
              "WRITE_SIZE_KiB": write.get(k, {}).get("WRITE_SIZE")}
         e["hbm_bytes_per_launch"] = 2 * e["FETCH_SIZE_KiB"] * 1024 + (e["WRITE_SIZE_KiB"] or 0) * 1024
+        if rays_per_launch:
+            e["hbm_bytes_per_ray"] = e["hbm_bytes_per_launch"] / rays_per_launch
+            e["write_bytes_per_ray"] = (e["WRITE_SIZE_KiB"] or 0) * 1024 / rays_per_launch
         if k in avg_ns:
             e["avg_kernel_ns"] = avg_ns[k]
             e["hbm_GBps"] = e["hbm_bytes_per_launch"] / avg_ns[k]
@@ -100,6 +110,8 @@ def main():
         s = sq.get(k)
         if s:
             e["sq"] = s
+            if rays_per_launch:
+                e["valu_insts_per_ray"] = s["SQ_INSTS_VALU"] / rays_per_launch
             if s.get("SQ_ACTIVE_INST_VALU"):
                 e["valu_lane_util"] = s["SQ_THREAD_CYCLES_VALU"] / (64.0 * s["SQ_ACTIVE_INST_VALU"])
             if s.get("SQ_WAVE_CYCLES"):
@@ -112,13 +124,15 @@ def main():
                     e["effective_clock_GHz"] = cycles / avg_ns[k]
         res["kernels"][k] = e
     json.dump(res, open(os.path.join(out, f"{a.tag}_pmc.json"), "w"), indent=1)
-    if a.bench_file:
+    if not a.no_bench_file:
         by = {}
         for k, e in res["kernels"].items():
             num = "fast" if k.endswith("_fast") else "exact"
-            by[num] = {x: e.get(x) for x in ("hbm_bytes_per_launch", "valu_busy", "valu_lane_util", "avg_kernel_ns")}
-        json.dump({"config": res["workload_config"], "by_numerics": by, "source": f"profiles/{a.tag}_pmc.json"},
-                  open(os.path.join(out, a.bench_file), "w"), indent=1)
+            by[num] = {x: e.get(x) for x in ("valu_insts_per_ray", "hbm_bytes_per_ray", "write_bytes_per_ray", "valu_busy",
+                                             "valu_lane_util", "avg_kernel_ns", "rays_per_launch")}
+        name = f"pmc_s{cfg[0]}_{cfg[1]}x{cfg[2]}.json"
+        json.dump({"config": cfg, "by_numerics": by, "source": f"profiles/{a.tag}_pmc.json"},
+                  open(os.path.join(out, name), "w"), indent=1)
     print(json.dumps(res, indent=1)[:6000])
 
 

@@ -7,7 +7,7 @@ set -e
 CFGS=${PROF_CFGS:-"c3:9:800:800:256 c4:8:1024:1024:256 c5:7:2048:2048:64"}
 for cfg in $CFGS; do
   IFS=: read name sid W H S <<< "$cfg"
-  PROF_OUT=gpurun_out/prof_$name PROF_ARGS="--steps 1 --warmup 0 --kernel-reps 1 --pipeline 1 --no-cpu-baseline --scene $sid --width $W --height $H --samples $S" \
+  PROF_OUT=gpurun_out/prof_$name PROF_ARGS="--steps 1 --warmup 0 --kernel-reps 1 --pipeline 1 --no-cpu-baseline --no-other-walk --no-parity --scene $sid --width $W --height $H --samples $S" \
     bash tools/profile.sh
   echo "== $name done $(date +%T)"
 done

@@ -11,7 +11,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=${PROF_OUT:-gpurun_out/prof}
 mkdir -p $OUT
-ARGS=${PROF_ARGS:-"--steps 1 --warmup 0 --kernel-reps 1 --pipeline 1 --no-cpu-baseline"}
+ARGS=${PROF_ARGS:-"--steps 1 --warmup 0 --kernel-reps 1 --pipeline 1 --no-cpu-baseline --no-other-walk --no-parity"}
 SQ=${PROF_SQ:-"SQ_WAVES,SQ_INSTS_VALU,SQ_ACTIVE_INST_VALU,SQ_THREAD_CYCLES_VALU,SQ_WAVE_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_BUSY_CYCLES,GRBM_GUI_ACTIVE"}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py $ARGS > $OUT/trace.log 2>&1
 echo "trace done $(date +%T)"
