@@ -327,7 +327,50 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
     // (bunny -4%, teapot -5%; Cornell +1.8%, book2 0)
     constexpr bool kShared = (F & FT_MESH) == 0;
     constexpr bool kResume = MRT_SIG_OF(F) == SIG_ROOM_MESH;
-    if constexpr (kShared) {
+    if constexpr (kResumeLin<F>) {
+        // Linear hit programs with bvh_node subtrees (random spheres, book2): the intersection is
+        // RESUMABLE per lane (mrt_resume.h): one iteration = (1) idle lanes take new paths; (2) the
+        // lanes walking a BVH subtree step until few still walk and enough others have work; (3) one
+        // sweep over the program for the lanes between walks (each from its own op); (4) the lanes
+        // whose intersection is complete shade, and end their path or begin the next segment.
+        ResumeState w;
+        w.st = RS_IDLE;
+        HitRec rec;
+        for (;;) {
+            take_paths([&](float u, float v) {
+                ps.r = camera_ray(S, ps.rng, u, v);
+                rs_begin(w, ps.r, Ls);
+            });
+            if (!__any(active)) break;
+            PH_MARK(ph, 0);
+            while (__any(w.st == RS_WALK)) {
+                if (w.st == RS_WALK) {
+                    const uint32_t res = bvhw_step<F>(S, w, rec, Ls, 0.001f);
+                    if (res != 0u) rs_walk_end<F>(S, w, rec, res);
+                }
+                if ((uint32_t)__popcll(__ballot(w.st == RS_WALK)) <= P.walk_min &&
+                    (uint32_t)__popcll(__ballot(w.st == RS_SWEEP || (!active && !exhausted))) >= MRT_WALK_OTHER)
+                    break;  // others can sweep / start paths
+            }
+            PH_MARK(ph, 11);
+            rs_sweep<F>(S, w, rec, Ls, ps.rng, 0.001f);
+            PH_MARK(ph, 1);
+            if (w.st == RS_DONE) {
+                ps.rays++;  // one trace() call (main.cpp:68)
+                const bool hit = rs_finish_hit<F>(S, w, ps.r, rec, Ls);
+                f3 L;
+                const bool ended = shade_hit<F, LK>(S, ps, P.max_bounces, lev, hit, rec, &L, ph);
+                PH_MARK(ph, 2);
+                if (ended) {
+                    finish_path(L);
+                    w.st = RS_IDLE;
+                } else {
+                    rs_begin(w, ps.r, Ls);
+                }
+            }
+            PH_MARK(ph, 3);
+        }
+    } else if constexpr (kShared) {
         // One iteration: (1) every lane with a ray traces one segment; a path that ends is folded
         // and stored; (2) lanes without a path take new ones (camera ray arguments); (3) ONE
         // make_ray for every lane with a next ray -- camera and scattered rays alike, instead of one

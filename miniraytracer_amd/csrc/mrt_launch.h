@@ -4,7 +4,7 @@
 // FMA contraction, hardware reciprocal/sqrt, f32 transcendentals).  DESIGN.md "Numerics contracts".
 #pragma once
 #include <hip/hip_runtime.h>
-#include "mrt_shade.h"
+#include "mrt_resume.h"
 
 namespace mrtd {
 
@@ -58,6 +58,15 @@ typedef void (*path_kernel_t)(PathParams);
 #endif
 // one claim must cover a whole wave's idle lanes (the pool hands out at most 64 at once)
 static_assert(MRT_TAIL_BATCH >= 64u && MRT_BATCH >= MRT_TAIL_BATCH, "claims must be at least a wave wide");
+
+// Linear programs with bvh_node subtrees run the resumable interpreter (mrt_resume.h); its query ray
+// lives in the LDS save area (15 words per lane slot, as instances need) -- MRT_RESUME_LIN=0 builds
+// the lockstep interpreter instead (A/B)
+#ifndef MRT_RESUME_LIN
+#define MRT_RESUME_LIN 1
+#endif
+template <uint32_t F>
+static constexpr bool kResumeLin = MRT_RESUME_LIN && (F & FT_LIN) != 0 && (F & FT_BVHW) != 0 && MRT_SIG_OF(F) == SIG_NONE;
 
 // kernel variants by scene features (the first instantiated superset is launched); FT_LIN
 // variants need the scene's linear hit program (mrt_lin.h), FT_ALL runs any graph.  The same list

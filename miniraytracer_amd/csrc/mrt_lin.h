@@ -28,7 +28,11 @@ enum : uint32_t {
     LOP_VBOUND = 9,
 };
 
-// one op = the node's own record (no second load): code = op | kind << 8 | flags << 16
+// one op = the node's own record (no second load): code = op | kind << 8 | flags << 16 | level << 24
+// (the nesting level the op is tested at).  Host-filled extras for the resumable interpreter
+// (mrt_resume.h): prim / mesh / bvh / volume ops carry the enclosing instance's op index in f[11]
+// (MRT_NONE outside instances), a BVHW op its subtree's root ref in skip, an INST_END op its
+// instance op's index in skip.
 struct LinOp {
     uint32_t code, node, skip, mat;
     float f[12];
@@ -38,6 +42,8 @@ static_assert(sizeof(LinOp) == 64, "LinOp is one 64 B scalar load");
 #define LOP_OP(o) ((o).code & 0xFFu)
 #define LOP_KIND(o) (((o).code >> 8) & 0xFFu)
 #define LOP_FLAGS(o) (((o).code >> 16) & 0xFFu)
+#define LOP_LVL(o) (((o).code >> 24) & 0xFFu)
+#define LOP_INST_OF(o) (__float_as_uint((o).f[11]))
 
 MRT_DFN uint32_t op_flags(const LinOp& o) { return LOP_FLAGS(o); }
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -161,19 +167,18 @@ MRT_DFN void lin_prim_rec(const DScene& S, uint32_t node, const Ray& r, float t,
         return;
     }
     const float ns = nf[5];
-    float pb, pc;
-    if (kind == MRT_K_XY) {
-        rec.n = f3{0, 0, ns};
-        if (MRT_FAST_SNAP) rec.p.z = nf[4];
-        if (needuv) { pb = r.o.x + t * r.d.x; pc = r.o.y + t * r.d.y; }
-    } else if (kind == MRT_K_XZ) {
-        rec.n = f3{0, ns, 0};
-        if (MRT_FAST_SNAP) rec.p.y = nf[4];
-        if (needuv) { pb = r.o.x + t * r.d.x; pc = r.o.z + t * r.d.z; }
-    } else {
-        rec.n = f3{ns, 0, 0};
-        if (MRT_FAST_SNAP) rec.p.x = nf[4];
-        if (needuv) { pb = r.o.y + t * r.d.y; pc = r.o.z + t * r.d.z; }
+    // the rect's in-plane hit coordinates (rect.cpp:34-38: o + t * d on its two axes) are the
+    // record's point before any snapping, chosen by selects (a kind-indexed choice had become a
+    // per-lane lookup table in scratch memory)
+    const f3 p0 = rec.p;
+    const float pb = kind == MRT_K_YZ ? p0.y : p0.x;
+    const float pc = kind == MRT_K_XY ? p0.y : p0.z;
+    const bool xy = kind == MRT_K_XY, xz = kind == MRT_K_XZ;
+    rec.n = f3{xy || xz ? 0.0f : ns, xz ? ns : 0.0f, xy ? ns : 0.0f};
+    if (MRT_FAST_SNAP) {
+        rec.p.x = xy || xz ? p0.x : nf[4];
+        rec.p.y = xz ? nf[4] : p0.y;
+        rec.p.z = xy ? nf[4] : p0.z;
     }
     if (needuv) {
         rec.u = (pb - nf[0]) / (nf[1] - nf[0]);

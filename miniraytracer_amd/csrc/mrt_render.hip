@@ -384,14 +384,24 @@ struct LinCompiler {
     const mrt_scene_view* v;
     std::vector<LinOp> prog;
     int max_lvl = 0;
-    LinOp op_of(uint32_t code, uint32_t id) {
+    uint32_t inst_pc = MRT_NONE;  // op index of the enclosing instance while its subtree is emitted
+    // code = op | kind << 8 | flags << 16 | nesting level << 24 (the level the op is tested at: the
+    // resumable interpreter, mrt_resume.h, restarts a lane mid-program without replaying the levels)
+    LinOp op_of(uint32_t code, uint32_t id, int lvl) {
         const mrt_node& n = nodes[id];
         LinOp o{};
-        o.code = code | ((n.kind & 0xFFu) << 8) | (n.kind & 0xFF0000u);
+        o.code = code | ((n.kind & 0xFFu) << 8) | (n.kind & 0xFF0000u) | ((uint32_t)lvl << 24);
         o.node = id;
         o.skip = 0;
         o.mat = n.mat;
         for (int i = 0; i < 12; i++) o.f[i] = n.f[i];
+        return o;
+    }
+    // primitive-like ops (prim, mesh, bvh subtree, volume) also carry the enclosing instance's op
+    // index in f[11] (which they do not use) for the resumable interpreter
+    LinOp leaf_op(uint32_t code, uint32_t id, int lvl) {
+        LinOp o = op_of(code, id, lvl);
+        memcpy(&o.f[11], &inst_pc, 4);
         return o;
     }
     bool emit(uint32_t id, int inst_depth, int lvl, int guard) {
@@ -401,38 +411,46 @@ struct LinCompiler {
         max_lvl = std::max(max_lvl, lvl);
         switch (k) {
         case MRT_K_SPHERE: case MRT_K_XY: case MRT_K_XZ: case MRT_K_YZ:
-            prog.push_back(op_of(LOP_PRIM, id));
+            prog.push_back(leaf_op(LOP_PRIM, id, lvl));
             return true;
         case MRT_K_MESH:
-            prog.push_back(op_of(LOP_MESH, id));
+            prog.push_back(leaf_op(LOP_MESH, id, lvl));
             return true;
-        case MRT_K_BVHW:
-            prog.push_back(op_of(LOP_BVHW, id));
+        case MRT_K_BVHW: {
+            LinOp o = leaf_op(LOP_BVHW, id, lvl);
+            o.skip = n.a;  // the subtree's root ref (the op's f[0..5] are its box)
+            prog.push_back(o);
             return true;
+        }
         case MRT_K_VOLUME: {  // a primitive boundary only (sphere / rect)
             if (n.a >= nodes.size()) return false;
             const uint32_t bk = nodes[n.a].kind & 0xFFu;
             if (bk != MRT_K_SPHERE && bk != MRT_K_XY && bk != MRT_K_XZ && bk != MRT_K_YZ) return false;
-            prog.push_back(op_of(LOP_VOLUME, id));
-            prog.push_back(op_of(LOP_VBOUND, n.a));
+            prog.push_back(leaf_op(LOP_VOLUME, id, lvl));
+            prog.push_back(op_of(LOP_VBOUND, n.a, lvl));
             return true;
         }
         case MRT_K_LIST: {
             size_t at = prog.size();
-            prog.push_back(op_of(LOP_LIST, id));
+            prog.push_back(op_of(LOP_LIST, id, lvl));
             for (uint32_t i = 0; i < n.b; i++)
                 if (!emit(v->children[n.a + i], inst_depth, lvl + 1, guard + 1)) return false;
             prog[at].skip = (uint32_t)prog.size();
-            prog.push_back(op_of(LOP_LIST_END, id));
+            prog.push_back(op_of(LOP_LIST_END, id, lvl));
             return true;
         }
         case MRT_K_TRANSLATE: case MRT_K_ROTY: case MRT_K_TRROTY: {
             if (inst_depth > 0) return false;
             size_t at = prog.size();
-            prog.push_back(op_of(LOP_INST, id));
-            if (!emit(n.a, inst_depth + 1, lvl + 1, guard + 1)) return false;
+            prog.push_back(op_of(LOP_INST, id, lvl));
+            inst_pc = (uint32_t)at;
+            const bool ok = emit(n.a, inst_depth + 1, lvl + 1, guard + 1);
+            inst_pc = MRT_NONE;
+            if (!ok) return false;
             prog[at].skip = (uint32_t)prog.size();
-            prog.push_back(op_of(LOP_INST_END, id));
+            LinOp e = op_of(LOP_INST_END, id, lvl);
+            e.skip = (uint32_t)at;  // its instance op
+            prog.push_back(e);
             return true;
         }
         default:
@@ -814,7 +832,8 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     s->lds_frames = lin_kernel ? 0 : (uint32_t)std::max(T.max_frames - 1, 0);
     s->lds_rays = lin_kernel ? 0 : (uint32_t)T.max_rays;
     s->lds_mesh = (uint32_t)T.max_mesh;
-    s->lds_save = (lin_kernel && (kVariants[s->variant] & FT_INST)) ? 15u : 0u;
+    // the query ray parked in LDS: instances (scene_hit_lin) and the resumable interpreter (mrt_resume.h)
+    s->lds_save = (lin_kernel && (kVariants[s->variant] & (FT_INST | (MRT_RESUME_LIN ? FT_BVHW : 0u)))) ? 15u : 0u;
     // resumable mesh walk: deeper pod_bvh trees keep the wave walking longer
     s->walk_min = T.wide.size() >= 2048 ? 40u : 32u;  // inner nodes: bunny 2937, teapot ~1045
     const std::vector<BvhWide>& bwide = T.bwide;

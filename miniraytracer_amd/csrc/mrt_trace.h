@@ -80,7 +80,14 @@ MRT_DFN WideNode load_wide(const W* p) {
 // BVHs are copied into the workgroup's LDS at kernel start, and a node ref below the treelet size
 // reads there -- one flat load per 16 B that the hardware routes to LDS or memory per lane.
 MRT_DFN WideNode load_wide_q(const float4* q) {
-    const float4 a = q[0], b = q[1], c = q[2], d = q[3];
+    float4 a = q[0], b = q[1], c = q[2], d = q[3];
+#if defined(__HIP_DEVICE_COMPILE__)
+    // all four 16-B pieces in flight together: otherwise the compiler sinks a child's box load
+    // below the test of its flag word (`!(flags & 1) || aabb_hit(...)`), a second dependent round
+    // trip per node visit
+    asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(a.z), "+v"(a.w), "+v"(b.x), "+v"(b.y), "+v"(b.z), "+v"(b.w));
+    asm volatile("" : "+v"(c.x), "+v"(c.y), "+v"(c.z), "+v"(c.w), "+v"(d.x), "+v"(d.y), "+v"(d.z), "+v"(d.w));
+#endif
     WideNode n;
     n.lmin = f3{a.x, a.y, a.z};
     n.lref = __float_as_uint(a.w);

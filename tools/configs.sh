@@ -10,5 +10,5 @@ for cfg in $CFGS; do
   echo "== scene $sid ${W}x${H} ${S}spp $(date +%T)"
   timeout -k 10 400 python bench.py --no-cpu-baseline --steps 1 --warmup 0 --kernel-reps 1 \
       --scene $sid --width $W --height $H --samples $S > gpurun_out/cfg_$sid.log 2>&1 || exit 3
-  python tools/_show.py gpurun_out/cfg_$sid.log "scene $sid"
+  python tools/show_bench.py gpurun_out/cfg_$sid.log "scene $sid"
 done
