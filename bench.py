@@ -71,6 +71,9 @@ def parse():
                     help="single-GPU rehearsal: render only rank --emulate-rank's share of an N-rank job "
                          "(no collectives); used to predict per-rank step time at N GPUs")
     ap.add_argument("--emulate-rank", type=int, default=0)
+    ap.add_argument("--emulate-gather", action="store_true",
+                    help="with --emulate-world: also run rank 0's framebuffer scatter of all N shards each "
+                         "step (the gather's device-side work; the xGMI transfer itself is not emulated)")
     ap.add_argument("--chunk-samples", type=int, default=0,
                     help="samples per path-kernel launch (0: the library's choice)")
     ap.add_argument("--fold", choices=["auto", "lean", "full"], default="full",
@@ -318,18 +321,25 @@ def main():
         r.prepare(desc)
     px = m.local_pixels(desc)
     n_local = len(px)
-    outs = [torch.zeros((n_local, 4), dtype=torch.float32, device=dev) for _ in range(npipe)]
+    n_rows = n_local
+    tg = eg = None
+    if world > 1:
+        from miniraytracer_amd.dist import TileGather
+        tg = TileGather(args.width, args.height, args.samples, args.depth, world, rank, dev, tile_size=args.tile_size)
+        assert tg.n_local == n_local
+        n_rows = tg.n_max  # renders write straight into the padded shard the gather sends
+    elif d_world > 1 and args.emulate_gather:
+        from miniraytracer_amd.dist import TileGather
+        eg = TileGather(args.width, args.height, args.samples, args.depth, d_world, 0, dev, tile_size=args.tile_size)
+        n_rows = eg.n_max
+    outs = [torch.zeros((n_rows, 4), dtype=torch.float32, device=dev) for _ in range(npipe)]
     out = outs[0]
     rays = torch.zeros(1, dtype=torch.int64, device=dev)  # every context adds its rays here (device atomics)
     stream = torch.cuda.current_stream(dev)
     streams = [stream] + [torch.cuda.Stream(dev) for _ in range(npipe - 1)]
 
-    if world > 1:
-        from miniraytracer_amd.dist import TileGather
-        tg = TileGather(args.width, args.height, args.samples, args.depth, world, rank, dev, tile_size=args.tile_size)
-        assert tg.n_local == n_local
-
     pending = [None]
+    sent = [None] * npipe  # the gather that last read context j's output buffer
     it = [0]
     ctx = [rnds]  # the render contexts measure() uses (the other-walk timing swaps in its own)
 
@@ -339,13 +349,17 @@ def main():
         j = it[0] % npipe
         it[0] += 1
         with torch.cuda.stream(streams[j]):
+            if sent[j] is not None:  # the gather of this buffer's previous render has read it
+                sent[j].wait()
             ctx[0][j].render_device(d, outs[j].data_ptr(), rays.data_ptr(), streams[j].cuda_stream)
             if world > 1:
                 # the one RCCL collective of the data path (tile shards -> rank 0), overlapped with
                 # the next render: finish the previous step's gather, then start this one's
                 if pending[0] is not None:
                     tg.finish(pending[0])
-                pending[0] = tg.start(outs[j])
+                pending[0] = sent[j] = tg.start(outs[j])
+            elif eg is not None:
+                eg.scatter()  # rehearsal: rank 0's device-side share of the gather
 
     def drain():
         if pending[0] is not None:
@@ -407,7 +421,7 @@ def main():
         if world > 1:
             return tg.full.view(args.height, args.width, 4).cpu().numpy() if rank == 0 else None
         full = np.zeros((args.width * args.height, 4), dtype=np.float32)
-        full[px] = outs[(it[0] - 1) % npipe].cpu().numpy()
+        full[px] = outs[(it[0] - 1) % npipe][:n_local].cpu().numpy()
         return full.reshape(args.height, args.width, 4)
 
     # parity of the timed render (after the timed region): the last step's image against the
@@ -505,7 +519,8 @@ def main():
                        "scene": args.scene, "width": args.width, "height": args.height,
                        "spp": desc.sqrt_samples ** 2, "depth": args.depth, "parallelism": f"tiles{world}",
                        "tile_size": args.tile_size, "pipeline": npipe, "fold": "lean" if lean_fold else "full", "numerics": args.numerics,
-                       **({"emulated_share": f"rank {d_rank} of {d_world}"} if d_world != world else {}),
+                       **({"emulated_share": f"rank {d_rank} of {d_world}" + (", + rank 0's scatter" if eg is not None else "")}
+                          if d_world != world else {}),
                        "rays_per_step": nrays // args.steps},
             "roofline": roof,
             "parity": par,

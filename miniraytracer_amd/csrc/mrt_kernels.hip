@@ -121,10 +121,18 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t words = (P.lds_frames * 2 + P.lds_rays * 11 + P.lds_mesh + P.lds_save + LK * 4 + PathQ<F>::words) * 64;
+    // per wave: its stacks and queues ([slot][word][lane]), then (MeshTreeOf) its mesh treelet
+    const uint32_t words = (P.lds_frames * 2 + P.lds_rays * 11 + P.lds_mesh + P.lds_save + LK * 4 + PathQ<F>::words) * 64 +
+                           (MeshTreeOf<F>::on ? P.mtree_n * 16u : 0u);
     uint32_t* wb = lds + wave * words;
     uint32_t* const wmesh = wb + P.lds_frames * 128 + P.lds_rays * 704;
     float4* tree = nullptr;
+    if constexpr (MeshTreeOf<F>::on) {
+        // the wave's own copy of the top mesh BVH nodes (one-wave groups: no other wave reads it)
+        tree = reinterpret_cast<float4*>(wb + words - P.mtree_n * 16u);
+        for (uint32_t i = lane; i < P.mtree_n * 4u; i += 64u) tree[i] = reinterpret_cast<const float4*>(P.sc.mwide)[i];
+        __syncthreads();
+    }
     if constexpr (TreeOf<F>::on) {
         // the workgroup's copy of the top wide nodes (after every wave's own region), filled once
         // before any wave starts a path; no other barrier follows in this persistent kernel
@@ -133,7 +141,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
         __syncthreads();
     }
     const LStack Ls{wb, (float*)(wb + P.lds_frames * 128), wmesh, (float*)(wmesh + P.lds_mesh * 64), lane, tree,
-                    TreeOf<F>::on ? P.tree_n : 0u};
+                    TreeOf<F>::on ? P.tree_n : MeshTreeOf<F>::on ? P.mtree_n : 0u};
     // the wave's queue of path starts ([word][entry], PathQ): after the fold levels
     float* const Lq = (float*)(wmesh + (P.lds_mesh + P.lds_save + LK * 4) * 64);
     const DScene& S = P.sc;
@@ -561,7 +569,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
             while (__any(phase == PH_WALK)) {
                 if (phase == PH_WALK) {
                     const mrt_node mn = ld_node(const_ptr(S.nodes) + prog[kMeshPC].node);
-                    const uint32_t st = mesh_step(S, mn, ps.r, 0.001f, w.closest, rec, Ls, ref, msp, w.hdone);
+                    const uint32_t st = mesh_step<MeshTreeOf<F>::on>(S, mn, ps.r, 0.001f, w.closest, rec, Ls, ref, msp, w.hdone);
                     if (st == 1u) w.hnode = kMeshPC;  // w.closest = the hit's t, w.hdone set
                     phase = st != 0u ? PH_DONE : PH_WALK;
                 }
@@ -632,7 +640,9 @@ const KernelTable& mrtd::kernel_table_exact() {
         {PathQ<kVariants[0]>::words, PathQ<kVariants[1]>::words, PathQ<kVariants[2]>::words, PathQ<kVariants[3]>::words,
          PathQ<kVariants[4]>::words, PathQ<kVariants[5]>::words, PathQ<kVariants[6]>::words},
         {kBox6Walk<kVariants[0]>, kBox6Walk<kVariants[1]>, kBox6Walk<kVariants[2]>, kBox6Walk<kVariants[3]>,
-         kBox6Walk<kVariants[4]>, kBox6Walk<kVariants[5]>, kBox6Walk<kVariants[6]>}};
+         kBox6Walk<kVariants[4]>, kBox6Walk<kVariants[5]>, kBox6Walk<kVariants[6]>},
+        {MeshTreeOf<kVariants[0]>::on, MeshTreeOf<kVariants[1]>::on, MeshTreeOf<kVariants[2]>::on, MeshTreeOf<kVariants[3]>::on,
+         MeshTreeOf<kVariants[4]>::on, MeshTreeOf<kVariants[5]>::on, MeshTreeOf<kVariants[6]>::on}};
     static_assert(kNumVariants == 7, "one table entry per variant");
     return t;
 }

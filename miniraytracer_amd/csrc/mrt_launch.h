@@ -42,6 +42,7 @@ struct PathParams {
     uint32_t walk_min;                    // resumable mesh walk: yield once at most this many lanes walk
     const float4* tree_src;               // TreeOf<F>::on kernels: BvhWide nodes copied to LDS at start
     uint32_t tree_n;                      // how many (the first tree_n of the breadth-first array)
+    uint32_t mtree_n;                     // MeshTreeOf<F>::on kernels: MeshWide nodes each wave copies to its LDS
 };
 
 typedef void (*path_kernel_t)(PathParams);
@@ -89,6 +90,7 @@ struct KernelTable {
     uint32_t tree[kNumVariants];  // 1: the kernel reads the top BvhWide nodes from an LDS treelet
     uint32_t pq[kNumVariants];    // LDS words per lane slot of the kernel's queue of path starts
     uint32_t box6_walk[kNumVariants];  // 1: Cornell shape walked by cornell_fast_hit when op 8 is MRT_F_BOX6
+    uint32_t mtree[kNumVariants];      // 1: each wave keeps a treelet of the top mesh BVH nodes in LDS
 };
 const KernelTable& kernel_table_exact();
 const KernelTable& kernel_table_fast();

@@ -189,25 +189,28 @@ struct PathLaunch {
     uint32_t vgprs = 0;
     uint32_t wg = 64;     // threads per workgroup
     uint32_t tree_n = 0;  // BvhWide nodes kept in each workgroup's LDS (treelet kernels)
+    uint32_t mtree_n = 0;  // MeshWide nodes kept in each wave's LDS (mesh treelet kernels)
     uint32_t lds_save = 0;  // LDS words per lane slot for the query ray parked during instances
 };
 
 // Wide nodes renumbered breadth-first over all roots together (level 0 of every tree, then level
 // 1, ...), so the first K nodes of the array are the top levels of the scene's BVHs -- what a
 // treelet of K nodes holds.  Only the labels change: every walk visits the same nodes.
+// limit: only the first `limit` nodes breadth-first, the others after them in their own order
+// (pod_bvh's depth-first layout keeps a subtree's nodes together in the cache).
 template <typename W>
-static void bfs_order(std::vector<W>& wide, std::vector<uint32_t*> roots, uint32_t leaf_bit) {
+static void bfs_order(std::vector<W>& wide, std::vector<uint32_t*> roots, uint32_t leaf_bit, uint32_t limit = 0xFFFFFFFFu) {
     const uint32_t n = (uint32_t)wide.size();
     std::vector<uint32_t> nid(n, MRT_NONE), order;
     order.reserve(n);
     for (uint32_t* r : roots)
-        if (!(*r & leaf_bit) && *r < n && nid[*r] == MRT_NONE) { nid[*r] = (uint32_t)order.size(); order.push_back(*r); }
-    for (size_t q = 0; q < order.size(); q++) {
+        if (!(*r & leaf_bit) && *r < n && nid[*r] == MRT_NONE && order.size() < limit) { nid[*r] = (uint32_t)order.size(); order.push_back(*r); }
+    for (size_t q = 0; q < order.size() && order.size() < limit; q++) {
         const W& w = wide[order[q]];
         for (uint32_t c : {w.lref, w.rref})
-            if (!(c & leaf_bit) && c < n && nid[c] == MRT_NONE) { nid[c] = (uint32_t)order.size(); order.push_back(c); }
+            if (!(c & leaf_bit) && c < n && nid[c] == MRT_NONE && order.size() < limit) { nid[c] = (uint32_t)order.size(); order.push_back(c); }
     }
-    for (uint32_t i = 0; i < n; i++)  // unreachable nodes keep a slot at the end
+    for (uint32_t i = 0; i < n; i++)  // the rest (and unreachable nodes) in their own order
         if (nid[i] == MRT_NONE) { nid[i] = (uint32_t)order.size(); order.push_back(i); }
     auto remap = [&](uint32_t c) { return (c & leaf_bit) || c >= n ? c : nid[c]; };
     std::vector<W> out(n);
@@ -591,6 +594,11 @@ mrt_status mrt_internal_scene_tables(const mrt_scene_view* v, SceneTables* T) {
         for (mrt_node& n : nodes)
             if ((n.kind & 0xFF) == MRT_K_MESH) n.b = ref_of(n.a);
         if (!ok) return mrt_internal_fail(MRT_ERR_INVALID, "mesh BVH outside the device encoding (leaf > 127 triangles or > 2^24 triangles)");
+        // the top levels first (the per-wave LDS treelet of the mesh kernels, mrt_kernels.hip)
+        std::vector<uint32_t*> mroots;
+        for (mrt_node& n : nodes)
+            if ((n.kind & 0xFF) == MRT_K_MESH) mroots.push_back(&n.b);
+        bfs_order(wide, mroots, MESH_LEAF, MRT_MESH_TREE_MAX);
     }
     // bvh_node subtrees whose leaves are primitives / object_lists of primitives (and of boxes of
     // primitives) -> wide nodes; the subtree root becomes an MRT_K_BVHW node (a = root ref)
@@ -876,6 +884,18 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
             L.tree_n = std::min(cap, (uint32_t)bwide.size());
             L.lds_bytes += (size_t)L.tree_n * 64u;
         }
+        if (tabs[k]->mtree[s->variant]) {
+            // each wave's copy of the top mesh nodes, in the LDS its resident groups leave free
+            // (so the treelet never costs occupancy)
+            const size_t per = (160u * 1024u) / (size_t)nb;
+            uint32_t cap = per > L.lds_bytes ? (uint32_t)((per - L.lds_bytes) / 64u) : 0u;
+#ifdef MRT_EXPERIMENTS
+            if (const char* e = getenv("MRT_MESH_TREE_NODES"))  // sweep hook
+                if (*e) cap = std::min<uint32_t>(cap, (uint32_t)atoi(e));
+#endif
+            L.mtree_n = std::min<uint32_t>({cap, MRT_MESH_TREE_MAX, (uint32_t)T.wide.size()});
+            L.lds_bytes += (size_t)L.mtree_n * 64u;
+        }
         L.vgprs = (uint32_t)fa.numRegs;
 #ifdef MRT_EXPERIMENTS
         if (const char* e = getenv("MRT_BLOCKS_PER_CU"))  // experiment hook
@@ -1096,6 +1116,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.walk_min = s->walk_min;
         P.tree_src = reinterpret_cast<const float4*>(s->S.bwide);
         P.tree_n = PL.tree_n;
+        P.mtree_n = PL.mtree_n;
         P.pixels = s->d_pixels;
         P.sdist = s->d_sdist;
         P.npix = s->npix;
@@ -1307,7 +1328,7 @@ extern "C" mrt_status mrt_scene_kernel_info(const mrt_scene* s, mrt_kernel_info*
     out->prog_ops = s->prog_ops;
     out->vgprs = L.vgprs;
     out->wg = L.wg;
-    out->tree_nodes = L.tree_n;
+    out->tree_nodes = L.tree_n ? L.tree_n : L.mtree_n;  // BvhWide per workgroup, or MeshWide per wave
     return MRT_OK;
 }
 

@@ -206,6 +206,20 @@ struct TreeOf {
                                ((F & (FT_BVHW | FT_TEX | FT_VOLUME)) != 0 || !(F & FT_LIN));
     static constexpr uint32_t wg = on ? MRT_TREE_WG : 64u;  // threads per path-kernel workgroup
 };
+// Hot pod_bvh nodes in LDS for the resumable mesh kernels (room + mesh, 7 one-wave groups per
+// SIMD): each wave keeps its OWN copy of the top MeshWide nodes (the upload numbers the first
+// MRT_MESH_TREE_MAX of them breadth-first) in the LDS its stacks leave free at that occupancy --
+// copied once at kernel start, no workgroup barrier, no occupancy given up.
+#ifndef MRT_MESH_TREE_MAX
+#define MRT_MESH_TREE_MAX 63u
+#endif
+#ifndef MRT_MESH_TREE
+#define MRT_MESH_TREE 1
+#endif
+template <uint32_t F>
+struct MeshTreeOf {
+    static constexpr bool on = MRT_MESH_TREE && (F & FT_MESH) != 0 && ((F >> 16) & 0xFFu) == 2u /* SIG_ROOM_MESH (mrt_sig.h) */;
+};
 // wide node `ref` of a BvhWide / MeshWide array: from the LDS treelet when it holds it
 template <bool TREE, typename W>
 MRT_DFN WideNode wide_at(const W* base, uint32_t ref, const LStack& L) {
@@ -452,6 +466,7 @@ MRT_DFN bool mesh_hit(const DScene& S, const mrt_node& n, const Ray& r, float tm
 // triangles) and lanes at inner nodes cost about the same per step.  Returns 0: keep walking,
 // 1: hit (rec complete, tt = its t; the walk is over: first-hit early-out), 2: no hit.  Every lane
 // performs mesh_hit's operations in mesh_hit's order: the results are bit-identical.
+template <bool TREE = false>
 MRT_DFN uint32_t mesh_step(const DScene& S, const mrt_node& n, const Ray& r, float tmin, float& tt, HitRec& rec,
                                               const LStack& L, uint32_t& ref, uint32_t& msp, bool& in_hit) {
     if (ref & MESH_LEAF) {
@@ -480,7 +495,7 @@ MRT_DFN uint32_t mesh_step(const DScene& S, const mrt_node& n, const Ray& r, flo
             return 1u;
         }
     } else {
-        const WideNode W = wide_at<false>(S.mwide, ref, L);
+        const WideNode W = wide_at<TREE>(S.mwide, ref, L);
         const bool hl = aabb_hit(W.lmin, W.lmax, r, tmin, tt);
         const bool hr = aabb_hit(W.rmin, W.rmax, r, tmin, tt);
         const bool left_first = (W.order & r.mask) != 0;

@@ -16,6 +16,12 @@ from . import local_pixels, render_desc
 
 
 class TileGather:
+    """One rank's end of the framebuffer gather.  Shards are gathered at their padded size
+    (n_max rows): a render writes its n_local rows straight into a padded buffer (bench.py
+    allocates its render outputs that way), so no pad copy is made; rank 0 receives all shards
+    into ONE [world, n_max, 4] tensor and scatters them into the framebuffer with ONE index_copy_
+    (padding rows land on a spare row past the image)."""
+
     def __init__(self, width, height, samples, depth, world, rank, device, tile_size=32):
         self.world, self.rank, self.device = world, rank, device
         self.width, self.height = width, height
@@ -26,25 +32,38 @@ class TileGather:
         self.n_local = self.counts[rank]
         self.pad = torch.zeros((self.n_max, 4), dtype=torch.float32, device=device)
         if rank == 0:
-            self.bufs = [torch.zeros((self.n_max, 4), dtype=torch.float32, device=device) for _ in range(world)]
-            self.idx = [torch.as_tensor(p.astype(np.int64), device=device) for p in self.px]
-            self.full = torch.zeros((width * height, 4), dtype=torch.float32, device=device)
+            self.recv = torch.zeros((world, self.n_max, 4), dtype=torch.float32, device=device)
+            self.bufs = list(self.recv.unbind(0))
+            spare = width * height  # padding rows of every shard go here
+            idx = np.full((world, self.n_max), spare, dtype=np.int64)
+            for r, p in enumerate(self.px):
+                idx[r, : len(p)] = p
+            self.idx = torch.as_tensor(idx.reshape(-1), device=device)
+            self.full_ext = torch.zeros((width * height + 1, 4), dtype=torch.float32, device=device)
+            self.full = self.full_ext[: width * height]
 
     def gather(self, local):
-        """local: [n_local, 4] float32 on `device`.  Returns the [H, W, 4] framebuffer on rank 0."""
+        """local: [n_local or n_max, 4] float32 on `device`.  Returns the [H, W, 4] framebuffer on rank 0."""
         return self.finish(self.start(local))
 
     def start(self, local):
-        """Enqueue the gather of `local` (its contents are copied before this returns on the
-        device stream, so the caller may render into it again).  Returns a handle for finish()."""
-        self.pad[: self.n_local].copy_(local)
-        return dist.gather(self.pad, self.bufs if self.rank == 0 else None, dst=0, async_op=True)
+        """Enqueue the gather of `local` (a padded [n_max, 4] buffer is sent as it is; a compact
+        [n_local, 4] one is first copied into the padded staging buffer).  The caller must not
+        write into a buffer it passed before finish() of that gather.  Returns a handle."""
+        src = local
+        if local.shape[0] != self.n_max:
+            self.pad[: self.n_local].copy_(local)
+            src = self.pad
+        return dist.gather(src, self.bufs if self.rank == 0 else None, dst=0, async_op=True)
 
     def finish(self, handle):
         """Wait for a start()ed gather and, on rank 0, scatter the shards into the framebuffer."""
         handle.wait()
         if self.rank != 0:
             return None
-        for r in range(self.world):
-            self.full.index_copy_(0, self.idx[r], self.bufs[r][: self.counts[r]])
+        self.scatter()
         return self.full.view(self.height, self.width, 4)
+
+    def scatter(self):
+        """Rank 0: the received shards -> framebuffer rows (one index_copy_)."""
+        self.full_ext.index_copy_(0, self.idx, self.recv.view(-1, 4))

@@ -49,8 +49,12 @@ def _worker(rank, world, port, q):
     # overlapped form used by bench.py: start() copies the shard, finish() scatters on rank 0
     h = tg.start(local * 0 + local)
     full2 = tg.finish(h)
+    # a render output allocated at the padded shard size is sent as it is (bench.py)
+    padded = torch.zeros((tg.n_max, 4), dtype=torch.float32)
+    padded[: tg.n_local] = local
+    full3 = tg.gather(padded)
     if rank == 0:
-        assert torch.equal(full, full2)
+        assert torch.equal(full, full2) and torch.equal(full, full3)
     total = torch.tensor([rays], dtype=torch.int64)
     dist.all_reduce(total)  # the ray count's one all_reduce
     if rank == 0:

@@ -11,9 +11,7 @@ step() {
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
     return 0
 }
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step gpu_tests 900 python -u -m pytest tests/ -x -v -m gpu --timeout 300 --timeout-method thread -k "not full_resolution"
-step parity 300 python tools/parity_record.py --scenes 5,9 --out gpurun_out/parity_s1.json
-step bench 600 python bench.py --steps 20 --warmup 5
-step prof 900 bash tools/profile.sh
+step gpu_tests 900 python -u -m pytest tests/ -x -v -m gpu --timeout 300 --timeout-method thread
+step parity 300 python tools/parity_record.py --scenes 5,9,8,7 --out gpurun_out/parity_s2.json
+LIBS="lockstep nomtree" step ab 900 bash tools/ab_walk.sh
 exit 0
