@@ -104,6 +104,7 @@ mrt_status mrt_cpu_scene_create(const mrt_scene_view* v, mrt_cpu_scene** out) {
     S.children = c->children.data();
     S.mnodes = c->mnodes.data();
     S.mwide = T.wide.data();
+    S.mwide_n = (uint32_t)T.wide.size();
     S.bwide = T.bwide.data();
     S.bprims = T.bprims.data();
     S.tri_geo = c->tri_geo.data();

@@ -120,12 +120,23 @@ MRT_DFN float sdot(f3 a) { return (a.x * a.x + a.y * a.y) + a.z * a.z; }
 // sphere::hit's quadratic (sphere.cpp:20-26): b = dot(oc, d), c = |oc|^2 - r^2, disc = b*b - c.
 // Never FMA-contracted, also in the tolerance-contract build (the CPU restatement built with
 // contraction loses 0.08% of book2's rays through this quadratic; DESIGN.md "Numerics contracts").
+#ifndef MRT_FAST_DISC_FMA
+#define MRT_FAST_DISC_FMA 0
+#endif
 MRT_DFN float sphere_disc(f3 oc, f3 d, float radius, float* bout) {
 #pragma clang fp contract(off)
     const float b = (oc.x * d.x + oc.y * d.y) + oc.z * d.z;
-    const float c = ((oc.x * oc.x + oc.y * oc.y) + oc.z * oc.z) - radius * radius;
+    const float s = (oc.x * oc.x + oc.y * oc.y) + oc.z * oc.z;
     *bout = b;
+#if MRT_FAST && MRT_FAST_DISC_FMA
+    // as clang contracts the reference's scalar tail (x86 -ffp-contract=on; the dot products are
+    // SSE intrinsics and stay unfused): c = fnmadd(r, r, s), disc = fmsub(b, b, c)
+    const float c = __builtin_fmaf(-radius, radius, s);
+    return __builtin_fmaf(b, b, -c);
+#else
+    const float c = s - radius * radius;
     return b * b - c;
+#endif
 }
 // ---- exact f32 division on a short path (tools/numcheck/markstein_check.hip) ----------------------
 // IEEE a/b compiles to 11 VALU (div_scale x2, rcp, 6 fma, div_fmas, div_fixup).  With y = RN(1/b)
@@ -166,7 +177,7 @@ MRT_DFN bool any_lane(bool p) {
 MRT_DFN uint32_t mag2(float x) { return __float_as_uint(x) << 1; }
 #define MRT_MAG2(e) ((uint32_t)((e) + 127) << 24)
 // |x| in [2^lo, 2^hi)
-#define MRT_MAG_IN(x, lo, hi) ((mag2(x) - MRT_MAG2(lo)) < (MRT_MAG2(hi) - MRT_MAG2(lo)))
+#define MRT_MAG_IN(x, lo, hi) ((uint32_t)((mag2(x) - MRT_MAG2(lo)) < (MRT_MAG2(hi) - MRT_MAG2(lo))))
 // Correctly rounded f32 square root.  hipcc's expansion is v_sqrt_f32, a one-ulp neighbour test
 // by fma residuals, and a 2^32 scaling of inputs below 2^-96 (+ zero/inf fix-up); the core alone
 // equals it for every input with |x| >= 2^-96 or x == +-0 (all 2^32 patterns checked on MI355X,
@@ -228,7 +239,14 @@ MRT_DFN void sincos_(float x, float* s, float* c) {
     *s = __builtin_amdgcn_sinf(rev);
     *c = __builtin_amdgcn_cosf(rev);
 }
+#ifndef MRT_FAST_LOG_LIB
+#define MRT_FAST_LOG_LIB 0
+#endif
+#if MRT_FAST_LOG_LIB
+MRT_DFN float log_(float x) { return logf(x); }  // ocml f32 log (v_log_f32 loses relative accuracy near 1)
+#else
 MRT_DFN float log_(float x) { return __builtin_amdgcn_logf(x) * 0.69314718055994531f; }
+#endif
 MRT_DFN float pow5_(float x) {
     const float x2 = x * x;
     return (x2 * x2) * x;

@@ -48,9 +48,13 @@ using namespace mrtd;
 #ifndef MRT_WPE_MESH
 #define MRT_WPE_MESH 7
 #endif
+#ifndef MRT_WPE_LIN_GEN
+#define MRT_WPE_LIN_GEN MRT_WPE_LIN  // the interpreter's compact variants (no program shape)
+#endif
 template <uint32_t F> struct PathOcc {
     static constexpr bool kWide = (F & (FT_BVHW | FT_TEX | FT_VOLUME)) != 0 || !(F & FT_LIN);
-    static constexpr int W = kWide ? MRT_WPE_WIDE : ((F & FT_MESH) != 0 ? MRT_WPE_MESH : MRT_WPE_LIN);
+    static constexpr int W = kWide ? MRT_WPE_WIDE
+                             : ((F & FT_MESH) != 0 ? MRT_WPE_MESH : (MRT_SIG_OF(F) != SIG_NONE ? MRT_WPE_LIN : MRT_WPE_LIN_GEN));
 };
 #if defined(MRT_EXPERIMENTS) && defined(MRT_PHASES)  // build ONE of the two TUs with it
 __device__ unsigned long long g_phases[12];

@@ -804,7 +804,15 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     UP(T.nodes.data(), T.nodes.size(), &S.nodes);
     UP(v->children, v->n_children, &S.children);
     UP(v->mesh_nodes, v->n_mesh_nodes, &S.mnodes);
+#if MRT_MESH_SOA  // layout experiment (mrt_trace.h mesh_wide): four 16-B planes
+    std::vector<float4> msoa(T.wide.size() * 4);
+    for (size_t i = 0; i < T.wide.size(); i++)
+        for (size_t k = 0; k < 4; k++) memcpy(&msoa[k * T.wide.size() + i], reinterpret_cast<const char*>(&T.wide[i]) + 16 * k, 16);
+    UP(msoa.data(), msoa.size(), (const float4**)&S.mwide);
+#else
     UP(T.wide.data(), T.wide.size(), &S.mwide);
+#endif
+    S.mwide_n = (uint32_t)T.wide.size();
     UP(T.bwide.data(), T.bwide.size(), &S.bwide);
     UP(T.bprims.data(), T.bprims.size(), &S.bprims);
     UP((const float4*)v->tri_geo, (size_t)v->n_tris * 3, &S.tri_geo);
@@ -844,6 +852,8 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     s->lds_save = (lin_kernel && (kVariants[s->variant] & (FT_INST | (MRT_RESUME_LIN ? FT_BVHW : 0u)))) ? 15u : 0u;
     // resumable mesh walk: deeper pod_bvh trees keep the wave walking longer
     s->walk_min = T.wide.size() >= 2048 ? 40u : 32u;  // inner nodes: bunny 2937, teapot ~1045
+    if (const char* e = getenv("MRT_WALK_MIN"))  // sweep hook (tools/ab_walk.sh)
+        if (*e) s->walk_min = (uint32_t)atoi(e);
     const std::vector<BvhWide>& bwide = T.bwide;
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));

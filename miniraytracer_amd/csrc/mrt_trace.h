@@ -131,7 +131,8 @@ struct DScene {
     const mrt_node* __restrict__ nodes;
     const uint32_t* __restrict__ children;
     const mrt_mesh_node* __restrict__ mnodes;
-    const MeshWide* __restrict__ mwide;
+    const MeshWide* __restrict__ mwide;   // (MRT_MESH_SOA device upload: four float4 planes of mwide_n nodes each)
+    uint32_t mwide_n;
     const BvhWide* __restrict__ bwide;
     const mrt_node* __restrict__ bprims;  // leaf primitive runs of the wide subtrees
     const float4* __restrict__ tri_geo;
@@ -214,7 +215,7 @@ struct TreeOf {
 #define MRT_MESH_TREE_MAX 63u
 #endif
 #ifndef MRT_MESH_TREE
-#define MRT_MESH_TREE 1
+#define MRT_MESH_TREE 0  // measured: bunny -2.6%, teapot -4.6%; kept as an option
 #endif
 template <uint32_t F>
 struct MeshTreeOf {
@@ -236,6 +237,37 @@ template <uint32_t F>
 MRT_DFN bool is_prim(uint32_t kind) {
     return kind == MRT_K_SPHERE || kind == MRT_K_XY || kind == MRT_K_XZ || kind == MRT_K_YZ || ((F & FT_MESH) && kind == MRT_K_MESH) ||
            ((F & FT_BVHW) && kind == MRT_K_BVHW);
+}
+
+// Layout experiment (north star: "BVH node array ... flattened to SoA in HBM"): with MRT_MESH_SOA
+// the device copy of the mesh wide nodes is four planes -- piece k (16 B: a child's min + ref,
+// max + ref, ...) of node i at plane k, index i -- instead of one 64-B record per node.  A visit
+// then reads four lines, one per plane, instead of one; A/B in DESIGN.md (N3).
+#ifndef MRT_MESH_SOA
+#define MRT_MESH_SOA 0
+#endif
+template <bool TREE>
+MRT_DFN WideNode mesh_wide(const DScene& S, uint32_t ref, const LStack& L) {
+#if MRT_MESH_SOA && defined(__HIP_DEVICE_COMPILE__)
+    (void)L;
+    const float4* b = reinterpret_cast<const float4*>(S.mwide);
+    const size_t n = S.mwide_n;
+    float4 a = b[ref], c1 = b[n + ref], c2 = b[2 * n + ref], d = b[3 * n + ref];
+    asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(a.z), "+v"(a.w), "+v"(c1.x), "+v"(c1.y), "+v"(c1.z), "+v"(c1.w));
+    asm volatile("" : "+v"(c2.x), "+v"(c2.y), "+v"(c2.z), "+v"(c2.w), "+v"(d.x), "+v"(d.y), "+v"(d.z), "+v"(d.w));
+    WideNode w;
+    w.lmin = f3{a.x, a.y, a.z};
+    w.lref = __float_as_uint(a.w);
+    w.lmax = f3{c1.x, c1.y, c1.z};
+    w.rref = __float_as_uint(c1.w);
+    w.rmin = f3{c2.x, c2.y, c2.z};
+    w.order = __float_as_uint(c2.w);
+    w.rmax = f3{d.x, d.y, d.z};
+    w.flags = __float_as_uint(d.w);
+    return w;
+#else
+    return wide_at<TREE>(S.mwide, ref, L);
+#endif
 }
 
 // get_sphere_uv (sphere.cpp:6-11)
@@ -412,7 +444,7 @@ MRT_DFN bool mesh_hit(const DScene& S, const mrt_node& n, const Ray& r, float tm
     // on the teapot (C3) than the one-step-per-iteration walk below, so kept as an experiment.
     for (;;) {
         while (!(ref & MESH_LEAF)) {
-            const WideNode W = wide_at<false>(S.mwide, ref, L);
+            const WideNode W = mesh_wide<false>(S, ref, L);
             const bool hl = aabb_hit(W.lmin, W.lmax, r, tmin, tmax);
             const bool hr = aabb_hit(W.rmin, W.rmax, r, tmin, tmax);
             const bool left_first = (W.order & r.mask) != 0;
@@ -437,7 +469,7 @@ MRT_DFN bool mesh_hit(const DScene& S, const mrt_node& n, const Ray& r, float tm
         if (ref & MESH_LEAF) {
             if (mesh_leaf(S, ref, n, r, tmin, tmax, rec, full)) return true;
         } else {
-            const WideNode W = wide_at<false>(S.mwide, ref, L);
+            const WideNode W = mesh_wide<false>(S, ref, L);
             const bool hl = aabb_hit(W.lmin, W.lmax, r, tmin, tmax);
             const bool hr = aabb_hit(W.rmin, W.rmax, r, tmin, tmax);
             const bool left_first = (W.order & r.mask) != 0;
@@ -495,7 +527,7 @@ MRT_DFN uint32_t mesh_step(const DScene& S, const mrt_node& n, const Ray& r, flo
             return 1u;
         }
     } else {
-        const WideNode W = wide_at<TREE>(S.mwide, ref, L);
+        const WideNode W = mesh_wide<TREE>(S, ref, L);
         const bool hl = aabb_hit(W.lmin, W.lmax, r, tmin, tt);
         const bool hr = aabb_hit(W.rmin, W.rmax, r, tmin, tt);
         const bool left_first = (W.order & r.mask) != 0;
