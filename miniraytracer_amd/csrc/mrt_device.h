@@ -375,11 +375,15 @@ MRT_DFN Ray make_ray(f3 o, f3 dir, float time, int inside) {
 // A ray whose direction argument is already of unit length up to rounding (a ray's normalized
 // direction, rotated or reused): the exact contract runs the constructor as the reference does;
 // the tolerance contract skips the renormalization (a change of at most an ulp or two).
+// U: skip it (the tolerance contract's kernels without bvh_node subtrees, textures or volumes --
+// kFastUnit<F>, mrt_trace.h; measured on book2 at 2048^2 x 1024 spp: renormalising keeps its
+// per-pixel RMSE vs the reference as shipped at 2.1e-3 instead of 1.2e-2, DESIGN.md "Numerics")
 #ifndef MRT_FAST_UNIT
 #define MRT_FAST_UNIT MRT_FAST
 #endif
+template <bool U = MRT_FAST_UNIT>
 MRT_DFN Ray make_ray_unit(f3 o, f3 dir, float time, int inside) {
-#if MRT_FAST_UNIT
+    if constexpr (!U) return make_ray(o, dir, time, inside);
     Ray r;
     r.o = o;
     r.d = dir;
@@ -390,21 +394,16 @@ MRT_DFN Ray make_ray_unit(f3 o, f3 dir, float time, int inside) {
     r.nice = ray_nice(r.o, r.d);
     r.inv = ray_inv(r.d, r.nice);
     return r;
-#else
-    return make_ray(o, dir, time, inside);
-#endif
 }
 // translate::hit's moved ray (scene_object.cpp:11): the same direction, a new origin
+template <bool U = MRT_FAST_UNIT>
 MRT_DFN Ray moved_ray(const Ray& r0, f3 o) {
-#if MRT_FAST_UNIT
+    if constexpr (!U) return make_ray(o, r0.d, r0.time, 0);
     Ray r = r0;  // direction, its reciprocal and mask reused as they are
     r.o = o;
     r.inside = 0;
     r.nice = ray_nice(r.o, r.d);
     return r;
-#else
-    return make_ray(o, r0.d, r0.time, 0);
-#endif
 }
 MRT_DFN f3 eval(const Ray& r, float t) { return add(r.o, fmul(t, r.d)); }
 

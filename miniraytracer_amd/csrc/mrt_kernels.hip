@@ -49,7 +49,7 @@ using namespace mrtd;
 #define MRT_WPE_MESH 7
 #endif
 #ifndef MRT_WPE_LIN_GEN
-#define MRT_WPE_LIN_GEN MRT_WPE_LIN  // the interpreter's compact variants (no program shape)
+#define MRT_WPE_LIN_GEN 6  // the interpreter's compact variants (no program shape): 6 waves (80 VGPRs) +9% over 7 on C2
 #endif
 template <uint32_t F> struct PathOcc {
     static constexpr bool kWide = (F & (FT_BVHW | FT_TEX | FT_VOLUME)) != 0 || !(F & FT_LIN);
@@ -337,7 +337,10 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
     };
     // mesh variants keep one constructor per branch: the shared-constructor loop spills there
     // (bunny -4%, teapot -5%; Cornell +1.8%, book2 0)
-    constexpr bool kShared = (F & FT_MESH) == 0;
+#ifndef MRT_SHARED_WIDE
+#define MRT_SHARED_WIDE 1  // the wide (bvh_node) variants too
+#endif
+    constexpr bool kShared = (F & FT_MESH) == 0 && (MRT_SHARED_WIDE || !PathOcc<F>::kWide);
     constexpr bool kResume = MRT_SIG_OF(F) == SIG_ROOM_MESH;
     if constexpr (kResumeLin<F>) {
         // Linear hit programs with bvh_node subtrees (random spheres, book2): the intersection is

@@ -61,10 +61,11 @@ typedef void (*path_kernel_t)(PathParams);
 static_assert(MRT_TAIL_BATCH >= 64u && MRT_BATCH >= MRT_TAIL_BATCH, "claims must be at least a wave wide");
 
 // Linear programs with bvh_node subtrees run the resumable interpreter (mrt_resume.h); its query ray
-// lives in the LDS save area (15 words per lane slot, as instances need) -- MRT_RESUME_LIN=0 builds
-// the lockstep interpreter instead (A/B)
+// lives in the LDS save area (15 words per lane slot, as instances need).  Measured SLOWER than the
+// lockstep interpreter (book2 3.77 vs 4.64, random spheres 5.82 vs 6.02 Grays/s), so
+// off by default: MRT_RESUME_LIN=1 builds it (A/B)
 #ifndef MRT_RESUME_LIN
-#define MRT_RESUME_LIN 1
+#define MRT_RESUME_LIN 0
 #endif
 template <uint32_t F>
 static constexpr bool kResumeLin = MRT_RESUME_LIN && (F & FT_LIN) != 0 && (F & FT_BVHW) != 0 && MRT_SIG_OF(F) == SIG_NONE;

@@ -358,7 +358,7 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
             bool in = on;
             const Ray r0 = lin_load_ray(L);
             if (kind == MRT_K_TRROTY) {  // translate::hit then rotate_y::hit (scene_object.cpp:9-18, 70-98)
-                cur = moved_ray(r0, sub(r0.o, f3{o.f[8], o.f[9], o.f[10]}));
+                cur = moved_ray<kFastUnit<F>>(r0, sub(r0.o, f3{o.f[8], o.f[9], o.f[10]}));
                 if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, cur, tmin, closest);
             } else if (kind == MRT_K_ROTY) {
                 cur = r0;
@@ -371,8 +371,8 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
                 pc = o.skip - 1;
                 continue;
             }
-            if (kind == MRT_K_TRROTY || kind == MRT_K_ROTY) cur = rotate_ray(cur, o.f[6], o.f[7]);
-            else cur = moved_ray(r0, sub(r0.o, f3{o.f[0], o.f[1], o.f[2]}));
+            if (kind == MRT_K_TRROTY || kind == MRT_K_ROTY) cur = rotate_ray<kFastUnit<F>>(cur, o.f[6], o.f[7]);
+            else cur = moved_ray<kFastUnit<F>>(r0, sub(r0.o, f3{o.f[0], o.f[1], o.f[2]}));
         } else if (INST && op == LOP_INST_END) {
             if (hinst == inst) {  // keep the instance-frame ray of the hit for the record
                 float* b = L.save + L.lane + 9 * 64;

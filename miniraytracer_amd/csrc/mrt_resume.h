@@ -200,13 +200,13 @@ MRT_DFN void rs_sweep(const DScene& S, ResumeState& w, HitRec& rec, const LStack
             const Ray r0 = lin_load_ray(L);
             Ray c = r0;
             if (kind == MRT_K_TRROTY) {  // translate::hit then rotate_y::hit (scene_object.cpp:9-18, 70-98)
-                c = moved_ray(r0, sub(r0.o, f3{o.f[8], o.f[9], o.f[10]}));
+                c = moved_ray<kFastUnit<F>>(r0, sub(r0.o, f3{o.f[8], o.f[9], o.f[10]}));
                 if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, c, tmin, w.closest);
             } else if (kind == MRT_K_ROTY) {
                 if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, c, tmin, w.closest);
             }
-            if (kind == MRT_K_TRROTY || kind == MRT_K_ROTY) c = rotate_ray(c, o.f[6], o.f[7]);
-            else c = moved_ray(r0, sub(r0.o, f3{o.f[0], o.f[1], o.f[2]}));
+            if (kind == MRT_K_TRROTY || kind == MRT_K_ROTY) c = rotate_ray<kFastUnit<F>>(c, o.f[6], o.f[7]);
+            else c = moved_ray<kFastUnit<F>>(r0, sub(r0.o, f3{o.f[0], o.f[1], o.f[2]}));
             if (here) {
                 w.act = (w.act & ~(2u << lvl)) | ((uint32_t)in << (lvl + 1u));
                 if (in) w.cur = c;

@@ -105,7 +105,7 @@ MRT_DFN float leaf_pdf_value(const DScene& S, const mrt_node& n, f3 origin, f3 d
     uint32_t k = MRT_NODE_KIND(n);
     HitRec rec;
     if (k == MRT_K_XZ) {  // xz_rect::pdf_value (rect.cpp:92-102), the hit test branch-free
-        const Ray r = make_ray_unit(origin, dir, 0.0f, 0);  // dir: the scattered ray's unit direction
+        const Ray r = make_ray_unit<kFastUnit<F>>(origin, dir, 0.0f, 0);  // dir: the scattered ray's unit direction
         float t;
         const bool h = lin_prim_t<F, MRT_K_XZ>(n, r, 0.001f, FLT_MAX_, &t);
         const float area = (n.f[1] - n.f[0]) * (n.f[3] - n.f[2]);
@@ -115,7 +115,7 @@ MRT_DFN float leaf_pdf_value(const DScene& S, const mrt_node& n, f3 origin, f3 d
         return h ? pdf : 0.0f;
     }
     if ((F & FT_BSPHERE) && k == MRT_K_SPHERE) {
-        Ray r = make_ray_unit(origin, dir, time, 0);
+        Ray r = make_ray_unit<kFastUnit<F>>(origin, dir, time, 0);
         if (sphere_hit<F>(n, r, 0.001f, FLT_MAX_, rec, false)) {
             float radius = n.f[8];
             float cos_theta_max = sqrt_(1 - (radius * radius) / sdot(sub(sphere_center<F>(n, time), origin)));

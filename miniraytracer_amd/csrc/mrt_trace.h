@@ -233,6 +233,11 @@ MRT_DFN WideNode wide_at(const W* base, uint32_t ref, const LStack& L) {
     }
 }
 
+// the tolerance contract's unit-direction shortcut (make_ray_unit) per kernel variant: not for
+// scenes with bvh_node subtrees, textures or volumes (book2's numerics are too sensitive to it)
+template <uint32_t F>
+static constexpr bool kFastUnit = MRT_FAST_UNIT && (F & (FT_BVHW | FT_TEX | FT_VOLUME)) == 0;
+
 template <uint32_t F>
 MRT_DFN bool is_prim(uint32_t kind) {
     return kind == MRT_K_SPHERE || kind == MRT_K_XY || kind == MRT_K_XZ || kind == MRT_K_YZ || ((F & FT_MESH) && kind == MRT_K_MESH) ||
@@ -731,13 +736,14 @@ MRT_DFN void pop_ray(const LStack& L, uint32_t slot, Ray& r) {
 }
 
 // rotate_y::hit ray transform (scene_object.cpp:75-82)
+template <bool U = MRT_FAST_UNIT>
 MRT_DFN Ray rotate_ray(const Ray& ray, float s, float c) {
     f3 o = ray.o, d = ray.d;
     o.x = c * ray.o.x - s * ray.o.z;
     o.z = c * ray.o.z + s * ray.o.x;
     d.x = c * ray.d.x - s * ray.d.z;
     d.z = c * ray.d.z + s * ray.d.x;
-    return make_ray_unit(o, d, ray.time, 0);
+    return make_ray_unit<U>(o, d, ray.time, 0);
 }
 // ... and the record back (scene_object.cpp:85-93)
 MRT_DFN void unrotate_rec(HitRec& rec, float s, float c) {
@@ -821,13 +827,13 @@ MRT_DFN bool scene_hit(const DScene& S, Ray ray, float tmin0, HitRec& rec, Pcg& 
         } else if ((F & FT_INST) && kind == MRT_K_TRROTY) {  // translate(rotate_y(x)) fused
             const float s = N.f[6], c = N.f[7];
             if (st == ST_ENTER) {
-                Ray moved = moved_ray(ray, sub(ray.o, ld3(N.f + 8)));  // translate::hit
+                Ray moved = moved_ray<kFastUnit<F>>(ray, sub(ray.o, ld3(N.f + 8)));  // translate::hit
                 if ((MRT_NODE_FLAGS(N) & MRT_F_HASBOX) && !aabb_hit(N.f, N.f + 3, moved, tmin, closest)) {
                     ret = false;
                     pop = true;
                 } else {
                     push_ray(L, rsp++, ray);
-                    ray = rotate_ray(moved, s, c);
+                    ray = rotate_ray<kFastUnit<F>>(moved, s, c);
                     req = N.a;
                     tstate = ST_PH1;
                 }
@@ -847,7 +853,7 @@ MRT_DFN bool scene_hit(const DScene& S, Ray ray, float tmin0, HitRec& rec, Pcg& 
                     pop = true;
                 } else {
                     push_ray(L, rsp++, ray);
-                    ray = roty ? rotate_ray(ray, N.f[6], N.f[7]) : moved_ray(ray, sub(ray.o, ld3(N.f)));
+                    ray = roty ? rotate_ray<kFastUnit<F>>(ray, N.f[6], N.f[7]) : moved_ray<kFastUnit<F>>(ray, sub(ray.o, ld3(N.f)));
                     req = N.a;
                     tstate = ST_PH1;
                 }

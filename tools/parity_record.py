@@ -26,6 +26,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "parity.json"))
     ap.add_argument("--scenes", default="5,9,8,7")
+    ap.add_argument("--numerics", default="exact,fast")
     a = ap.parse_args()
     import miniraytracer_amd as m
     from fixture_cmp import GOLDEN, compare
@@ -35,7 +36,7 @@ def main():
         g = np.load(path)
         _, w, h, spp, depth = (int(x) for x in g["meta"])
         r = m.Renderer(m.select_scene(sid, w / h), device=0)
-        for numerics in ("exact", "fast"):
+        for numerics in a.numerics.split(","):
             t0 = time.perf_counter()
             img, rays = r.render(m.render_desc(w, h, spp, depth=depth, numerics=numerics))
             dt = time.perf_counter() - t0
