@@ -192,9 +192,8 @@ static void render_tiles(mrt_cpu_scene* c, const mrt_render_desc* d, const std::
                     ps.r = camera_ray(S, ps.rng, u, v);
                     ps.depth = 0;
                     ps.nlev = 0;
-                    ps.rays = 0;
                     const f3 L = trace_path<F>(S, ps, d->max_bounces, lev, Ls);
-                    my_rays += ps.rays;
+                    my_rays += ps.rays();
                     col = fold_sample(col, L, s, d->mode, d->max_luminance);
                 }
                 col = final_pixel(col, ns, d->mode, d->max_luminance);
@@ -242,10 +241,9 @@ static void render_ref_order(mrt_cpu_scene* c, const mrt_render_desc* d, const s
         ps.r = camera_ray(S, ps.rng, u, v);
         ps.depth = 0;
         ps.nlev = 0;
-        ps.rays = 0;
         const f3 L = trace_path<F>(S, ps, d->max_bounces, lev, Ls);
         rng = ps.rng;
-        my_rays += ps.rays;
+        my_rays += ps.rays();
         return L;
     };
     std::vector<float> tb;

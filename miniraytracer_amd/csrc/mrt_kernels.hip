@@ -295,7 +295,6 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
 #if MRT_FWD_FOLD
         ps.T = f3{1.0f, 1.0f, 1.0f};
 #endif
-        ps.rays = 0;
         active = true;
     };
     // Lanes without a path take the next path indices from the wave's pool (ballot + mbcnt
@@ -331,8 +330,8 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
 #if defined(MRT_EXPERIMENTS) && defined(MRT_EXP_NOSTORE)
         }
 #endif
-        if (P.path_rays) P.path_rays[idx] = ps.rays;
-        done_rays += ps.rays;
+        if (P.path_rays) P.path_rays[idx] = ps.rays();
+        done_rays += ps.rays();
         active = false;
     };
     // mesh variants keep one constructor per branch: the shared-constructor loop spills there
@@ -371,7 +370,6 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
             rs_sweep<F>(S, w, rec, Ls, ps.rng, 0.001f);
             PH_MARK(ph, 1);
             if (w.st == RS_DONE) {
-                ps.rays++;  // one trace() call (main.cpp:68)
                 const bool hit = rs_finish_hit<F>(S, w, ps.r, rec, Ls);
                 f3 L;
                 const bool ended = shade_hit<F, LK>(S, ps, P.max_bounces, lev, hit, rec, &L, ph);
@@ -421,8 +419,8 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                     st_v = end_path(ps, lev, L);
                     st_off = idx * 12u;
                     st_pend = true;
-                    if (P.path_rays) P.path_rays[idx] = ps.rays;
-                    done_rays += ps.rays;
+                    if (P.path_rays) P.path_rays[idx] = ps.rays();
+                    done_rays += ps.rays();
                     active = false;
                 } else {
                     want_ray = true;
@@ -544,7 +542,6 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
             if (!__any(active)) break;
             PH_MARK(ph, 0);
             if (phase == PH_BEGIN) {  // the room's walls (scene_hit_sig's ops 0..6), then the mesh root box
-                ps.rays++;
                 w.cur = ps.r;
                 w.closest = FLT_MAX_;
                 w.hnode = MRT_NONE;

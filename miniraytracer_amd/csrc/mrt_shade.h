@@ -192,7 +192,9 @@ struct PathState {
     Pcg rng;
     uint32_t depth;  // bounces so far (trace depth)
     uint32_t nlev;   // stored fold levels | LEV_LOUD once a level could turn a black result non-zero
-    uint32_t rays;   // trace() calls of this path
+    // trace() calls of a finished path: every segment but the last scatters (depth++), so the count
+    // is depth + 1 -- derived, not kept in a register of its own across the path loop
+    MRT_DFN uint32_t rays() const { return depth + 1u; }
 #if MRT_FWD_FOLD
     f3 T;            // throughput of the bounces so far (forward fold)
 #endif
@@ -409,7 +411,6 @@ MRT_DFN bool shade_hit(const DScene& S, PathState& ps, uint32_t max_bounces, con
 template <uint32_t F, uint32_t LK>
 MRT_DFN bool trace_segment(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev,
                                               const LStack& Ls, f3* L, PhaseClock& ph) {
-    ps.rays++;
     HitRec rec;
     bool hit;
     if constexpr (MRT_SIG_OF(F) != SIG_NONE) hit = scene_hit_sig<F>(S, ps.r, 0.001f, rec, Ls);
@@ -437,7 +438,6 @@ struct PendRay {
 template <uint32_t F, uint32_t LK, typename FLUSH>
 MRT_DFN bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev,
                                             const LStack& Ls, f3* L, PendRay* pr, PhaseClock& ph, FLUSH&& flush) {
-    ps.rays++;
     HitRec rec;
     Ray& r = ps.r;
     bool hit;

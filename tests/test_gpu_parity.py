@@ -337,10 +337,14 @@ def test_full_c2_within_tolerance_of_shipped_reference(gpu, numerics):
 # Full-resolution fixtures of C3 / C4 / C5 (tools/make_golden.py FULLRES: the reference as shipped,
 # stream-matched, 1024 spp at the configs' own resolution).  Per-pixel RMSE over a band of rows and
 # a seeded sample of pixels (tests/fixture_cmp.py), 32x32-grid block means, channel means, rays.
-# Bars: per-pixel RMSE < 1e-3 (the north-star bar, at 1024 spp as for C2) -- except where stated;
-# measured values in profiles/r03_parity.json (tools/parity_record.py).
+# Bars: per-pixel RMSE < 1e-3 (the north-star bar, at 1024 spp as for C2) for C3 and C4.  C5 (book2:
+# 1000 spheres, fog everywhere) is chaotic under ANY rounding change: the reference built exact --
+# which the exact contract reproduces bit for bit -- differs from the reference as shipped by 2.68e-3
+# per pixel at this config, so the bar there is 1.3x that build-to-build difference (3.5e-3), stated
+# here.  Block means (SURVEY 8(d) parity 3: 25x25-pixel-class block means within 1e-3), channel
+# means within 1e-4, rays within 0.5% (parity 4) everywhere.  Measured values: profiles/r03_parity.json.
 FULL_RMSE = {(9, "exact"): 1e-3, (9, "fast"): 1e-3, (8, "exact"): 1e-3, (8, "fast"): 1e-3,
-             (7, "exact"): 1e-3, (7, "fast"): 1e-3}
+             (7, "exact"): 3.5e-3, (7, "fast"): 3.5e-3}
 FULL_RAYS = {"exact": 1e-3, "fast": 5e-3}
 
 
@@ -358,7 +362,7 @@ def test_full_resolution_within_tolerance_of_shipped_reference(gpu, sid, numeric
     c = compare(img, rays, path)
     print(c)
     assert c["rmse"] < FULL_RMSE[(sid, numerics)], c
-    assert c["block_rmse"] < 1e-4, c
+    assert c["block_rmse"] < 1e-3, c
     assert c["mean_delta"] < 1e-4, c
     assert abs(c["ray_ratio"] - 1) < FULL_RAYS[numerics], c
 
