@@ -236,12 +236,8 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
         const float2 dd = P.sdist[s];  // ((i + 0.5) / sq, (j + 0.5) / sq), s = i*sq + j
         // (x + dx) / W with RN(1/W) from the host: numerator >= 1/(2 sq) >= 2^-17, W <= 2^24
         const float nu = (float)x + dd.x, nv = (float)y + dd.y;
-        float u = div_core(nu, (float)P.width, P.inv_w), v = div_core(nv, (float)P.height, P.inv_h);
-        if (!P.fast_uv) {  // a real (uniform) branch: the barrier keeps it from being if-converted
-            asm volatile("" ::: "memory");
-            u = nu / (float)P.width;
-            v = nv / (float)P.height;
-        }
+        // exact for every image the host accepts (width, height <= 2^24, mrt_prepare)
+        const float u = div_core(nu, (float)P.width, P.inv_w), v = div_core(nv, (float)P.height, P.inv_h);
         const uint64_t path_id = (uint64_t)pix * P.ns + s;
         pcg_seed(rng, splitmix64(P.seed ^ path_id), path_id);
         *uo = u;

@@ -52,9 +52,29 @@ static uint32_t pick_variant(uint32_t features) {
 // few pixels are local (multi-GPU shards): samples are fetched FOLD_DEPTH at a time (coalesced
 // across the wave's pixels) before the dependent adds.
 #define FOLD_DEPTH 16
+// The render's last chunk (out != null) also finishes the pixels -- final_pixel into the caller's
+// output -- and resets the counters (FoldEnd), so no separate final kernel follows it.
+struct FoldEnd {
+    float4* out;                     // the render's output (last chunk), or null: keep folding into acc
+    uint32_t ns;                     // samples per pixel (mode 0 divides by it)
+    unsigned long long* counters;    // work counters of the render's launches (MRT_COUNTER_STRIDE apart)
+    unsigned long long* hprog;       // their progress snapshots in host memory (or null)
+    uint32_t nreset;                 // how many of each
+};
+// what the render's path kernels consumed, reset for the context's next render in stream order
+// after them: the work counters (word (k * MRT_NPART + part) * MRT_COUNTER_STRIDE) and the
+// progress snapshots -- instead of clearing fills enqueued before each render (a blit kernel
+// needs a free wave slot, which the other pipelined contexts' persistent path kernels hold)
+MRT_DFN void reset_counters(const FoldEnd& e, uint32_t i) {
+    if (i < e.nreset) {
+        e.counters[(size_t)i * MRT_COUNTER_STRIDE] = 0ull;
+        if (e.hprog) __hip_atomic_store(e.hprog + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
 __global__ void __launch_bounds__(256) mrt_fold_kernel(const float* __restrict__ rad, float4* __restrict__ acc, uint32_t npix, uint32_t s0,
-                                                      uint32_t s1, uint32_t mode, float max_lum) {
+                                                      uint32_t s1, uint32_t mode, float max_lum, FoldEnd fe) {
     uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
+    reset_counters(fe, lp);
     if (lp >= npix) return;
     // a render's first chunk starts from +0 without reading acc (no per-render clearing fill:
     // folding +0 first gives the same bits as starting from a zeroed accumulator)
@@ -80,7 +100,12 @@ __global__ void __launch_bounds__(256) mrt_fold_kernel(const float* __restrict__
         const float* e = q + (size_t)(s - s0) * stride;
         c = fold_sample(c, f3{e[0], e[1], e[2]}, s, mode, max_lum);
     }
-    acc[lp] = make_float4(c.x, c.y, c.z, 0.0f);
+    if (fe.out) {
+        c = final_pixel(c, fe.ns, mode, max_lum);
+        fe.out[lp] = make_float4(c.x, c.y, c.z, 0.0f);
+    } else {
+        acc[lp] = make_float4(c.x, c.y, c.z, 0.0f);
+    }
 }
 
 // draw()'s fold (mode 0) in 8 VGPRs: the persistent path kernel fills 7 waves per SIMD with 72
@@ -121,18 +146,30 @@ mrt_fold_lean_kernel(const float* __restrict__ rad, float4* __restrict__ acc, ui
 // MRT_COUNTER_STRIDE) and their progress snapshots in host memory -- instead of clearing fills
 // enqueued before each render (a blit kernel needs a free wave slot, which the persistent path
 // kernels of the other pipelined contexts hold: up to 49 ms waits in the bench trace).
-__global__ void __launch_bounds__(256) mrt_final_kernel(const float4* __restrict__ acc, float4* __restrict__ out, uint32_t npix, uint32_t ns,
-                                                       uint32_t mode, float max_lum, unsigned long long* __restrict__ counters,
-                                                       unsigned long long* hprog, uint32_t nreset) {
-    uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
+// Lean like mrt_fold_lean_kernel (one-wave groups, 8 VGPRs): a 256-thread group of a 13-VGPR
+// kernel needs a wave slot on every SIMD, which the other pipelined contexts' persistent path
+// kernels (7 waves x 72 VGPRs per SIMD) do not leave free -- the final of one render then waited
+// for another render's path kernel to end, and the next render on its stream with it (the
+// bench's 3-context timeline, DESIGN.md "Pipelined renders").  Same operations, same bits.
+#ifndef MRT_FINAL_WG
+#define MRT_FINAL_WG 64
+#endif
+__global__ void __launch_bounds__(MRT_FINAL_WG) __attribute__((amdgpu_num_vgpr(8)))
+mrt_final_kernel(const float4* __restrict__ acc, float4* __restrict__ out, uint32_t npix, uint32_t ns, uint32_t mode, float max_lum,
+                 unsigned long long* __restrict__ counters, unsigned long long* hprog, uint32_t nreset) {
+    const uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
     if (lp < nreset) {
         counters[(size_t)lp * MRT_COUNTER_STRIDE] = 0ull;
         if (hprog) __hip_atomic_store(hprog + lp, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (lp >= npix) return;
-    float4 a = acc[lp];
-    const f3 c = final_pixel(f3{a.x, a.y, a.z}, ns, mode, max_lum);
-    out[lp] = make_float4(c.x, c.y, c.z, 0.0f);
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(acc), 0, 0xFFFFFFFFu, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(out, 0, 0xFFFFFFFFu, 0x00020000);
+    const auto a = __builtin_amdgcn_raw_buffer_load_b96(ra, lp * 16u, 0, 0);
+    const f3 c = final_pixel(f3{__uint_as_float(a[0]), __uint_as_float(a[1]), __uint_as_float(a[2])}, ns, mode, max_lum);
+    using u4 = decltype(__builtin_amdgcn_raw_buffer_load_b128(ra, 0u, 0, 0));
+    const u4 o = {__float_as_uint(c.x), __float_as_uint(c.y), __float_as_uint(c.z), 0u};
+    __builtin_amdgcn_raw_buffer_store_b128(o, ro, lp * 16u, 0, 0);
 }
 
 // Image output on the device (main.cpp:416-444): global max luminance, then per-pixel Drago +
@@ -983,6 +1020,9 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
     MRT_GPU_ONLY(s, "mrt_prepare");
     if (!s || !d || d->width == 0 || d->height == 0 || d->sqrt_samples == 0 || (d->world && d->rank >= d->world))
         return mrt_internal_fail(MRT_ERR_INVALID, "mrt_prepare: bad desc");
+    // the path kernel's u = (x + dx) / W by one reciprocal is exact up to 2^24 (mrt_kernels.hip)
+    if (d->width > (1u << 24) || d->height > (1u << 24))
+        return mrt_internal_fail(MRT_ERR_INVALID, "mrt_prepare: width / height above 2^24 pixels");
     HIPCHK(hipSetDevice(s->device));
     mrt_status st;
     bool relayout = !s->have_ws || !same_layout(s->wdesc, *d);
@@ -1135,7 +1175,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.height = d->height;
         P.inv_w = 1.0f / (float)d->width;
         P.inv_h = 1.0f / (float)d->height;
-        P.fast_uv = d->width <= (1u << 24) && d->height <= (1u << 24) && d->sqrt_samples <= (1u << 16);
+        P.fast_uv = 1;  // checked by mrt_prepare (and sq < 2^16 since sq^2 fits in 32 bits)
         P.sq = d->sqrt_samples;
         P.ns = ns;
         P.s0 = s0;
@@ -1164,15 +1204,23 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(s->ev[2 * s->n_launch + 1], q));
         s->n_launch++;
-        uint32_t blocks = (s->npix + 255) / 256;
-        if ((d->flags & MRT_RF_FOLD_BEHIND) && d->mode == 0)
+        // the last chunk's full fold finishes the render (no preview: no snapshot of acc needed;
+        // the 8-VGPR lean fold cannot take the division as well: a final kernel follows it)
+        const bool lean = (d->flags & MRT_RF_FOLD_BEHIND) && d->mode == 0;
+        const bool last = s1 == ns && !preview && !lean;
+        FoldEnd fe{last ? (float4*)d_local : nullptr, ns, last ? (unsigned long long*)s->d_counters : nullptr,
+                   last ? (unsigned long long*)s->h_prog : nullptr, last ? launches * MRT_NPART : 0u};
+        const uint32_t nthr = std::max(s->npix, fe.nreset);
+        if (lean)
             hipLaunchKernelGGL(mrt_fold_lean_kernel, dim3((s->npix + MRT_FOLD_LEAN_WG - 1) / MRT_FOLD_LEAN_WG), dim3(MRT_FOLD_LEAN_WG), 0, q,
                                s->d_rad, s->d_acc, s->npix, s1 - s0, (uint32_t)(s0 == 0));
         else
-            hipLaunchKernelGGL(mrt_fold_kernel, dim3(blocks), dim3(256), 0, q, s->d_rad, s->d_acc, s->npix, s0, s1, d->mode, d->max_luminance);
+            hipLaunchKernelGGL(mrt_fold_kernel, dim3((nthr + 255) / 256), dim3(256), 0, q, s->d_rad, s->d_acc, s->npix, s0, s1, d->mode,
+                               d->max_luminance, fe);
         HIPCHK(hipGetLastError());
         if (preview) {  // the image after s1 samples, copied under the sequence lock
-            hipLaunchKernelGGL(mrt_final_kernel, dim3(blocks), dim3(256), 0, q, s->d_acc, s->d_prev, s->npix, s1, d->mode, d->max_luminance,
+            hipLaunchKernelGGL(mrt_final_kernel, dim3((s->npix + MRT_FINAL_WG - 1) / MRT_FINAL_WG), dim3(MRT_FINAL_WG), 0, q, s->d_acc, s->d_prev,
+                               s->npix, s1, d->mode, d->max_luminance,
                                (unsigned long long*)nullptr, (unsigned long long*)nullptr, 0u);
             HIPCHK(hipGetLastError());
             HIPCHK(hipStreamWriteValue32(q, s->h_seq, 2 * seq + 1, 0));
@@ -1183,11 +1231,13 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         }
         s->last_paths = P.n_paths;
     }
-    const uint32_t nreset = launches * MRT_NPART;
-    const uint32_t blocks = (std::max(s->npix, nreset) + 255) / 256;
-    hipLaunchKernelGGL(mrt_final_kernel, dim3(blocks), dim3(256), 0, q, s->d_acc, (float4*)d_local, s->npix, ns, d->mode, d->max_luminance,
-                       (unsigned long long*)s->d_counters, (unsigned long long*)s->h_prog, nreset);
-    HIPCHK(hipGetLastError());
+    if (preview || ((d->flags & MRT_RF_FOLD_BEHIND) && d->mode == 0)) {  // (otherwise the last fold wrote the output and reset the counters)
+        const uint32_t nreset = launches * MRT_NPART;
+        const uint32_t blocks = (std::max(s->npix, nreset) + MRT_FINAL_WG - 1) / MRT_FINAL_WG;
+        hipLaunchKernelGGL(mrt_final_kernel, dim3(blocks), dim3(MRT_FINAL_WG), 0, q, s->d_acc, (float4*)d_local, s->npix, ns, d->mode,
+                           d->max_luminance, (unsigned long long*)s->d_counters, (unsigned long long*)s->h_prog, nreset);
+        HIPCHK(hipGetLastError());
+    }
     HIPCHK(hipEventRecord(s->ev_done, q));
     s->ev_done_pending = true;
     s->n_chunks.store(launches, std::memory_order_release);  // progress reads start once every launch and its events are enqueued

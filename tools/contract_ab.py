@@ -7,7 +7,9 @@ f32 transcendentals, forward fold), each priced by
   * VALU wave-instructions and active-lane instructions per ray (rocprofv3 SQ counters of the same
     workloads, profiles/<tag>_pmc.json from tools/profile.sh / tools/prof_configs.sh),
   * per-pixel RMSE and ray-count ratio against the reference AS SHIPPED on the same per-path streams
-    (tests/golden/shipped_stream_*.npz: C2 at full size, the others at fixture size).
+    (tests/golden: C2 shipped_stream_5.npz, the whole image; C3-C5 shipped_full_<id>.npz, full
+    resolution at 1024 spp, per-pixel RMSE over a band of rows + a seeded pixel sample,
+    tests/fixture_cmp.py).
 
   python tools/contract_ab.py --measure                   (GPU box) -> gpurun_out/contract_ab_measure.json
   python tools/contract_ab.py --summarize TAG [PMC ...]   -> profiles/TAG_contract_ab.json (+ table)"""
@@ -18,14 +20,15 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CASES = {"C2": (5, 500, 500, 1024), "C3": (9, 800, 800, 1024), "C4": (8, 1024, 1024, 256), "C5": (7, 2048, 2048, 256)}
-FIXTURE = {"C2": "shipped_stream_5.npz", "C3": "shipped_stream_9_small.npz", "C4": "shipped_stream_8_small.npz",
-           "C5": "shipped_stream_7_small.npz"}
+FIXTURE = {"C2": "shipped_stream_5.npz", "C3": "shipped_full_9.npz", "C4": "shipped_full_8.npz", "C5": "shipped_full_7.npz"}
 
 
 def measure():
     import numpy as np
     sys.path.insert(0, ROOT)
     import miniraytracer_amd as m
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from fixture_cmp import compare
     out = {}
     for name, (sid, w, h, spp) in CASES.items():
         r = m.Renderer(m.select_scene(sid, w / h), 0)
@@ -42,10 +45,10 @@ def measure():
                 t, n = r.kernel_ms()
                 ms.append(t)
             img, frays = rf.render(m.render_desc(fw, fh, fspp, depth=fdepth, numerics=num))
-            diff = img[..., :3].astype(np.float64) - g["image"]
+            c = compare(img, frays, os.path.join(ROOT, "tests", "golden", FIXTURE[name]))
             out[f"{name}_{num}"] = {"grays": round(rays / min(ms) / 1e6, 3), "kernel_ms": round(min(ms), 3), "rays": int(rays),
-                                    "rmse": float(np.sqrt((diff ** 2).mean())), "ray_ratio": frays / float(g["rays"][0]) - 1,
-                                    "fixture": f"{FIXTURE[name]} ({fw}x{fh}, {fspp} spp)"}
+                                    "rmse": c["rmse"], "ray_ratio": c["ray_ratio"] - 1, "block_rmse": c["block_rmse"],
+                                    "fixture": f"{FIXTURE[name]} ({fw}x{fh}, {fspp} spp; {c['over']})"}
             print(name, num, out[f"{name}_{num}"], flush=True)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     json.dump(out, open(os.path.join(ROOT, "gpurun_out", "contract_ab_measure.json"), "w"), indent=1)

@@ -12,6 +12,7 @@ step() {
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
     return 0
 }
+step gpu_tests 900 python -u -m pytest tests/ -v -m gpu --timeout 300 --timeout-method thread
 step par7 200 python tools/parity_record.py --scenes 7 --out gpurun_out/par7_unitfix.json
 B="python bench.py --no-cpu-baseline --no-compare-numerics --no-other-walk --no-parity --steps 20 --warmup 5"
 for p in 1 2 3; do for i in 1 2 3 4; do step pipe${p}_$i 120 $B --pipeline $p; done; done
