@@ -81,10 +81,13 @@ def parse():
                          "(MRT_RF_FOLD_BEHIND, beside the other contexts' path kernels: 8.35-8.45 ms per "
                          "C2 step in most runs but 9.8-10.1 in about one of five, against a steady 8.62 "
                          "for full), auto = lean from ~96 M paths per rank")
-    ap.add_argument("--pipeline", type=int, default=3,
-                    help="render contexts used round-robin on their own HIP streams: step i+1's launch "
-                         "fills the CUs freed by step i's tail instead of waiting for it (C2 per step, full "
-                         "fold: 8.66 / 8.61 ms at 2 / 3 contexts)")
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="render contexts used round-robin on their own HIP streams (0 = auto: 3 when a rank "
+                         "traces fewer than ~100 M paths per step, else 1).  With several contexts the GPU "
+                         "runs their path kernels side by side, which hides a short launch's fixed costs "
+                         "(emulated 8-rank C2 share: 1.235 / 1.191 / 1.132 ms per step at 1 / 2 / 3 contexts) "
+                         "but gains nothing on a full C2 render and makes it bimodal (8.60-8.63 ms at 1 "
+                         "context; 8.69-8.71, and 9.3-9.4 in 2 runs of 4, at 3; DESIGN.md §4)")
     ap.add_argument("--verify", action="store_true",
                     help="after timing, rank 0 checks the assembled framebuffer of the last step against a "
                          "single-context full render, bit for bit")
@@ -298,18 +301,20 @@ def main():
 
     # scene build + upload + workspace: outside the timed region (main.cpp:309 precedes 375)
     scene = m.select_scene(args.scene, args.width / args.height)
-    npipe = max(1, args.pipeline)
-    rnds = [m.Renderer(scene, device=local) for _ in range(npipe)]
-    rnd = rnds[0]
     d_rank, d_world = rank, world
     if world == 1 and args.emulate_world > 1:
         d_rank, d_world = args.emulate_rank, args.emulate_world
+    n_paths_local = len(m.local_pixels(m.render_desc(args.width, args.height, args.samples, tile_size=args.tile_size,
+                                                     rank=d_rank, world=d_world))) * (int(np.sqrt(np.float32(args.samples))) ** 2)
+    # contexts: several only where they pay -- a short per-rank launch (its fixed start / tail costs
+    # hidden by the other contexts' kernels); a full C2 render gains nothing and turns bimodal
+    npipe = args.pipeline if args.pipeline > 0 else (3 if n_paths_local < 100_000_000 else 1)
+    rnds = [m.Renderer(scene, device=local) for _ in range(npipe)]
+    rnd = rnds[0]
     # The lean fold keeps one load in flight per lane, so beside the other contexts' path kernels it
     # needs ~ns load round trips whatever the pixel count: it wins while the rank's path kernel is
     # long (C2 per-rank share, lean vs full, ms/step: 1 rank 8.36 / 8.59, 2: 4.16 / 4.30, 4: 2.19 /
-    # 2.16, 8: 1.19 / 1.15; tools/_fold_world.sh) -- auto: lean from ~96 M paths per rank
-    n_paths_local = len(m.local_pixels(m.render_desc(args.width, args.height, args.samples, tile_size=args.tile_size,
-                                                     rank=d_rank, world=d_world))) * (int(np.sqrt(np.float32(args.samples))) ** 2)
+    # 2.16, 8: 1.19 / 1.15; round 2) -- auto: lean from ~96 M paths per rank, with several contexts
     lean_fold = args.fold == "lean" or (args.fold == "auto" and npipe > 1 and n_paths_local >= 96_000_000)
     def desc_of(numerics):
         return m.render_desc(args.width, args.height, args.samples, depth=args.depth, tile_size=args.tile_size,

@@ -333,7 +333,8 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
     // mesh variants keep one constructor per branch: the shared-constructor loop spills there
     // (bunny -4%, teapot -5%; Cornell +1.8%, book2 0)
 #ifndef MRT_SHARED_WIDE
-#define MRT_SHARED_WIDE 1  // the wide (bvh_node) variants too
+#define MRT_SHARED_WIDE 0  // not the wide (bvh_node) variants: the plain loop has 6 spills instead of 29 there
+                           // (random spheres +4.4%, scene 1 +5%; profiles/r03_ab.txt)
 #endif
     constexpr bool kShared = (F & FT_MESH) == 0 && (MRT_SHARED_WIDE || !PathOcc<F>::kWide);
     constexpr bool kResume = MRT_SIG_OF(F) == SIG_ROOM_MESH;
