@@ -67,6 +67,16 @@ extern "C" int mrt_debug_phases(unsigned long long* out, int reset) {
     return 0;
 }
 #endif
+#if defined(MRT_EXPERIMENTS) && defined(MRT_WTIMES)  // build ONE of the two TUs with it
+// per wave of the last launch: start, pool exhausted, end (s_memrealtime, 100 MHz), workgroup
+__device__ unsigned long long g_wtimes[4 * 16384];
+extern "C" int mrt_debug_wtimes(unsigned long long* out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wtimes), sizeof(unsigned long long) * 4 * (size_t)n) != hipSuccess;
+}
+#define WT_MARK(v) (v) = __builtin_amdgcn_s_memrealtime()
+#else
+#define WT_MARK(v) (void)0
+#endif
 #if defined(MRT_EXPERIMENTS) && defined(MRT_BSTATS)  // build ONE of the two TUs with it
 namespace mrtd { __device__ unsigned long long g_bstats[64]; }
 extern "C" int mrt_debug_bstats(unsigned long long* out, int reset) {
@@ -160,6 +170,10 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
     // main.cpp:180/235 stop on !G_isRunning: a launch of a cancelled render does no work (mrt_render
     // splits a cancellable render into several launches)
     if (__hip_atomic_load(P.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return;
+#if defined(MRT_EXPERIMENTS) && defined(MRT_WTIMES)
+    uint64_t wt0 = 0, wt_ex = 0, wt1 = 0;
+    WT_MARK(wt0);
+#endif
     bool active = false;
     uint32_t idx = 0;
     PathState ps;
@@ -284,6 +298,9 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
             pool_next += c;
         }
         exhausted = part_tries >= MRT_NPART && pool_next >= pool_end;
+#if defined(MRT_EXPERIMENTS) && defined(MRT_WTIMES)
+        if (exhausted && wt_ex == 0) WT_MARK(wt_ex);
+#endif
     };
     auto begin_path = [&]() {
         ps.depth = 0;
@@ -609,6 +626,18 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
 #ifdef MRT_PHASES
     if (lane == 0)
         for (int i = 0; i < 12; i++) atomicAdd(&g_phases[i], (unsigned long long)ph.a[i]);
+#endif
+#if defined(MRT_EXPERIMENTS) && defined(MRT_WTIMES)
+    WT_MARK(wt1);
+    if (lane == 0) {
+        const size_t g = ((size_t)blockIdx.x * (blockDim.x >> 6) + wave) * 4;
+        if (g + 3 < 4 * 16384) {
+            g_wtimes[g] = wt0;
+            g_wtimes[g + 1] = wt_ex;
+            g_wtimes[g + 2] = wt1;
+            g_wtimes[g + 3] = blockIdx.x;
+        }
+    }
 #endif
     // one 64-bit add per wave
     uint64_t my = done_rays;
