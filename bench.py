@@ -5,7 +5,8 @@ scene 5, 500x500, 1024 spp, 32 bounces).
 One step = one full render of the workload: every (pixel, sample) path traced by mrt_path_kernel,
 folded per pixel in sample order (draw() semantics) and, for N > 1 GPUs, the tile shards gathered
 to rank 0 over RCCL and scattered into the full framebuffer.  The image is fixed as N grows
-(strong scaling); tile k of the work_queue order belongs to rank k % N.
+(strong scaling); the work_queue tiles are dealt to the ranks in rounds of N, each round in its
+own pseudo-random rank order (mrt_local_pixels).
 
 Prints ONE JSON line (rank 0).  `value` = total rays traced by all ranks / max-over-ranks wall
 time of the K timed steps.  `roofline` bounds the dominant kernel (mrt_path_kernel) by what limits
@@ -56,7 +57,7 @@ def parse():
     ap.add_argument("--samples", type=int, default=1024)
     ap.add_argument("--depth", type=int, default=32)
     ap.add_argument("--tile-size", type=int, default=8,
-                    help="work_queue tile edge; also the multi-GPU partition grain (tile k -> rank k %% N)")
+                    help="work_queue tile edge; also the multi-GPU partition grain (tiles dealt to the ranks in permuted rounds of N)")
     ap.add_argument("--cpu-spp", type=int, default=256, help="spp of the bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-quick", action="store_true", help="time the CPU baseline on the quota threads only")

@@ -106,7 +106,8 @@ typedef struct mrt_render_desc {
     uint32_t mode;           /* 0 draw() semantics, 1 draw2() semantics */
     uint64_t seed;           /* stream key: path p -> pcg32_srandom(splitmix64(seed ^ p), p) */
     uint32_t tile_size;      /* work_queue tiles (work_queue.cpp:64-128) */
-    uint32_t rank, world;    /* this call renders tiles k (inverted-Hilbert order) with k % world == rank */
+    uint32_t rank, world;    /* this call renders the tiles (inverted-Hilbert order) dealt to `rank`: rounds of
+                                `world` consecutive tiles, each round in its own permutation of the ranks */
     uint32_t chunk_samples;  /* samples per launch (0 = auto, bounded by HBM budget) */
     uint32_t flags;          /* MRT_RF_* */
     uint32_t threads;        /* CPU backend: worker threads (0 = every core); the GPU backend ignores it */

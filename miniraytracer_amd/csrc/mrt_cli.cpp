@@ -3,8 +3,8 @@
 // MI355X(s) through the C-ABI, prints the reference's "Trace: ... Mrays/s" line (main.cpp:403-406)
 // and writes the image (-o out.pfm: linear; -o out.ppm: Drago tone map, main.cpp:416-444).
 //
-// -gpus N shards the work_queue tiles over N GPUs (one host thread per device, tile k -> GPU
-// k % N); 0 = every visible GPU.  -backend cpu renders on the host instead (the CPU backend: the
+// -gpus N shards the work_queue tiles over N GPUs (one host thread per device, the tiles dealt in
+// permuted rounds of N, mrt_local_pixels); 0 = every visible GPU.  -backend cpu renders on the host instead (the CPU backend: the
 // same hot-path code compiled for the host, exact contract), with -threads worker threads as the
 // reference's -threads (0 = every core).  -numerics exact|fast picks the GPU's arithmetic contract.
 #include <chrono>

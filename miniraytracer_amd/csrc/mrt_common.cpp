@@ -252,12 +252,39 @@ std::vector<mrt_tile> mrt_internal_tiles(uint32_t W, uint32_t H, uint32_t ts) {
     return out;
 }
 
+// Tile k of the work_queue order -> its rank.  The tiles are dealt in rounds of `world` consecutive
+// tiles; round b goes to the ranks in the order of its own permutation (Fisher-Yates, draws
+// splitmix64^i(b)).  Dealing every round in rank order (k % world) gave one rank the same position of
+// every small Hilbert block, a systematic share: on the Cornell box at 8 ranks up to 2.8% more rays
+// than the mean rank (per-tile ray counts); permuted rounds leave the statistical spread.
+static uint64_t owner_mix(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+std::vector<uint32_t> mrt_internal_tile_owners(size_t ntiles, uint32_t world) {
+    std::vector<uint32_t> own(ntiles, 0u), perm(world);
+    if (world <= 1) return own;
+    for (size_t b = 0; b * world < ntiles; b++) {
+        for (uint32_t i = 0; i < world; i++) perm[i] = i;
+        uint64_t st = b;
+        for (uint32_t i = world - 1; i > 0; i--) {
+            st = owner_mix(st);
+            std::swap(perm[i], perm[st % (i + 1u)]);
+        }
+        for (uint32_t j = 0; j < world && b * world + j < ntiles; j++) own[b * world + j] = perm[j];
+    }
+    return own;
+}
+
 std::vector<uint32_t> mrt_internal_local_pixels(const mrt_render_desc* d) {
     std::vector<mrt_tile> tiles = mrt_internal_tiles(d->width, d->height, d->tile_size ? d->tile_size : 32);
     std::vector<uint32_t> px;
     uint32_t world = d->world ? d->world : 1;
+    const std::vector<uint32_t> own = mrt_internal_tile_owners(tiles.size(), world);
     for (size_t k = 0; k < tiles.size(); k++) {
-        if (k % world != d->rank) continue;
+        if (own[k] != d->rank) continue;
         const mrt_tile& t = tiles[k];
         for (uint32_t y = t.ymin; y < t.ymax; y++)
             for (uint32_t x = t.xmin; x < t.xmax; x++) px.push_back(x + y * d->width);

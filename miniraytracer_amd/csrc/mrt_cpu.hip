@@ -117,6 +117,8 @@ mrt_status mrt_cpu_scene_create(const mrt_scene_view* v, mrt_cpu_scene** out) {
     S.prog = T.prog.data();
     S.bleaf = T.bleaf.data();
     S.nbleaf = T.nbleaf;
+    S.nbleaf_f = (float)T.nbleaf;
+    S.inv_nbleaf = 1.0f / S.nbleaf_f;
     S.blist = T.blist;
     S.root = v->root;
     S.biased = v->biased;
@@ -317,8 +319,9 @@ mrt_status mrt_cpu_render(mrt_cpu_scene* c, const mrt_render_desc* d, float* rgb
     std::vector<mrt_tile> tiles;  // this rank's tiles, in work_queue order
     {
         const std::vector<mrt_tile> all = mrt_internal_tiles(d->width, d->height, d->tile_size ? d->tile_size : 32u);
+        const std::vector<uint32_t> own = mrt_internal_tile_owners(all.size(), world);
         for (size_t k = 0; k < all.size(); k++)
-            if (k % world == d->rank) tiles.push_back(all[k]);
+            if (own[k] == d->rank) tiles.push_back(all[k]);
     }
     uint64_t px = 0;
     for (const mrt_tile& t : tiles) px += (uint64_t)(t.xmax - t.xmin) * (t.ymax - t.ymin);

@@ -13,6 +13,10 @@ struct mrt_tile {
     uint32_t xmin, xmax, ymin, ymax;
 };
 std::vector<mrt_tile> mrt_internal_tiles(uint32_t width, uint32_t height, uint32_t tile_size);
-// Pixels (row-major index, row 0 = bottom) owned by `rank` of `world`: tiles k % world == rank,
-// each tile scanned row by row (the order draw() visits them, main.cpp:148-149).
+// The rank of each work_queue tile: rounds of `world` consecutive tiles, each dealt in the order of
+// its own pseudo-random permutation of the ranks (mrt_common.cpp).
+std::vector<uint32_t> mrt_internal_tile_owners(size_t ntiles, uint32_t world);
+// Pixels (row-major index, row 0 = bottom) owned by `rank` of `world`: the tiles
+// mrt_internal_tile_owners gives it, each scanned row by row (the order draw() visits them,
+// main.cpp:148-149).
 std::vector<uint32_t> mrt_internal_local_pixels(const mrt_render_desc* d);

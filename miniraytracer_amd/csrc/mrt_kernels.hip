@@ -67,11 +67,27 @@ extern "C" int mrt_debug_phases(unsigned long long* out, int reset) {
     return 0;
 }
 #endif
+// Launch end.  A wave whose partition is handed out takes work from ONE other partition (chosen
+// per wave group in four directions, MRT_STEAL_SPREAD), in small claims, then ends.  Visiting all
+// eight (the round-2 rule) cost every wave 8 failing atomics at the launch's end, on 8 addresses
+// hit by all 7168 waves at once: 3.5-4 us each against 0.6 us for a claim mid-launch (wave
+// timelines, tools/wtimes.py), while the wave's in-flight lanes waited -- a fixed ~40 us per launch,
+// 4% of an 8-rank share.  Every partition is still finished by its own waves.
+#ifndef MRT_STEAL_SMALL
+#define MRT_STEAL_SMALL 1
+#endif
+#ifndef MRT_STEAL_TRIES
+#define MRT_STEAL_TRIES 2u  // partitions a wave takes work from (its own first) before it ends
+#endif
+#ifndef MRT_STEAL_SPREAD
+#define MRT_STEAL_SPREAD 1
+#endif
 #if defined(MRT_EXPERIMENTS) && defined(MRT_WTIMES)  // build ONE of the two TUs with it
 // per wave of the last launch: start, pool exhausted, end (s_memrealtime, 100 MHz), workgroup
-__device__ unsigned long long g_wtimes[4 * 16384];
+// + time inside successful / failed claim atomics (10-ns ticks) and their counts (ok | fail << 32)
+__device__ unsigned long long g_wtimes[7 * 16384];
 extern "C" int mrt_debug_wtimes(unsigned long long* out, int n) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wtimes), sizeof(unsigned long long) * 4 * (size_t)n) != hipSuccess;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wtimes), sizeof(unsigned long long) * 7 * (size_t)n) != hipSuccess;
 }
 #define WT_MARK(v) (v) = __builtin_amdgcn_s_memrealtime()
 #else
@@ -171,7 +187,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
     // splits a cancellable render into several launches)
     if (__hip_atomic_load(P.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return;
 #if defined(MRT_EXPERIMENTS) && defined(MRT_WTIMES)
-    uint64_t wt0 = 0, wt_ex = 0, wt1 = 0;
+    uint64_t wt0 = 0, wt_ex = 0, wt1 = 0, wt_f = 0, wt_aok = 0, wt_afail = 0, wt_n = 0;
     WT_MARK(wt0);
 #endif
     bool active = false;
@@ -197,6 +213,9 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
     const uint32_t wpb = blockDim.x >> 6;  // waves per workgroup
     uint32_t part = blockIdx.x % MRT_NPART;  // wave-uniform: the partition claims come from
     uint32_t part_tries = 0;                 // partitions found handed out
+    // the partitions a wave visits after its own: every one (step odd, coprime with 8); with
+    // MRT_STEAL_SPREAD the waves of one partition leave it in four directions instead of one
+    const uint32_t steal_step = MRT_STEAL_SPREAD ? 1u + 2u * ((blockIdx.x / MRT_NPART) & 3u) : 1u;
     bool in_tail = false;                    // the partition's last paths: small claims
     uint64_t pool_next = 0, pool_end = 0;    // wave-uniform: the wave's claimed, not yet taken paths
     if (P.static_first) {
@@ -263,9 +282,13 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
         const uint32_t have = (uint32_t)(pool_end - pool_next);
         uint64_t nb = 0, ne = 0;
         if (have < c) {
-            while (part_tries < MRT_NPART) {  // wave-uniform
+            while (part_tries < MRT_STEAL_TRIES) {  // wave-uniform
                 const uint64_t pe = P.part_base[part + 1], p0 = P.part_dyn[part];
                 const uint32_t batch = in_tail ? MRT_TAIL_BATCH : MRT_BATCH;
+#if defined(MRT_EXPERIMENTS) && defined(MRT_WTIMES)
+                uint64_t wt_a = 0;
+                WT_MARK(wt_a);
+#endif
                 if (lane == 0) {
                     nb = p0 + atomicAdd(P.counter + part * MRT_COUNTER_STRIDE, (unsigned long long)batch);
                     // every 32nd claim: a system-scope store to host memory, read by mrt_progress
@@ -276,15 +299,32 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                 // lane 0's claim to every lane, as a scalar (the whole wave runs claim())
                 nb = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(nb >> 32)) << 32) |
                      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)nb);
+#if defined(MRT_EXPERIMENTS) && defined(MRT_WTIMES)
+                {
+                    uint64_t wt_b = 0;
+                    WT_MARK(wt_b);
+                    if (nb < pe) { wt_aok += wt_b - wt_a; wt_n += 1; }
+                    else { wt_afail += wt_b - wt_a; wt_n += 1ull << 32; }
+                }
+#endif
                 if (nb < pe) {
                     ne = umin64(nb + batch, pe);
                     // near the partition's end, claims shrink so the last ones finish together
+#if MRT_STEAL_SMALL
+                    in_tail = pe - ne <= P.tail_zone / MRT_NPART;
+#else
                     in_tail = in_tail || pe - ne <= P.tail_zone / MRT_NPART;
+#endif
                     break;
                 }
+#if defined(MRT_EXPERIMENTS) && defined(MRT_WTIMES)
+                if (wt_f == 0) WT_MARK(wt_f);
+#endif
                 part_tries++;
-                part = (part + 1) % MRT_NPART;
-                in_tail = false;
+                part = (part + steal_step) % MRT_NPART;
+                // (MRT_STEAL_SMALL: the first claim on the next partition is a small one -- it is
+                // usually in its own tail zone -- and the claim's position decides the next size)
+                in_tail = MRT_STEAL_SMALL;
             }
         }
         if (want) {
@@ -297,7 +337,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
         } else {
             pool_next += c;
         }
-        exhausted = part_tries >= MRT_NPART && pool_next >= pool_end;
+        exhausted = part_tries >= MRT_STEAL_TRIES && pool_next >= pool_end;
 #if defined(MRT_EXPERIMENTS) && defined(MRT_WTIMES)
         if (exhausted && wt_ex == 0) WT_MARK(wt_ex);
 #endif
@@ -630,12 +670,15 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
 #if defined(MRT_EXPERIMENTS) && defined(MRT_WTIMES)
     WT_MARK(wt1);
     if (lane == 0) {
-        const size_t g = ((size_t)blockIdx.x * (blockDim.x >> 6) + wave) * 4;
-        if (g + 3 < 4 * 16384) {
+        const size_t g = ((size_t)blockIdx.x * (blockDim.x >> 6) + wave) * 7;
+        if (g + 6 < 7 * 16384) {
+            g_wtimes[g + 4] = wt_aok;
+            g_wtimes[g + 5] = wt_afail;
+            g_wtimes[g + 6] = wt_n;
             g_wtimes[g] = wt0;
             g_wtimes[g + 1] = wt_ex;
             g_wtimes[g + 2] = wt1;
-            g_wtimes[g + 3] = blockIdx.x;
+            g_wtimes[g + 3] = (uint64_t)blockIdx.x | ((wt_f ? wt_f - wt0 : 0ull) << 20);
         }
     }
 #endif

@@ -12,6 +12,7 @@ namespace mrtd {
 #define MRT_NPART 8u  // work partitions (and counters) per launch: one per XCD (mrt_kernels.hip)
 #endif
 #define MRT_COUNTER_STRIDE 16u  // uint64 words between two partitions' counters (128 B)
+#define MRT_CNT_SLOTS MRT_NPART  // counter slots per launch (the reset kernels' unit)
 
 struct PathParams {
     DScene sc;                            // by value: kernarg (constant) memory, scalar-loaded

@@ -59,17 +59,16 @@ struct FoldEnd {
     uint32_t ns;                     // samples per pixel (mode 0 divides by it)
     unsigned long long* counters;    // work counters of the render's launches (MRT_COUNTER_STRIDE apart)
     unsigned long long* hprog;       // their progress snapshots in host memory (or null)
-    uint32_t nreset;                 // how many of each
+    uint32_t nreset;                 // counter slots to reset (MRT_CNT_SLOTS per launch)
+    uint32_t nprog;                  // progress snapshots to reset (MRT_NPART per launch)
 };
 // what the render's path kernels consumed, reset for the context's next render in stream order
-// after them: the work counters (word (k * MRT_NPART + part) * MRT_COUNTER_STRIDE) and the
+// after them: the counter slots (word (k * MRT_CNT_SLOTS + slot) * MRT_COUNTER_STRIDE) and the
 // progress snapshots -- instead of clearing fills enqueued before each render (a blit kernel
 // needs a free wave slot, which the other pipelined contexts' persistent path kernels hold)
 MRT_DFN void reset_counters(const FoldEnd& e, uint32_t i) {
-    if (i < e.nreset) {
-        e.counters[(size_t)i * MRT_COUNTER_STRIDE] = 0ull;
-        if (e.hprog) __hip_atomic_store(e.hprog + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    if (i < e.nreset) e.counters[(size_t)i * MRT_COUNTER_STRIDE] = 0ull;
+    if (i < e.nprog && e.hprog) __hip_atomic_store(e.hprog + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __global__ void __launch_bounds__(256) mrt_fold_kernel(const float* __restrict__ rad, float4* __restrict__ acc, uint32_t npix, uint32_t s0,
                                                       uint32_t s1, uint32_t mode, float max_lum, FoldEnd fe) {
@@ -142,7 +141,7 @@ mrt_fold_lean_kernel(const float* __restrict__ rad, float4* __restrict__ acc, ui
 }
 
 // Also resets what the render's path kernels consumed, for the context's next render, in stream
-// order after them: the work counters of its launches (word (k * MRT_NPART + part) *
+// order after them: the counter slots of its launches (word (k * MRT_CNT_SLOTS + slot) *
 // MRT_COUNTER_STRIDE) and their progress snapshots in host memory -- instead of clearing fills
 // enqueued before each render (a blit kernel needs a free wave slot, which the persistent path
 // kernels of the other pipelined contexts hold: up to 49 ms waits in the bench trace).
@@ -156,12 +155,10 @@ mrt_fold_lean_kernel(const float* __restrict__ rad, float4* __restrict__ acc, ui
 #endif
 __global__ void __launch_bounds__(MRT_FINAL_WG) __attribute__((amdgpu_num_vgpr(8)))
 mrt_final_kernel(const float4* __restrict__ acc, float4* __restrict__ out, uint32_t npix, uint32_t ns, uint32_t mode, float max_lum,
-                 unsigned long long* __restrict__ counters, unsigned long long* hprog, uint32_t nreset) {
+                 unsigned long long* __restrict__ counters, unsigned long long* hprog, uint32_t nreset, uint32_t nprog) {
     const uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
-    if (lp < nreset) {
-        counters[(size_t)lp * MRT_COUNTER_STRIDE] = 0ull;
-        if (hprog) __hip_atomic_store(hprog + lp, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    if (lp < nreset) counters[(size_t)lp * MRT_COUNTER_STRIDE] = 0ull;
+    if (lp < nprog && hprog) __hip_atomic_store(hprog + lp, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (lp >= npix) return;
     const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(acc), 0, 0xFFFFFFFFu, 0x00020000);
     const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(out, 0, 0xFFFFFFFFu, 0x00020000);
@@ -857,6 +854,8 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     UP(T.dmats.data(), T.dmats.size(), &S.mats);
     UP(T.bleaf.data(), T.bleaf.size(), &S.bleaf);
     S.nbleaf = T.nbleaf;
+    S.nbleaf_f = (float)T.nbleaf;
+    S.inv_nbleaf = 1.0f / S.nbleaf_f;
     S.blist = T.blist;
     UP(v->textures, v->n_textures, &S.texs);
     UP((const float4*)v->perlin_ranvec, 256, &S.ranvec);
@@ -949,6 +948,9 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
             if (*e) nb = std::max(1, atoi(e));
 #endif
         L.grid = prop.multiProcessorCount * nb;
+        // every work partition needs waves of its own: a wave leaves its partition only once it is
+        // handed out, and visits at most MRT_STEAL_TRIES partitions (mrt_kernels.hip)
+        if (L.grid < (int)MRT_NPART) return mrt_internal_fail(MRT_ERR_HIP, "path kernel grid smaller than the work partitions");
         s->max_threads = std::max(s->max_threads, (size_t)L.grid * L.wg);
     }
     *out = s;
@@ -1085,7 +1087,7 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
     s->lev_rows = std::max<uint32_t>(d->max_bounces, 1);
     if ((st = grow(s, (void**)&s->d_lev, &s->lev_cap, (size_t)s->lev_rows * s->max_threads * 16))) return st;
     uint32_t launches = (ns + s->chunk - 1) / s->chunk;
-    const size_t cnt_words = (size_t)MRT_NPART * MRT_COUNTER_STRIDE;  // per launch
+    const size_t cnt_words = (size_t)MRT_CNT_SLOTS * MRT_COUNTER_STRIDE;  // per launch
     {
         void* const before = s->d_counters;
         if ((st = grow(s, (void**)&s->d_counters, &s->cnt_cap, (size_t)launches * cnt_words * 8))) return st;
@@ -1193,7 +1195,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.max_bounces = d->max_bounces;
         P.rad = s->d_rad;
         P.path_rays = (d->flags & MRT_RF_PATH_DEBUG) ? s->d_path_rays : nullptr;
-        P.counter = (unsigned long long*)(s->d_counters + (size_t)s->n_launch * MRT_NPART * MRT_COUNTER_STRIDE);
+        P.counter = (unsigned long long*)(s->d_counters + (size_t)s->n_launch * MRT_CNT_SLOTS * MRT_COUNTER_STRIDE);
         P.hprog = (unsigned long long*)(s->h_prog + (size_t)s->n_launch * MRT_NPART);
         P.cancel = (const int*)(s->d_counter + 4);
         P.rays = d_rays ? (unsigned long long*)d_rays : s->d_rays;
@@ -1209,7 +1211,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         const bool lean = (d->flags & MRT_RF_FOLD_BEHIND) && d->mode == 0;
         const bool last = s1 == ns && !preview && !lean;
         FoldEnd fe{last ? (float4*)d_local : nullptr, ns, last ? (unsigned long long*)s->d_counters : nullptr,
-                   last ? (unsigned long long*)s->h_prog : nullptr, last ? launches * MRT_NPART : 0u};
+                   last ? (unsigned long long*)s->h_prog : nullptr, last ? launches * MRT_CNT_SLOTS : 0u, last ? launches * MRT_NPART : 0u};
         const uint32_t nthr = std::max(s->npix, fe.nreset);
         if (lean)
             hipLaunchKernelGGL(mrt_fold_lean_kernel, dim3((s->npix + MRT_FOLD_LEAN_WG - 1) / MRT_FOLD_LEAN_WG), dim3(MRT_FOLD_LEAN_WG), 0, q,
@@ -1221,7 +1223,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         if (preview) {  // the image after s1 samples, copied under the sequence lock
             hipLaunchKernelGGL(mrt_final_kernel, dim3((s->npix + MRT_FINAL_WG - 1) / MRT_FINAL_WG), dim3(MRT_FINAL_WG), 0, q, s->d_acc, s->d_prev,
                                s->npix, s1, d->mode, d->max_luminance,
-                               (unsigned long long*)nullptr, (unsigned long long*)nullptr, 0u);
+                               (unsigned long long*)nullptr, (unsigned long long*)nullptr, 0u, 0u);
             HIPCHK(hipGetLastError());
             HIPCHK(hipStreamWriteValue32(q, s->h_seq, 2 * seq + 1, 0));
             HIPCHK(hipMemcpyAsync(s->h_prev, s->d_prev, (size_t)s->npix * 16, hipMemcpyDeviceToHost, q));
@@ -1232,10 +1234,10 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         s->last_paths = P.n_paths;
     }
     if (preview || ((d->flags & MRT_RF_FOLD_BEHIND) && d->mode == 0)) {  // (otherwise the last fold wrote the output and reset the counters)
-        const uint32_t nreset = launches * MRT_NPART;
+        const uint32_t nreset = launches * MRT_CNT_SLOTS;
         const uint32_t blocks = (std::max(s->npix, nreset) + MRT_FINAL_WG - 1) / MRT_FINAL_WG;
         hipLaunchKernelGGL(mrt_final_kernel, dim3(blocks), dim3(MRT_FINAL_WG), 0, q, s->d_acc, (float4*)d_local, s->npix, ns, d->mode,
-                           d->max_luminance, (unsigned long long*)s->d_counters, (unsigned long long*)s->h_prog, nreset);
+                           d->max_luminance, (unsigned long long*)s->d_counters, (unsigned long long*)s->h_prog, nreset, launches * MRT_NPART);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(s->ev_done, q));

@@ -144,7 +144,11 @@ MRT_DFN float biased_pdf_value(const DScene& S, f3 origin, f3 dir, float time) {
         const mrt_node n = ld_node(bl + i);
         sum += leaf_pdf_value<F>(S, n, origin, dir, time);
     }
-    return sum / (float)S.nbleaf;
+#if MRT_FAST
+    return sum * S.inv_nbleaf;  // (-freciprocal-math: the division by the loop-invariant count)
+#else
+    return sum / S.nbleaf_f;
+#endif
 }
 template <uint32_t F>
 MRT_DFN f3 leaf_pdf_generate(const DScene& S, const mrt_node& n, f3 origin, float time, Pcg& rng, Draws& dr) {
@@ -171,7 +175,7 @@ MRT_DFN f3 biased_pdf_generate(const DScene& S, f3 origin, float time, Pcg& rng,
         const mrt_node n = ld_node(const_ptr(S.bleaf));
         return leaf_pdf_generate<F>(S, n, origin, time, rng, dr);
     }
-    const int i = int(dr.next(rng) * (float)S.nbleaf);  // object_list::pdf_generate (scene_object.h:72-77)
+    const int i = int(dr.next(rng) * S.nbleaf_f);  // object_list::pdf_generate (scene_object.h:72-77)
     if (S.nbleaf == 1) {
         const mrt_node n = ld_node(const_ptr(S.bleaf));
         return leaf_pdf_generate<F>(S, n, origin, time, rng, dr);

@@ -145,6 +145,8 @@ struct DScene {
     const LinOp* __restrict__ prog;  // linear hit program (FT_LIN kernels), mrt_lin.h
     const mrt_node* __restrict__ bleaf;  // leaves of scene.biased_objects (the list's children, or the object)
     uint32_t nbleaf, blist;              // leaf count; 1 if biased_objects is an object_list
+    float nbleaf_f, inv_nbleaf;          // (float)nbleaf and RN(1 / (float)nbleaf), from the host: kernarg
+                                         // scalars (converted on the device they held two VGPRs, spilled)
     uint32_t root, biased, sky;
     mrt_camera cam;
     const mrt_camera* __restrict__ camp;  // the camera in HBM, read at each path start (scalar loads)

@@ -1,8 +1,10 @@
 """Multi-GPU framebuffer assembly: tile shards -> rank 0 with ONE collective.
 
 The reference splits the image into work_queue tiles (work_queue.cpp:64-128) that its threads
-pull from one atomic counter.  Here tile k (in the same inverted-Hilbert order) belongs to rank
-k % world; each rank renders its tiles into a compact [n_local, 4] buffer in HBM, and one
+pull from one atomic counter.  Here the tiles (in the same inverted-Hilbert order) are dealt to the
+ranks in rounds of `world`, each round in its own pseudo-random rank order (local_pixels /
+mrt_local_pixels: a fixed deal, so no rank always takes the same position of the curve's small
+blocks); each rank renders its tiles into a compact [n_local, 4] buffer in HBM, and one
 gather over RCCL (xGMI) brings the equal-size (padded) shards to rank 0, which scatters them into
 the W*H framebuffer (row 0 = bottom, G_linearBackBuffer layout, main.cpp:58).  Ray counts are
 summed with one all_reduce.  Works with any torch.distributed backend (nccl on GPUs, gloo on CPU

@@ -48,7 +48,7 @@ def test_cpu_backend_matches_c_restatement(mrt, orc, sid, w, h, spp, depth, mode
 
 
 def test_cpu_backend_independent_of_threads_and_ranks(mrt):
-    """Per-path stream keys: 1 thread, 5 threads and two rank shards (tile k -> rank k % 2)
+    """Per-path stream keys: 1 thread, 5 threads and two rank shards (the tiles dealt to 2 ranks)
     assembled give the same image bit for bit."""
     sc, r = cpu_renderer(mrt, 5, 40, 24)
     a, ra = r.render(mrt.render_desc(40, 24, 9, tile_size=8, threads=1))

@@ -1,4 +1,4 @@
-"""World-size-2/3 gloo test of the multi-GPU path on CPU: tile ownership (tile k -> rank k % world),
+"""World-size-2/3 gloo test of the multi-GPU path on CPU: tile ownership (the permuted deal of tiles to ranks),
 each rank rendering ONLY its own tiles through the product's render path (the CPU backend behind the
 same C-ABI: mrt_render with rank / world in the desc, the hot-path code compiled for the host),
 padded gather to rank 0 and scatter into the framebuffer.  The assembled image must equal a

@@ -75,7 +75,7 @@ def test_gpu_matches_oracle(gpu, orc, sid, w, h, spp, depth):
 
 
 def test_sharded_ranks_reassemble_bit_identical(gpu):
-    """Tile k -> rank k % world (work_queue order): every rank's pixels, gathered, equal the
+    """Tiles dealt to the ranks (work_queue order, permuted rounds): every rank's pixels, gathered, equal the
     single-GPU image bit for bit (per-path PCG streams make the image independent of the split)."""
     w, h, spp = 70, 45, 16
     sc, r = renderer(gpu, 5, w, h)

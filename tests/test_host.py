@@ -127,14 +127,50 @@ def reference_tiles(W, H, ts):
     return out
 
 
+M64 = (1 << 64) - 1
+
+
+def tile_owners(n, world):
+    """The multi-GPU deal (mrt_common.cpp mrt_internal_tile_owners): rounds of `world` consecutive
+    work_queue tiles, round b to the ranks in the order of a Fisher-Yates permutation whose draws
+    are splitmix64 iterated from b."""
+    def mix(z):
+        z = (z + 0x9E3779B97F4A7C15) & M64
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+        return z ^ (z >> 31)
+    own = [0] * n
+    if world <= 1:
+        return own
+    for b in range((n + world - 1) // world):
+        perm, st = list(range(world)), b
+        for i in range(world - 1, 0, -1):
+            st = mix(st)
+            j = st % (i + 1)
+            perm[i], perm[j] = perm[j], perm[i]
+        for j in range(world):
+            if b * world + j < n:
+                own[b * world + j] = perm[j]
+    return own
+
+
+def test_tile_deal_is_balanced_and_permuted():
+    """Every round of `world` tiles gives each rank exactly one tile, and not always the same one."""
+    own = tile_owners(4096, 8)
+    for b in range(512):
+        assert sorted(own[8 * b:8 * b + 8]) == list(range(8))
+    assert any(own[8 * b:8 * b + 8] != own[:8] for b in range(1, 512))
+
+
 @pytest.mark.parametrize("W,H,ts,world", [(500, 500, 32, 1), (500, 500, 32, 8), (200, 100, 32, 3), (37, 23, 7, 2),
-                                           (1, 1, 32, 1), (1024, 1024, 32, 8), (64, 640, 16, 5)])
+                                           (1, 1, 32, 1), (1024, 1024, 32, 8), (64, 640, 16, 5), (500, 500, 4, 8)])
 def test_local_pixels_follow_work_queue_tiles(mrt, W, H, ts, world):
     tiles = reference_tiles(W, H, ts)
+    own = tile_owners(len(tiles), world)
     seen = np.zeros(W * H, dtype=np.int32)
     for rank in range(world):
         px = mrt.local_pixels(mrt.render_desc(W, H, 16, tile_size=ts, rank=rank, world=world))
-        exp = [x + y * W for k, (x0, x1, y0, y1) in enumerate(tiles) if k % world == rank
+        exp = [x + y * W for k, (x0, x1, y0, y1) in enumerate(tiles) if own[k] == rank
                for y in range(y0, y1) for x in range(x0, x1)]
         assert px.tolist() == exp
         seen[px] += 1

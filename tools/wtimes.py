@@ -16,15 +16,15 @@ scene, w, h, spps = args[0], args[1], args[2], args[3:]
 sc = m.select_scene(scene, w / h)
 r = m.Renderer(sc, 0)
 NW = 16384
-buf = (C.c_ulonglong * (4 * NW))()
+buf = (C.c_ulonglong * (7 * NW))()
 for spp in spps:
-    d = m.render_desc(w, h, spp, numerics=os.environ.get("NUMERICS", "fast"))
+    d = m.render_desc(w, h, spp, depth=int(os.environ.get("DEPTH", "32")), numerics=os.environ.get("NUMERICS", "fast"))
     r.render(d)
     C.memset(buf, 0, C.sizeof(buf))
     img, rays = r.render(d)
     if lib().mrt_debug_wtimes(buf, NW):
         raise SystemExit("mrt_debug_wtimes failed")
-    a = np.frombuffer(buf, dtype=np.uint64).reshape(NW, 4).astype(np.int64)
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(NW, 7).astype(np.int64)
     a = a[a[:, 0] != 0]
     t0 = a[:, 0].min()
     st, ex, en = (a[:, 0] - t0) / 100.0, (a[:, 1] - t0) / 100.0, (a[:, 2] - t0) / 100.0
@@ -35,6 +35,14 @@ for spp in spps:
     print(f"  exhausted  {q(ex)}")
     print(f"  end        {q(en)}")
     print(f"  end-exh    {q(en - ex)}")
-    xcd = a[:, 3] % 8
+    ff = np.where((a[:, 3] >> 20) != 0, st + (a[:, 3] >> 20) / 100.0, np.nan)
+    print(f"  first fail {q(ff)}")
+    print(f"  exh-fail   {q(ex - ff)}")
+    nok, nfail = a[:, 6] & 0xFFFFFFFF, a[:, 6] >> 32
+    print(f"  claim atomics per wave: ok {nok.mean():.1f}, failed {nfail.mean():.1f}; mean latency ok "
+          f"{a[:, 4].sum() / max(nok.sum(), 1) / 100:.2f} us, failed {a[:, 5].sum() / max(nfail.sum(), 1) / 100:.2f} us")
+    print(f"  time in failed atomics per wave {q(a[:, 5] / 100.0)}")
+    print(f"  time in ok atomics per wave     {q(a[:, 4] / 100.0)}")
+    xcd = (a[:, 3] & 0xFFFFF) % 8
     print("  per XCD (by workgroup % 8) last end: " + " ".join(f"{en[xcd == k].max():.1f}" for k in range(8)))
     print("  per XCD median exhausted:            " + " ".join(f"{np.nanmedian(ex[xcd == k]):.1f}" for k in range(8)))
