@@ -130,7 +130,7 @@ extern "C" int mrt_debug_bstats(unsigned long long* out, int reset) {
 #endif
 template <uint32_t F> struct PathLevLds {
     static constexpr uint32_t K = MRT_FWD_FOLD ? 0u  // no stored levels
-                                  : ((F & 0xFFFFu) == (FT_LIN | FT_INST)) ? MRT_LEVK_CORNELL
+                                  : ((F & 0xFFFFu & ~FT_BIASED) == (FT_LIN | FT_INST)) ? MRT_LEVK_CORNELL
                                   : PathOcc<F>::kWide                  ? MRT_LEVK_WIDE
                                   : ((F & FT_MESH) != 0)               ? MRT_LEVK_MESH
                                                                        : 0u;

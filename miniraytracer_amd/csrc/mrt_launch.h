@@ -74,10 +74,12 @@ static constexpr bool kResumeLin = MRT_RESUME_LIN && (F & FT_LIN) != 0 && (F & F
 // kernel variants by scene features (the first instantiated superset is launched); FT_LIN
 // variants need the scene's linear hit program (mrt_lin.h), FT_ALL runs any graph.  The same list
 // in both numerics builds.
-static constexpr uint32_t kVariants[] = {FT_LIN | FT_INST | MRT_SIG_BITS(SIG_CORNELL),
-                                         FT_LIN | FT_MESH | FT_METAL | MRT_SIG_BITS(SIG_ROOM_MESH),
-                                         FT_LIN | FT_INST,
-                                         FT_LIN | FT_MESH | FT_METAL,
+static constexpr uint32_t kVariants[] = {FT_LIN | FT_INST | FT_BIASED | MRT_SIG_BITS(SIG_CORNELL),
+                                         FT_LIN | FT_MESH | FT_METAL | FT_BIASED | MRT_SIG_BITS(SIG_ROOM_MESH),
+                                         FT_LIN | FT_INST | FT_BIASED,
+                                         FT_LIN | FT_MESH | FT_METAL | FT_BIASED,
+                                         // sky-lit scenes 0-4: no light sampling compiled in (its registers
+                                         // pushed this 128-VGPR kernel into a spill inside the bounce loop)
                                          FT_LIN | FT_BVHW | FT_TEX | FT_METAL | FT_MOVING | FT_SKY | FT_UV,
                                          FT_LIN | FT_ALL,
                                          FT_ALL};

@@ -518,6 +518,7 @@ static uint32_t scene_features(const mrt_scene_view* v, const std::vector<mrt_no
     }
     if (v->sky) f |= FT_SKY;
     if (v->biased != MRT_NONE) {
+        f |= FT_BIASED;
         const mrt_node& b = nodes[v->biased];
         if ((b.kind & 0xFF) == MRT_K_SPHERE) f |= FT_BSPHERE;
         if ((b.kind & 0xFF) == MRT_K_LIST)

@@ -379,7 +379,7 @@ MRT_DFN bool shade_hit(const DScene& S, PathState& ps, uint32_t max_bounces, con
     const bool lamb = !(F & FT_ISO) || M.kind == MRT_M_LAMBERTIAN;
     const f3 att = mat_color<F>(S, M, rec);
     f3 gen;
-    const bool light = S.biased != MRT_NONE && randf(ps.rng) < 0.5f;
+    const bool light = ((F & FT_BIASED) && S.biased != MRT_NONE) && randf(ps.rng) < 0.5f;
     // both sides of the mix start with two draws when the surface side is cosine sampling
     Draws dr{0.0f, 0.0f, 2u};
     if (lamb) {
@@ -404,7 +404,7 @@ MRT_DFN bool shade_hit(const DScene& S, PathState& ps, uint32_t max_bounces, con
         sval = 1 / (2 * PI_F);
         spdf = 1.0f / (2.0f * PI_F);
     }
-    const float pdf_v = S.biased != MRT_NONE ? 0.5f * (biased_pdf_value<F>(S, rec.p, sc.d, r.time) + sval) : sval;
+    const float pdf_v = ((F & FT_BIASED) && S.biased != MRT_NONE) ? 0.5f * (biased_pdf_value<F>(S, rec.p, sc.d, r.time) + sval) : sval;
     const float4 lv = make_float4(att.x * spdf, att.y * spdf, att.z * spdf, pdf_v);
     push_level(ps, lev, lv);
     r = sc;
@@ -530,7 +530,7 @@ MRT_DFN bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, c
     pr->n = rec.n;
     pr->kind = lamb ? 1u : 2u;
     BSTAT(6);
-    const bool light = S.biased != MRT_NONE && randf(ps.rng) < 0.5f;
+    const bool light = ((F & FT_BIASED) && S.biased != MRT_NONE) && randf(ps.rng) < 0.5f;
     Draws dr{0.0f, 0.0f, 2u};
     if (lamb) {
         dr.v0 = randf(ps.rng);
@@ -560,7 +560,7 @@ MRT_DFN void finish_scatter(const DScene& S, PathState& ps, const LevStore<LK>& 
         sval = 1 / (2 * PI_F);
         spdf = 1.0f / (2.0f * PI_F);
     }
-    const float pdf_v = S.biased != MRT_NONE ? 0.5f * (biased_pdf_value<F>(S, sc.o, sc.d, sc.time) + sval) : sval;
+    const float pdf_v = ((F & FT_BIASED) && S.biased != MRT_NONE) ? 0.5f * (biased_pdf_value<F>(S, sc.o, sc.d, sc.time) + sval) : sval;
     const float4 lv = make_float4(pr.att.x * spdf, pr.att.y * spdf, pr.att.z * spdf, pdf_v);
     push_level(ps, lev, lv);
 }

@@ -176,7 +176,8 @@ enum : uint32_t {
     FT_UV = 1u << 10,      // uv sampled on spheres / rects
     FT_LIN = 1u << 11,     // scene graph compiled to a linear hit program (mrt_lin.h)
     FT_BVHW = 1u << 12,    // bvh_node subtrees as wide nodes (MRT_K_BVHW)
-    FT_ALL = ((1u << 13) - 1) & ~FT_LIN,
+    FT_BIASED = 1u << 13,  // a biased (light-sampling) list: the mixture pdf of main.cpp:86-101
+    FT_ALL = ((1u << 14) - 1) & ~FT_LIN,
 };
 
 // Per-wave LDS stacks, lane-interleaved ([slot][word][lane]) so every access is conflict-free.

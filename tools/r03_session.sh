@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-3: GPU suite on the new claim policy; pipeline depth at an 8-rank share; host-side biased-list count A/B
+# round-3: GPU suite, bvh/mesh A/B against the pre-change build, full rehearsal on the final claim policy and tile deal
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -14,10 +14,6 @@ step() {
     return 0
 }
 step gpu_tests 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
-for rep in 1 2 3; do
-  for p in 1 2 3; do
-    CFGS="8,1" STEPS=60 SCALE_ARGS="--pipeline $p" step pipe_p${p}_$rep 300 bash tools/scale_rehearsal.sh
-  done
-done
-CFGS="7,2048,2048,64 0,1200,800,64 1,1200,800,64" LIBS="old" step ab_nbleaf 900 bash tools/ab_walk.sh
+CFGS="7,2048,2048,64 0,1200,800,64 1,1200,800,64 8,1024,1024,256 9,800,800,256" LIBS="old" step ab_final 900 bash tools/ab_walk.sh
+CFGS="1,0 2,0 2,1 4,0 4,1 4,2 4,3 8,0 8,1 8,2 8,3 8,4 8,5 8,6 8,7" STEPS=60 step scale_final 900 bash tools/scale_rehearsal.sh
 exit 0
