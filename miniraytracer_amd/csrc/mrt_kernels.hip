@@ -167,7 +167,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
         // the workgroup's copy of the top wide nodes (after every wave's own region), filled once
         // before any wave starts a path; no other barrier follows in this persistent kernel
         tree = reinterpret_cast<float4*>(lds + (TreeOf<F>::wg / 64u) * words);
-        for (uint32_t i = threadIdx.x; i < P.tree_n * 4u; i += blockDim.x) tree[i] = P.tree_src[i];
+        for (uint32_t i = threadIdx.x; i < P.tree_n * (MRT_BVH4 ? BVH4_Q : 4u); i += blockDim.x) tree[i] = P.tree_src[i];
         __syncthreads();
     }
     const LStack Ls{wb, (float*)(wb + P.lds_frames * 128), wmesh, (float*)(wmesh + P.lds_mesh * 64), lane, tree,

@@ -340,7 +340,7 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
             pc++;  // past the boundary op
             PH_MARK(ph, 10);
         } else if ((F & FT_BVHW) && op == LOP_BVHW) {
-            if (on && bvhw_hit<F>(S, S.nodes[o.node], cur, tmin, closest, rec, true, L)) {
+            if (on && bvhw_walk<F>(S, S.nodes[o.node], cur, tmin, closest, rec, true, L)) {
                 closest = rec.t;
                 hnode = o.node;
                 hinst = inst;

@@ -743,8 +743,66 @@ mrt_status mrt_internal_scene_tables(const mrt_scene_view* v, SceneTables* T) {
             if ((n.kind & 0xFF) == MRT_K_BVHW) broots.push_back(&n.a);
         bfs_order(bwide, broots, BVHW_LEAF);
     }
+    // the same subtrees as Bvh4 nodes (mrt_trace.h), breadth-first across all roots (the treelet
+    // holds the top levels); a BVHW node's b = its root Bvh4 node
+    std::vector<float4> bwide4;
+    {
+        const uint32_t nb = (uint32_t)bwide.size();
+        std::vector<uint32_t> id4(nb, MRT_NONE), order;
+        auto enq = [&](uint32_t c) -> uint32_t {
+            if (c & BVHW_LEAF) return c;
+            if (id4[c] == MRT_NONE) { id4[c] = (uint32_t)order.size(); order.push_back(c); }
+            return id4[c];
+        };
+        for (mrt_node& n : nodes)
+            if ((n.kind & 0xFF) == MRT_K_BVHW) n.b = enq(n.a);
+        for (size_t q = 0; q < order.size(); q++) {
+            const BvhWide W = bwide[order[q]];
+            float f[44] = {};
+            uint32_t ref[4] = {0, 0, 0, 0}, ord[3] = {W.order, 0xFFu, 0xFFu}, meta = 0;
+            if (W.flags & 1u) meta |= BVH4_A_BOX;
+            if (W.flags & 2u) meta |= BVH4_B_BOX;
+            if (W.lref == W.rref) meta |= BVH4_B_SAME;
+            for (int k = 0; k < 3; k++) {
+                f[0 + k] = W.lmin[k]; f[4 + k] = W.lmax[k]; f[8 + k] = W.rmin[k]; f[12 + k] = W.rmax[k];
+            }
+            for (int x = 0; x < 2; x++) {
+                const uint32_t X = x ? W.rref : W.lref;
+                if (X & BVHW_LEAF) {  // a leaf child: its first slot, no box of its own
+                    ref[2 * x] = X;
+                    meta |= BVH4_S_VALID(2 * x);
+                    continue;
+                }
+                const BvhWide C = bwide[X];
+                ord[1 + x] = C.order;
+                for (int y = 0; y < 2; y++) {
+                    const int k = 2 * x + y;
+                    if (y == 1 && C.rref == C.lref) continue;  // bvh_node of one object: visited once
+                    ref[k] = enq(y ? C.rref : C.lref);
+                    meta |= BVH4_S_VALID(k);
+                    if (C.flags & (1u << y)) {
+                        meta |= BVH4_S_BOX(k);
+                        for (int a = 0; a < 3; a++) {
+                            f[16 + 6 * k + a] = y ? C.rmin[a] : C.lmin[a];
+                            f[16 + 6 * k + 3 + a] = y ? C.rmax[a] : C.lmax[a];
+                        }
+                    }
+                }
+            }
+            uint32_t w[44];
+            memcpy(w, f, sizeof(w));
+            w[3] = ref[0]; w[7] = ref[1]; w[11] = ref[2]; w[15] = ref[3];
+            w[40] = ord[0]; w[41] = ord[1]; w[42] = ord[2]; w[43] = meta;
+            for (int k = 0; k < 11; k++) {
+                float4 v;
+                memcpy(&v, w + 4 * k, 16);
+                bwide4.push_back(v);
+            }
+        }
+    }
     GraphCheck gc{nodes, v};
-    gc.bvhw_depth = bvhw_depth;
+    // stack words: one per level for the binary walk, up to three per Bvh4 level
+    gc.bvhw_depth = std::max(bvhw_depth, 3 * ((bvhw_depth + 1) / 2) + 1);
     gc.walk(v->root, 0, 0, false, 0);
     if (!gc.ok) return mrt_internal_fail(MRT_ERR_INVALID, gc.why.c_str());
     if (v->biased != MRT_NONE) {
@@ -806,6 +864,7 @@ mrt_status mrt_internal_scene_tables(const mrt_scene_view* v, SceneTables* T) {
     T->nodes.swap(nodes);
     T->wide.swap(wide);
     T->bwide.swap(bwide);
+    T->bwide4.swap(bwide4);
     T->bprims.swap(bprims);
     T->dmats.swap(dmats);
     T->bleaf.swap(bleaf);
@@ -849,6 +908,7 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
 #endif
     S.mwide_n = (uint32_t)T.wide.size();
     UP(T.bwide.data(), T.bwide.size(), &S.bwide);
+    UP(T.bwide4.data(), T.bwide4.size(), &S.bwide4);
     UP(T.bprims.data(), T.bprims.size(), &S.bprims);
     UP((const float4*)v->tri_geo, (size_t)v->n_tris * 3, &S.tri_geo);
     UP((const float4*)v->tri_nrm, (size_t)v->n_tris * 3, &S.tri_nrm);
@@ -923,19 +983,23 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
         if (tabs[k]->tree[s->variant]) {
             // the LDS the resident groups leave free, split among them: the treelet of each group
             const size_t per = std::min<size_t>((160u * 1024u) / nb, (size_t)prop.sharedMemPerBlock);
-            uint32_t cap = per > L.lds_bytes ? (uint32_t)((per - L.lds_bytes) / 64u) : 0u;
+            const uint32_t node_bytes = MRT_BVH4 ? BVH4_Q * 16u : 64u;  // (Bvh4 / BvhWide)
+            const uint32_t n_nodes = MRT_BVH4 ? (uint32_t)(T.bwide4.size() / BVH4_Q) : (uint32_t)bwide.size();
+            uint32_t cap = per > L.lds_bytes ? (uint32_t)((per - L.lds_bytes) / node_bytes) : 0u;
 #ifdef MRT_EXPERIMENTS
             if (const char* e = getenv("MRT_TREELET_NODES"))  // sweep hook
                 if (*e) cap = std::min<uint32_t>(cap, (uint32_t)atoi(e));
 #endif
-            L.tree_n = std::min(cap, (uint32_t)bwide.size());
-            L.lds_bytes += (size_t)L.tree_n * 64u;
+            L.tree_n = std::min(cap, n_nodes);
+            L.lds_bytes += (size_t)L.tree_n * node_bytes;
         }
         if (tabs[k]->mtree[s->variant]) {
             // each wave's copy of the top mesh nodes, in the LDS its resident groups leave free
             // (so the treelet never costs occupancy)
             const size_t per = (160u * 1024u) / (size_t)nb;
-            uint32_t cap = per > L.lds_bytes ? (uint32_t)((per - L.lds_bytes) / 64u) : 0u;
+            const uint32_t node_bytes = MRT_BVH4 ? BVH4_Q * 16u : 64u;  // (Bvh4 / BvhWide)
+            const uint32_t n_nodes = MRT_BVH4 ? (uint32_t)(T.bwide4.size() / BVH4_Q) : (uint32_t)bwide.size();
+            uint32_t cap = per > L.lds_bytes ? (uint32_t)((per - L.lds_bytes) / node_bytes) : 0u;
 #ifdef MRT_EXPERIMENTS
             if (const char* e = getenv("MRT_MESH_TREE_NODES"))  // sweep hook
                 if (*e) cap = std::min<uint32_t>(cap, (uint32_t)atoi(e));
@@ -1167,7 +1231,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.lds_mesh = s->lds_mesh;
         P.lds_save = PL.lds_save;
         P.walk_min = s->walk_min;
-        P.tree_src = reinterpret_cast<const float4*>(s->S.bwide);
+        P.tree_src = MRT_BVH4 ? s->S.bwide4 : reinterpret_cast<const float4*>(s->S.bwide);
         P.tree_n = PL.tree_n;
         P.mtree_n = PL.mtree_n;
         P.pixels = s->d_pixels;

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-3: bf16 per-path radiance (tolerance contract): GPU suite, parity at every config, bench, 8-rank rehearsal
+# round-3: Bvh4 walk (two bvh_node levels per visit) against the binary walk; GPU suite
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -14,7 +14,7 @@ step() {
     return 0
 }
 step gpu_tests 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
-step parity 600 python tools/parity_record.py --numerics fast
-step bench 600 python bench.py --no-cpu-baseline --no-other-walk --steps 20 --warmup 5
-CFGS="1,0 8,0 8,1 8,2 8,3 8,4 8,5 8,6 8,7" STEPS=60 step scale_bf16 900 bash tools/scale_rehearsal.sh
+for rep in 1 2; do
+  CFGS="7,2048,2048,64 0,1200,800,64 1,1200,800,64 5,500,500,1024" LIBS="bin" step ab_bvh4_$rep 900 bash tools/ab_walk.sh
+done
 exit 0
