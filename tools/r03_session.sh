@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-3: Bvh4 walk (two bvh_node levels per visit) against the binary walk; GPU suite
+# round-3: per-wave mesh treelet again, now read with LDS instructions
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -13,8 +13,7 @@ step() {
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
     return 0
 }
-step gpu_tests 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
 for rep in 1 2; do
-  CFGS="7,2048,2048,64 0,1200,800,64 1,1200,800,64 5,500,500,1024" LIBS="bin" step ab_bvh4_$rep 900 bash tools/ab_walk.sh
+  CFGS="8,1024,1024,256 9,800,800,256" LIBS="mtree" step ab_mtree_$rep 900 bash tools/ab_walk.sh
 done
 exit 0
