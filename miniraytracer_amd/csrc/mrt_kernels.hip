@@ -425,7 +425,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
             PH_MARK(ph, 1);
             if (w.st == RS_DONE) {
                 const bool hit = rs_finish_hit<F>(S, w, ps.r, rec, Ls);
-                f3 L;
+                f3 L{0.0f, 0.0f, 0.0f};
                 const bool ended = shade_hit<F, LK>(S, ps, P.max_bounces, lev, hit, rec, &L, ph);
                 PH_MARK(ph, 2);
                 if (ended) {
@@ -443,7 +443,6 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
         // make_ray for every lane with a next ray -- camera and scattered rays alike, instead of one
         // constructor per branch at partial lane occupancy; (4) diffuse scatters finish their pdfs
         // on the new ray.
-        PendRay pr;
         uint32_t q_head = 0, q_n = 0;  // wave-uniform: the queue's next entry, its valid entries
         // The radiance store of a path that ended is held in registers and issued in the NEXT
         // iteration, after the hit, beside the material load: the code waits for the vector memory
@@ -456,8 +455,11 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
         bool st_pend = false;
         for (;;) {
             bool want_ray = false;
+            // the next ray's arguments: written and read within one iteration (declared here, a
+            // field a branch leaves unset is dead, not carried round the loop in copied registers)
+            PendRay pr;
             if (active) {
-                f3 L;
+                f3 L{0.0f, 0.0f, 0.0f};  // (left undefined, it was carried round the loop in copied registers)
                 // (the held store is issued inside, after the hit, beside the material load)
                 const bool ended = trace_split<F, LK>(S, ps, P.max_bounces, lev, Ls, &L, &pr, ph, [&]() {
                     if (st_pend) {
@@ -638,7 +640,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
             PH_MARK(ph, 6);
             if (phase == PH_DONE) {
                 if (!w.hdone && w.hnode != MRT_NONE) W::template derive<0>(prog, w, ps.r, ps.r, rec);
-                f3 L;
+                f3 L{0.0f, 0.0f, 0.0f};
                 const bool ended = shade_hit<F, LK>(S, ps, P.max_bounces, lev, w.hnode != MRT_NONE, rec, &L, ph);
                 PH_MARK(ph, 2);
                 phase = PH_BEGIN;
@@ -655,7 +657,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
             if (!__any(active)) break;
             PH_MARK(ph, 0);
             if (active) {
-                f3 L;
+                f3 L{0.0f, 0.0f, 0.0f};
                 const bool ended = trace_segment<F, LK>(S, ps, P.max_bounces, lev, Ls, &L, ph);
                 PH_MARK(ph, 2);
                 if (ended) finish_path(L);

@@ -997,8 +997,7 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
             // each wave's copy of the top mesh nodes, in the LDS its resident groups leave free
             // (so the treelet never costs occupancy)
             const size_t per = (160u * 1024u) / (size_t)nb;
-            const uint32_t node_bytes = MRT_BVH4 ? BVH4_Q * 16u : 64u;  // (Bvh4 / BvhWide)
-            const uint32_t n_nodes = MRT_BVH4 ? (uint32_t)(T.bwide4.size() / BVH4_Q) : (uint32_t)bwide.size();
+            const uint32_t node_bytes = 64u;  // MeshWide
             uint32_t cap = per > L.lds_bytes ? (uint32_t)((per - L.lds_bytes) / node_bytes) : 0u;
 #ifdef MRT_EXPERIMENTS
             if (const char* e = getenv("MRT_MESH_TREE_NODES"))  // sweep hook

@@ -479,6 +479,13 @@ MRT_DFN bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, c
     pr->time = r.time;
     pr->inside = 0;
     pr->kind = 0;
+    // the diffuse scatter's attenuation and normal, set on every branch: set only on the diffuse one,
+    // the merge after the material branches cost a register copy of each on every path
+    constexpr bool kAttEarly = (F & FT_TEX) == 0;  // (a constant colour: no texture lookup wasted)
+    if constexpr (kAttEarly) {
+        pr->att = mat_color<F>(S, M, rec);
+        pr->n = rec.n;
+    }
     if ((F & FT_METAL) && M.kind == MRT_M_METAL) {  // metal::scatter (material.h:91-98)
         f3 reflected = sub(r.d, fmul(2.0f * dot(r.d, rec.n), rec.n));
         f3 rs = random_in_sphere(ps.rng);
@@ -526,8 +533,10 @@ MRT_DFN bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, c
     }
     // lambertian / isotropic (material.h:48-74): the direction now, the pdfs after the ray exists
     const bool lamb = !(F & FT_ISO) || M.kind == MRT_M_LAMBERTIAN;
-    pr->att = mat_color<F>(S, M, rec);
-    pr->n = rec.n;
+    if constexpr (!kAttEarly) {
+        pr->att = mat_color<F>(S, M, rec);
+        pr->n = rec.n;
+    }
     pr->kind = lamb ? 1u : 2u;
     BSTAT(6);
     const bool light = ((F & FT_BIASED) && S.biased != MRT_NONE) && randf(ps.rng) < 0.5f;
