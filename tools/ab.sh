@@ -15,14 +15,7 @@ for r in $(seq 1 "${ROUNDS:-2}"); do
       log=gpurun_out/ab_${tag}_${sid}_$r.log
       MRT_EXPERIMENT_LIB=$lib timeout -k 10 300 python bench.py --no-cpu-baseline --no-compare-numerics --no-other-walk \
           --no-parity --steps "$STEPS" --warmup 2 --scene "$sid" --width "$W" --height "$H" --samples "$S" ${BENCH_ARGS:-} > "$log" 2>&1 || exit 3
-      python - "$log" "$tag" "$sid" "$r" <<'EOF'
-import json, sys
-line = [l for l in open(sys.argv[1]) if l.startswith("{")][-1]
-d = json.loads(line)
-rf = d.get("roofline", {})
-print(f"{sys.argv[2]:>12} scene {sys.argv[3]} round {sys.argv[4]}: {d['ms_per_step']:.3f} ms/step, "
-      f"kernel {rf.get('kernel_ms')} ms, {d['value']:.0f} {d['unit']}")
-EOF
+      python tools/show_bench.py "$log" "$tag scene $sid round $r"
     done
   done
 done
