@@ -16,7 +16,8 @@ HIPDEV   = -mllvm -disable-promote-alloca-to-vector -mllvm -structurizecfg-skip-
 CSRC     = miniraytracer_amd/csrc
 OBJDIR   = build/obj
 
-LIB_OBJS = $(OBJDIR)/mrt_render.o $(OBJDIR)/mrt_kernels_exact.o $(OBJDIR)/mrt_kernels_fast.o $(OBJDIR)/mrt_cpu.o $(OBJDIR)/scene_builder.o $(OBJDIR)/mrt_common.o
+LIB_OBJS = $(OBJDIR)/mrt_render.o $(OBJDIR)/mrt_kernels_exact.o $(OBJDIR)/mrt_kernels_fast.o $(OBJDIR)/mrt_kernels_fastz.o \
+           $(OBJDIR)/mrt_cpu.o $(OBJDIR)/scene_builder.o $(OBJDIR)/mrt_common.o
 # the path kernels twice: exact contract (no contraction, IEEE division) and tolerance contract
 # (FMA contraction, reciprocal division, hardware rcp/sqrt/rsq, f32 transcendentals)
 # (-fno-hip-fp32-correctly-rounded-divide-sqrt: f32 division by v_rcp_f32 + multiply instead of
@@ -33,6 +34,13 @@ $(OBJDIR)/mrt_kernels_exact.o: $(CSRC)/mrt_kernels.hip $(HDRS)
 $(OBJDIR)/mrt_kernels_fast.o: $(CSRC)/mrt_kernels.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(HIPDEV) $(FASTFLAGS) -c $< -o $@
+
+# the tolerance contract again with f32 denormals flushed, for the variants mrt_launch.h's
+# kFtzVariant selects (the others are not instantiated in it)
+FTZFLAGS = -fgpu-flush-denormals-to-zero -DMRT_TABLE_FTZ=1
+$(OBJDIR)/mrt_kernels_fastz.o: $(CSRC)/mrt_kernels.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) $(HIPDEV) $(FASTFLAGS) $(FTZFLAGS) -c $< -o $@
 
 # the CPU backend: the same hot-path headers compiled for the host only (exact contract)
 $(OBJDIR)/mrt_cpu.o: $(CSRC)/mrt_cpu.hip $(HDRS)

@@ -115,8 +115,9 @@ def _cpu_quota():
 
 
 def cpu_baseline(args):
-    """The reference as shipped (multithreaded work_queue, mode 1, atomic ray counter) on this
-    host, over a bounded sample of the same scene; its own Mrays/s formula (main.cpp:403-405).
+    """The reference as shipped (multithreaded work_queue, atomic ray counter) on this host, over a
+    bounded sample of the same scene, in the GPU leg's accumulation mode (-mode 0: draw(), the
+    bench's render; the reference's default is draw2); its own Mrays/s formula (main.cpp:403-405).
     Timed twice: with as many threads as this process may use (affinity / cgroup quota) and with
     -threads = os.cpu_count() (every CPU the machine reports; on a shared GPU box that is more than
     the box's share, so the two differ)."""
@@ -125,12 +126,12 @@ def cpu_baseline(args):
     quota = _cpu_quota()
     used = int(os.environ.get("MRT_CPU_THREADS", quota))
     sample = (f"scene {args.scene}, {args.width}x{args.height}, {args.cpu_spp} spp (of {args.samples}), "
-              f"depth {args.depth}, -mode 1")
+              f"depth {args.depth}, -mode 0 (draw(), as the GPU leg)")
     b = oracle.ref_binary(exact=False)
     if b is not None:
         def run(threads):
             return oracle.run_ref(["-scene", args.scene, "-width", args.width, "-height", args.height, "-samples",
-                                   args.cpu_spp, "-depth", args.depth, "-threads", threads], exact=False, timeout=900)
+                                   args.cpu_spp, "-depth", args.depth, "-threads", threads, "-mode", 0], exact=False, timeout=900)
         r = run(used)
         res = {"value": round(r["mrays_per_s"], 3), "unit": "Mrays/s", "cores": used, "cores_used": used,
                "cores_total": total, "cores_quota": quota, "kind": "reference",
@@ -164,8 +165,13 @@ def roofline(args, k_ms, rays_per_launch, numerics, kinfo):
     WRITE_SIZE, MI355X_MICROARCH.md) -> hbm_frac.  Per-ray figures, so a rank's share (world > 1)
     is priced by its own rays; they do not depend on spp."""
     k_s = k_ms * 1e-3
+    # the kernel's name in rocprofv3 traces: the tolerance contract's variants without volumes run
+    # the denormal-flushing build (mrt_launch.h kFtzVariant; MRT_FTZ=0 turns it off)
+    FT_VOLUME = 1 << 2
+    ftz = numerics == "fast" and not (kinfo["kernel_features"] & FT_VOLUME) and os.environ.get("MRT_FTZ", "1") != "0"
+    kname = "mrt_path_kernel" + (("_fastz" if ftz else "_fast") if numerics == "fast" else "")
     out = {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_G, 1), "unit": "G VALU wave-instr/s", "frac": None,
-           "traffic": None, "kernel": "mrt_path_kernel" + ("_fast" if numerics == "fast" else ""), "kernel_ms": round(k_ms, 3),
+           "traffic": None, "kernel": kname, "kernel_ms": round(k_ms, 3),
            "rays_per_launch": int(rays_per_launch),
            **{k: kinfo[k] for k in ("grid", "wg", "lds_bytes", "vgprs", "tree_nodes")}}
     b_ray = B_RAY.get(args.scene)

@@ -21,7 +21,14 @@ using namespace mrtd;
 #ifndef MRT_TABLE_FAST
 #define MRT_TABLE_FAST MRT_FAST
 #endif
-#if MRT_TABLE_FAST
+// the third build: the tolerance contract with f32 denormals flushed (-fgpu-flush-denormals-to-zero),
+// for the variants kFtzVariant selects (mrt_launch.h)
+#ifndef MRT_TABLE_FTZ
+#define MRT_TABLE_FTZ 0
+#endif
+#if MRT_TABLE_FTZ
+#define MRT_PATH_KERNEL mrt_path_kernel_fastz
+#elif MRT_TABLE_FAST
 #define MRT_PATH_KERNEL mrt_path_kernel_fast
 #else
 #define MRT_PATH_KERNEL mrt_path_kernel
@@ -627,7 +634,16 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
             // at least one step per iteration for every walking lane (no lane starves), then more
             // while enough lanes walk or too few have anything else to do
             while (__any(phase == PH_WALK)) {
-                if (phase == PH_WALK) {
+                bool step = phase == PH_WALK;
+                if (P.leaf_min) {
+                    // leaves postponed: a lane holding a leaf waits while other lanes still descend,
+                    // until leaf_min lanes hold one (or none descends), so the triangle test runs
+                    // with more lanes at once instead of beside every inner-node step
+                    const bool leafy = step && (ref & MESH_LEAF) != 0u;
+                    const uint32_t nl = (uint32_t)__popcll(__ballot(leafy)), nw = (uint32_t)__popcll(__ballot(step));
+                    if (nl < P.leaf_min && nl < nw) step = step && !leafy;
+                }
+                if (step) {
                     const mrt_node mn = ld_node(const_ptr(S.nodes) + prog[kMeshPC].node);
                     const uint32_t st = mesh_step<MeshTreeOf<F>::on>(S, mn, ps.r, 0.001f, w.closest, rec, Ls, ref, msp, w.hdone);
                     if (st == 1u) w.hnode = kMeshPC;  // w.closest = the hit's t, w.hdone set
@@ -692,10 +708,18 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
 
 template <uint32_t F>
 static constexpr path_kernel_t kfn() {
+#if MRT_TABLE_FTZ
+    if constexpr (!kFtzVariant<F>) return nullptr;  // (not instantiated: the plain fast build runs it)
+    else
+#endif
     return MRT_PATH_KERNEL<F>;
 }
 
-#if MRT_TABLE_FAST
+#if MRT_TABLE_FTZ
+const KernelTable& mrtd::kernel_table_fast_ftz() {
+    static const KernelTable t = {
+        "fast",
+#elif MRT_TABLE_FAST
 const KernelTable& mrtd::kernel_table_fast() {
     static const KernelTable t = {
         "fast",

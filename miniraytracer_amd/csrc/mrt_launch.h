@@ -41,6 +41,7 @@ struct PathParams {
     uint32_t lev_rows;                    // levels per lane (max_bounces, at least 1)
     uint32_t lds_frames, lds_rays, lds_mesh, lds_save;  // LDS stack slots / words per lane
     uint32_t walk_min;                    // resumable mesh walk: yield once at most this many lanes walk
+    uint32_t leaf_min;                    // ... and its leaves wait until this many lanes hold one (0: off)
     const float4* tree_src;               // TreeOf<F>::on kernels: BvhWide nodes copied to LDS at start
     uint32_t tree_n;                      // how many (the first tree_n of the breadth-first array)
     uint32_t mtree_n;                     // MeshTreeOf<F>::on kernels: MeshWide nodes each wave copies to its LDS
@@ -98,5 +99,17 @@ struct KernelTable {
 };
 const KernelTable& kernel_table_exact();
 const KernelTable& kernel_table_fast();
+// Tolerance-contract variants built with f32 denormals flushed to zero (a third build of the path
+// kernels, mrt_kernels_fastz.o; DESIGN.md "Numerics contracts"): the denormal-safe reciprocal /
+// sqrt sequences become single instructions.  Measured per variant (tools/ab.sh, kernel time):
+// Cornell (C2) -1.0%, room + mesh -0.3..-0.4%, sky-lit bvh_node scenes -0.4%; book2 (volumes) +0.9%,
+// so the variants with volumes keep the plain fast build.
+#ifndef MRT_FAST_FTZ
+#define MRT_FAST_FTZ 1
+#endif
+template <uint32_t F>
+static constexpr bool kFtzVariant = MRT_FAST_FTZ && (F & FT_VOLUME) == 0;
+// the FTZ build's table: a kernel for the kFtzVariant variants, null for the others
+const KernelTable& kernel_table_fast_ftz();
 
 }  // namespace mrtd

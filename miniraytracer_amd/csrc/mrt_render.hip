@@ -36,6 +36,22 @@ using namespace mrtd;
         if (e_ != hipSuccess) return mrt_internal_fail(MRT_ERR_HIP, (std::string(#x) + ": " + hipGetErrorString(e_)).c_str()); \
     } while (0)
 
+// The tolerance contract's kernels: the plain fast build, with the kFtzVariant variants taken
+// from the denormal-flushing build (mrt_launch.h); MRT_FTZ=0 in the environment keeps the plain
+// build for every variant (A/B).
+static const KernelTable& fast_table() {
+    static const KernelTable t = [] {
+        KernelTable m = kernel_table_fast();
+        const char* e = getenv("MRT_FTZ");
+        if (e && *e && atoi(e) == 0) return m;
+        const KernelTable& z = kernel_table_fast_ftz();
+        for (uint32_t i = 0; i < kNumVariants; i++)
+            if (z.kernel[i]) m.kernel[i] = z.kernel[i];
+        return m;
+    }();
+    return t;
+}
+
 // first variant covering the scene's features: its own program shape first, then the interpreter
 static uint32_t pick_variant(uint32_t features) {
     const uint32_t feat = features & 0xFFFFu, sig = MRT_SIG_OF(features);
@@ -312,6 +328,7 @@ struct mrt_scene {
     uint32_t features = 0, variant = 0;
     uint32_t lds_frames = 0, lds_rays = 0, lds_mesh = 0, lds_save = 0;
     uint32_t walk_min = 32;  // resumable mesh walk threshold (PathParams::walk_min)
+    uint32_t leaf_min = 0;   // its leaf postponement (PathParams::leaf_min)
     PathLaunch pl[2];            // [0] exact contract, [1] tolerance contract (MRT_RF_FAST)
     size_t max_threads = 0;  // largest path-kernel grid in threads (per-lane level rows)
     std::vector<hipEvent_t> ev;  // [2*k]: start/stop of path-kernel launch k of the last render
@@ -951,6 +968,11 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     s->walk_min = T.wide.size() >= 2048 ? 40u : 32u;  // inner nodes: bunny 2937, teapot ~1045
     if (const char* e = getenv("MRT_WALK_MIN"))  // sweep hook (tools/ab_walk.sh)
         if (*e) s->walk_min = (uint32_t)atoi(e);
+    // leaves postponed (off): at 16 lanes bunny +1.6% in one session, +-0.3% in the next; teapot
+    // -4%; 8 lanes -2% / -3% (profiles/r03_ab_session2.txt)
+    s->leaf_min = 0u;
+    if (const char* e = getenv("MRT_LEAF_MIN"))  // sweep hook
+        if (*e) s->leaf_min = (uint32_t)atoi(e);
     const std::vector<BvhWide>& bwide = T.bwide;
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
@@ -958,7 +980,7 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     // a quarter of that); VGPRs (512 per SIMD lane, granule 8) and LDS (160 KiB per CU) bound it.
     // (The runtime occupancy query under-counts gfx950 register budgets, so it is computed from
     // the kernel's attributes.)  Per numerics build: their register counts differ.
-    const KernelTable* tabs[2] = {&kernel_table_exact(), &kernel_table_fast()};
+    const KernelTable* tabs[2] = {&kernel_table_exact(), &fast_table()};
     for (int k = 0; k < 2; k++) {
         PathLaunch& L = s->pl[k];
         L.fn = tabs[k]->kernel[s->variant];
@@ -1230,6 +1252,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.lds_mesh = s->lds_mesh;
         P.lds_save = PL.lds_save;
         P.walk_min = s->walk_min;
+        P.leaf_min = s->leaf_min;
         P.tree_src = MRT_BVH4 ? s->S.bwide4 : reinterpret_cast<const float4*>(s->S.bwide);
         P.tree_n = PL.tree_n;
         P.mtree_n = PL.mtree_n;

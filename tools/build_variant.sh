@@ -13,6 +13,9 @@ make -s build/obj/scene_builder.o build/obj/mrt_common.o build/obj/mrt_render.o 
 mkdir -p exp/obj_$tag
 BASE="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-fast-math -fno-slp-vectorize -w -mllvm -disable-promote-alloca-to-vector -mllvm -structurizecfg-skip-uniform-regions -DMRT_EXPERIMENTS"
 /opt/rocm/bin/hipcc $BASE -DMRT_TABLE_FAST=1 $flags -c miniraytracer_amd/csrc/mrt_kernels.hip -o exp/obj_$tag/mrt_kernels_fast.o
+# the denormal-flushing build of the same flags (the kFtzVariant variants; run with MRT_FTZ=0 to A/B
+# without it)
+/opt/rocm/bin/hipcc $BASE -DMRT_TABLE_FAST=1 $flags -fgpu-flush-denormals-to-zero -DMRT_TABLE_FTZ=1 -c miniraytracer_amd/csrc/mrt_kernels.hip -o exp/obj_$tag/mrt_kernels_fastz.o
 EX=build/obj/mrt_kernels_exact.o
 # host defines (MRT_NPART, MRT_BATCH, ...) change PathParams / the claim protocol: the exact TU must
 # be built with them too, or the exact kernel reads a foreign parameter layout (a GPU memory fault)
@@ -26,6 +29,6 @@ if [ -n "${HOST_FLAGS:-}" ]; then  # host TU too (e.g. -DMRT_PATH_WG=..., which 
   /opt/rocm/bin/hipcc $BASE -ffp-contract=off $HOST_FLAGS -c miniraytracer_amd/csrc/mrt_render.hip -o exp/obj_$tag/mrt_render.o
   RO=exp/obj_$tag/mrt_render.o
 fi
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $RO $EX exp/obj_$tag/mrt_kernels_fast.o \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $RO $EX exp/obj_$tag/mrt_kernels_fast.o exp/obj_$tag/mrt_kernels_fastz.o \
     build/obj/mrt_cpu.o build/obj/scene_builder.o build/obj/mrt_common.o -ldl -o exp/libmrt_$tag.so
 echo "built exp/libmrt_$tag.so"
