@@ -168,7 +168,7 @@ def roofline(args, k_ms, rays_per_launch, numerics, kinfo):
     # the kernel's name in rocprofv3 traces: the tolerance contract's variants without volumes run
     # the denormal-flushing build (mrt_launch.h kFtzVariant; MRT_FTZ=0 turns it off)
     FT_VOLUME = 1 << 2
-    ftz = numerics == "fast" and not (kinfo["kernel_features"] & FT_VOLUME) and os.environ.get("MRT_FTZ", "1") != "0"
+    ftz = numerics == "fast" and not (kinfo.get("kernel_features", 0) & FT_VOLUME) and os.environ.get("MRT_FTZ", "1") != "0"
     kname = "mrt_path_kernel" + (("_fastz" if ftz else "_fast") if numerics == "fast" else "")
     out = {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_G, 1), "unit": "G VALU wave-instr/s", "frac": None,
            "traffic": None, "kernel": kname, "kernel_ms": round(k_ms, 3),
