@@ -66,8 +66,9 @@ def parse():
                          "vs the reference as shipped, tests/test_gpu_parity.py), exact = bit-for-bit the reference "
                          "built exact; the other one is timed too and reported as other_numerics")
     ap.add_argument("--no-compare-numerics", action="store_true")
-    ap.add_argument("--kernel-reps", type=int, default=3,
-                    help="extra renders after the timed region whose HIP-event kernel time feeds roofline")
+    ap.add_argument("--kernel-reps", type=int, default=0,
+                    help="ignored (kept for old command lines): the roofline's kernel time is now the HIP-event "
+                         "time of the timed steps' own launches")
     ap.add_argument("--emulate-world", type=int, default=1,
                     help="single-GPU rehearsal: render only rank --emulate-rank's share of an N-rank job "
                          "(no collectives); used to predict per-rank step time at N GPUs")
@@ -382,9 +383,12 @@ def main():
         if rank == 0:
             print(f"bench.py: {msg} ({time.strftime('%H:%M:%S')})", file=sys.stderr, flush=True)
 
+    live = [None]  # (path-kernel ms per launch, launches per render) of the last measure()
+
     def measure(d):
         """W untimed warmup steps, then EXACTLY K steps between barrier + synchronize on both
-        sides; (max-over-ranks seconds, total rays of all ranks, this rank's rays per step)."""
+        sides; (max-over-ranks seconds, total rays of all ranks, this rank's rays per step); the
+        path kernel's HIP-event time of the timed steps in live[0]."""
         note(f"measuring numerics={'fast' if d.flags & m._lib.RF_FAST else 'exact'}")
         # setup, untimed: one render per context, so every context's first-use costs (workspace
         # first touch, first launch on its stream) are paid before the warmup steps
@@ -418,6 +422,12 @@ def main():
         if world > 1:
             dist.barrier()
         t1 = time.perf_counter()
+        # the path kernel's time inside the timed region: HIP events recorded around each launch on
+        # its stream by the library, read for every context's last timed render (reading them here,
+        # before any untimed work, keeps the clocks of the timed region: renders timed after the
+        # parity check ran on a GPU that had idled for seconds, 8.6-9.0 ms against 8.0 ms)
+        kl = [c.kernel_ms() for c in ctx[0][:min(npipe, max(args.steps, 1))]]
+        live[0] = (float(np.mean([ms / max(n, 1) for ms, n in kl])), max(kl[0][1], 1))
         elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
         total_rays = rays.clone()
         if world > 1:
@@ -461,17 +471,8 @@ def main():
         verified = bool(np.array_equal(img[..., :3].view(np.uint32), ref[..., :3].view(np.uint32))
                         and nrays == ref_rays * args.steps)
 
-    # dominant kernel: mrt_path_kernel, HIP events recorded on the launch stream (extra renders)
-    def kernel_ms(d, r=None):
-        r = r or rnd
-        kms = []
-        for _ in range(max(args.kernel_reps, 1)):
-            r.render_device(d, out.data_ptr(), rays.data_ptr(), stream.cuda_stream)
-            ms, launches = r.kernel_ms()
-            kms.append(ms / max(launches, 1))
-        return float(np.mean(kms)), max(launches, 1)
-
-    k_ms, launches = kernel_ms(desc)
+    # dominant kernel: mrt_path_kernel, HIP events of the timed steps (measure())
+    k_ms, launches = live[0]
     roof = roofline(args, k_ms, rays_per_step_local / launches, args.numerics, rnd.kernel_info())
 
     # the other numerics contract, same protocol (reported beside the headline, never as `value`)
@@ -479,8 +480,8 @@ def main():
     if not args.no_compare_numerics:
         alt = "exact" if args.numerics == "fast" else "fast"
         a_secs, a_rays, a_local = measure(desc_of(alt))
+        a_kms, a_launches = live[0]
         a_par = parity(a_rays)
-        a_kms, a_launches = kernel_ms(desc_of(alt))
         a_roof = roofline(args, a_kms, a_local / a_launches, alt, rnd.kernel_info())
         other = {"numerics": alt, "value": round(a_rays / a_secs / 1e6, 2), "ms_per_step": round(a_secs / args.steps * 1e3, 3),
                  "kernel_ms": round(a_kms, 3), "roofline_frac": a_roof["frac"], "valu_lane_util": a_roof.get("valu_lane_util"),
@@ -500,9 +501,9 @@ def main():
             r.prepare(desc)
         ctx[0] = gen
         g_secs, g_rays, g_local = measure(desc)
+        g_kms, g_launches = live[0]
         g_par = parity(g_rays)
         ctx[0] = rnds
-        g_kms, g_launches = kernel_ms(desc, gen[0])
         g_roof = roofline(args, g_kms, g_local / g_launches, args.numerics, gen[0].kernel_info())
         other_walk = {"walk": "linear-program interpreter (MRT_NO_SIG=1)", "numerics": args.numerics,
                       "kernel_features": gen[0].kernel_info()["kernel_features"],

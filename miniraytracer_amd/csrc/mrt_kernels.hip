@@ -1,11 +1,13 @@
-// mrt_kernels.hip -- the path kernel (DESIGN.md "Kernels"), built twice from this one source:
+// mrt_kernels.hip -- the path kernel (DESIGN.md "Kernels"), built three times from this one source:
 //   build/obj/mrt_kernels_exact.o  MRT_FAST=0, -ffp-contract=off: the exact numerics contract,
 //                                  bit-for-bit the reference built exact (tests/golden/stream_*.npz)
 //   build/obj/mrt_kernels_fast.o   MRT_FAST=1, FMA contraction + reciprocal division + hardware
 //                                  rcp/sqrt/rsq + f32 transcendentals: the tolerance contract
 //                                  (per-pixel RMSE < 1e-3 vs the reference as shipped)
+//   build/obj/mrt_kernels_fastz.o  the tolerance contract with f32 denormals flushed, for the
+//                                  variants mrt_launch.h's kFtzVariant selects
 // Each build exports its KernelTable (mrt_launch.h); the host picks one per render
-// (mrt_render_desc.flags & MRT_RF_FAST).
+// (mrt_render_desc.flags & MRT_RF_FAST), the fast one merged with the FTZ build's variants.
 //
 // mrt_path_kernel: persistent waves pull 256-path batches (64 near the end of a launch) from
 // per-XCD partition counters (one atomic per wave per batch, like work_queue::getWork pulls a tile,
