@@ -390,7 +390,9 @@ MRT_DFN void cornell_take1(CornellRoom& d) {
 // through the face of its smallest far-plane distance; that face, if the room has it, is the
 // wall hit (front-facing: the walls face inward; any face the ray crosses going in is back-facing
 // and missed, rect.cpp:26-30).  Differs from the five rect tests by rounding at the room's edges.
-template <uint32_t F>
+// (kRec false: the caller reads only the hit's code, distance and side -- room_walls_op -- so the
+// face's plane and material are not selected: sel3's asm would keep the dead selects alive)
+template <uint32_t F, bool kRec = true>
 MRT_DFN void cornell_room(const CornellRoom& d, const Ray& r, float tmin, CornellRec& w) {
     const float lo0 = __uint_as_float(d.lo0), lo1 = __uint_as_float(d.lo1), lo2 = __uint_as_float(d.lo2);
     const float hi0 = __uint_as_float(d.hi0), hi1 = __uint_as_float(d.hi1), hi2 = __uint_as_float(d.hi2);
@@ -409,15 +411,17 @@ MRT_DFN void cornell_room(const CornellRoom& d, const Ray& r, float tmin, Cornel
     const bool h = (tn <= tf) & (((d.mask >> face) & 1u) != 0u) & (tf >= tmin) & (tf <= w.closest);
     // plane and material of the face by selects (a chain of compares with one index became a
     // per-lane lookup table in scratch memory)
-    const bool up = side != 0u;
-    const float k = up ? sel3(a, hi0, hi1, hi2) : sel3(a, lo0, lo1, lo2);
-    const uint32_t m = __float_as_uint(up ? sel3(a, __uint_as_float(d.m1), __uint_as_float(d.m3), __uint_as_float(d.m5))
-                                          : sel3(a, __uint_as_float(d.m0), __uint_as_float(d.m2), __uint_as_float(d.m4)));
     w.closest = h ? tf : w.closest;
     w.code = h ? 1u + a : w.code;
-    w.k = h ? k : w.k;
     w.ns = h ? (side ? -1.0f : 1.0f) : w.ns;
-    w.mat = h ? m : w.mat;
+    if constexpr (kRec) {
+        const bool up = side != 0u;
+        const float k = up ? sel3(a, hi0, hi1, hi2) : sel3(a, lo0, lo1, lo2);
+        const uint32_t m = __float_as_uint(up ? sel3(a, __uint_as_float(d.m1), __uint_as_float(d.m3), __uint_as_float(d.m5))
+                                              : sel3(a, __uint_as_float(d.m0), __uint_as_float(d.m2), __uint_as_float(d.m4)));
+        w.k = h ? k : w.k;
+        w.mat = h ? m : w.mat;
+    }
 }
 // The room + mesh walk's walls (scenes 8 / 9, tolerance build): the room's slab test as above,
 // the hit face's op index as the hit op (the record is then derived op by op, SigWalk::derive)
@@ -429,7 +433,7 @@ MRT_DFN void room_walls_op(const MRT_CONST_AS LinOp& e, const Ray& r, float tmin
 #endif
     cornell_take1(d);
     CornellRec c{w.closest, 0.0f, 0.0f, 0u, 0u};
-    cornell_room<0u>(d, r, tmin, c);
+    cornell_room<0u, false>(d, r, tmin, c);
     if (c.code != 0u) {  // per lane: the exit face's axis from the code, its side from the sign
         const uint32_t face = (c.code - 1u) * 2u + (c.ns < 0.0f ? 1u : 0u);
         w.closest = c.closest;
