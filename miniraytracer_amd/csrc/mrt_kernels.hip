@@ -647,7 +647,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                 }
                 if (step) {
                     const mrt_node mn = ld_node(const_ptr(S.nodes) + prog[kMeshPC].node);
-                    const uint32_t st = mesh_step<MeshTreeOf<F>::on>(S, mn, ps.r, 0.001f, w.closest, rec, Ls, ref, msp, w.hdone);
+                    const uint32_t st = mesh_step<MeshTreeOf<F>::on, true>(S, mn, ps.r, 0.001f, w.closest, rec, Ls, ref, msp, w.hdone);
                     if (st == 1u) w.hnode = kMeshPC;  // w.closest = the hit's t, w.hdone set
                     phase = st != 0u ? PH_DONE : PH_WALK;
                 }
@@ -657,7 +657,12 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
             }
             PH_MARK(ph, 6);
             if (phase == PH_DONE) {
-                if (!w.hdone && w.hnode != MRT_NONE) W::template derive<0>(prog, w, ps.r, ps.r, rec);
+                if (w.hnode == kMeshPC) {  // the mesh's record, deferred by the walk (mesh_step<.., true>)
+                    const mrt_node mn = ld_node(const_ptr(S.nodes) + prog[kMeshPC].node);
+                    mesh_hit_rec(S, mn, ps.r, w.closest, rec);
+                } else if (!w.hdone && w.hnode != MRT_NONE) {
+                    W::template derive<0>(prog, w, ps.r, ps.r, rec);
+                }
                 f3 L{0.0f, 0.0f, 0.0f};
                 const bool ended = shade_hit<F, LK>(S, ps, P.max_bounces, lev, w.hnode != MRT_NONE, rec, &L, ph);
                 PH_MARK(ph, 2);

@@ -560,9 +560,48 @@ MRT_DFN bool mesh_hit(const DScene& S, const mrt_node& n, const Ray& r, float tm
 // triangles) and lanes at inner nodes cost about the same per step.  Returns 0: keep walking,
 // 1: hit (rec complete, tt = its t; the walk is over: first-hit early-out), 2: no hit.  Every lane
 // performs mesh_hit's operations in mesh_hit's order: the results are bit-identical.
-template <bool TREE = false>
+// DEFER: on a hit, return 1 with the record's triangle (rec.mat), barycentrics (rec.u, rec.v) and
+// tt only -- mesh_hit_rec completes it once the walk is over.  Completed inside the step, the point
+// and normal were carried round every walk step of the wave (the compiler copied all six registers
+// in and out of each step's branches).
+template <bool TREE = false, bool DEFER = false>
 MRT_DFN uint32_t mesh_step(const DScene& S, const mrt_node& n, const Ray& r, float tmin, float& tt, HitRec& rec,
                                               const LStack& L, uint32_t& ref, uint32_t& msp, bool& in_hit) {
+    if constexpr (DEFER) {
+        // the same step with the walk state updated by selects where mesh_step branches and
+        // returns: each branch's results otherwise merged in copies of every state register
+        uint32_t res = 0u;
+        bool pop;
+        if (ref & MESH_LEAF) {
+            const uint32_t first = ref & 0xFFFFFFu, cnt = (ref >> 24) & 0x7Fu;
+            float t = 0.0f, uu = 0.0f, vv = 0.0f;
+            const bool h = cnt > 0 && tri_hit(S, first, r, tmin, tt, &t, &uu, &vv);
+            in_hit = in_hit || h;
+            tt = h ? t : tt;
+            rec.mat = h ? first : rec.mat;
+            rec.u = h ? uu : rec.u;
+            rec.v = h ? vv : rec.v;
+            const bool more = cnt > 1;
+            ref = more ? (MESH_LEAF | ((cnt - 1) << 24) | (first + 1)) : ref;
+            res = (!more && in_hit) ? 1u : 0u;
+            pop = !more && !in_hit;
+        } else {
+            const WideNode W = mesh_wide<TREE>(S, ref, L);
+            const bool hl = aabb_hit(W.lmin, W.lmax, r, tmin, tt);
+            const bool hr = aabb_hit(W.rmin, W.rmax, r, tmin, tt);
+            const bool left_first = (W.order & r.mask) != 0;
+            const uint32_t cref = left_first ? W.lref : W.rref, fref = left_first ? W.rref : W.lref;
+            const bool hc = left_first ? hl : hr, hf = left_first ? hr : hl;
+            if (hc && hf) L.mesh[(msp++) * 64 + L.lane] = fref;
+            ref = hc ? cref : (hf ? fref : ref);
+            pop = !hc && !hf;
+        }
+        if (pop) {
+            if (msp == 0) res = 2u;
+            else ref = L.mesh[(--msp) * 64 + L.lane];
+        }
+        return res;
+    }
     if (ref & MESH_LEAF) {
         const uint32_t first = ref & 0xFFFFFFu, cnt = (ref >> 24) & 0x7Fu;
         float t, uu, vv;
@@ -608,6 +647,18 @@ MRT_DFN uint32_t mesh_step(const DScene& S, const mrt_node& n, const Ray& r, flo
     if (msp == 0) return 2u;
     ref = L.mesh[(--msp) * 64 + L.lane];
     return 0u;
+}
+// the record mesh_step<TREE, true> left for mesh_leaf: its closest triangle's point and normal,
+// the mesh's material (the same operations as mesh_step's own completion)
+MRT_DFN void mesh_hit_rec(const DScene& S, const mrt_node& n, const Ray& r, float tt, HitRec& rec) {
+    const uint32_t best = rec.mat;
+    const float bu = rec.u, bv = rec.v;
+    const float4* q = S.tri_nrm + (size_t)best * 3;
+    f3 nm = ld3(q[0]), nu = ld3(q[1]), nv = ld3(q[2]);
+    rec.t = tt;
+    rec.p = eval(r, tt);
+    rec.n = normalize(add(add(mulf(nm, (1 - bu) - bv), mulf(nu, bu)), mulf(nv, bv)));
+    rec.mat = n.mat;
 }
 
 template <uint32_t F>
@@ -711,17 +762,16 @@ MRT_DFN bool bvhw_hit(const DScene& S, const mrt_node& n, const Ray& r, float tm
     for (;;) {
         while (!(ref & BVHW_LEAF)) {
             const WideNode W = wide_at<TreeOf<F>::on>(S.bwide, ref, L);
-            const bool hl = !(W.flags & 1u) || aabb_hit(W.lmin, W.lmax, r, tmin, tmax);
-            const bool hr = !(W.flags & 2u) || aabb_hit(W.rmin, W.rmax, r, tmin, tmax);
+            // (both boxes tested on every lane, `|` rather than `||`: a box-less slot's test is
+            // ignored, and the walk keeps no branch around each test)
+            const bool hl = !(W.flags & 1u) | aabb_hit(W.lmin, W.lmax, r, tmin, tmax);
+            const bool hr = !(W.flags & 2u) | aabb_hit(W.rmin, W.rmax, r, tmin, tmax);
             const bool left_first = (W.order & r.mask) != 0;
             const uint32_t cref = left_first ? W.lref : W.rref, fref = left_first ? W.rref : W.lref;
             const bool hc = left_first ? hl : hr, hf = left_first ? hr : hl;
-            if (hc) {
-                if (hf && fref != cref) L.mesh[(sp++) * 64 + L.lane] = fref;  // n == 1: left == right, a repeat misses again
-                ref = cref;
-            } else if (hf) {
-                ref = fref;
-            } else {
+            if (hc && hf && fref != cref) L.mesh[(sp++) * 64 + L.lane] = fref;  // n == 1: left == right, a repeat misses again
+            ref = hc ? cref : fref;
+            if (!hc && !hf) {
                 if (sp == 0) return false;
                 ref = L.mesh[(--sp) * 64 + L.lane];
             }
