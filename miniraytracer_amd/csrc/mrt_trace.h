@@ -719,29 +719,43 @@ MRT_DFN bool bvhw_leaf(const DScene& S, uint32_t ref, const Ray& r, float tmin, 
         const uint32_t k = MRT_NODE_KIND(n);
         return k != MRT_K_LIST && leaf_prim_hit<F>(n, k, r, tmin, tmax, rec, full);
     }
-    float closest = tmax;
-    bool hit = false;
+    // The run's primitives are tested for t alone; the closest one's full record is computed once
+    // after the loop, by the same test with the same (tmin, tmax) it passed with -- the same bits.
+    // (Each hit writing the whole record inside the loop merged all its registers at every
+    // primitive-kind branch: 132 of the loop's 233 VALU instructions were copies.)
+    float closest = tmax, t_before = tmax;
+    uint32_t best = ~0u;
     for (uint32_t i = 0; i < cnt; i++) {
         const mrt_node c = ld_node_v(run + i);
         const uint32_t ck = MRT_NODE_KIND(c);
+        HitRec tr;
         if (ck == MRT_K_LIST) {
             if (MRT_FAST_BOX && (MRT_NODE_FLAGS(c) & MRT_F_BOX6)) {  // box.h's six rects as one slab test
-                if (box6_leaf_hit(c, r, tmin, closest, rec, full)) {
-                    hit = true;
-                    closest = rec.t;
-                }
+                const bool h = box6_leaf_hit(c, r, tmin, closest, tr, false);
+                t_before = h ? closest : t_before;
+                best = h ? i : best;
+                closest = h ? tr.t : closest;
                 i += c.b;
                 continue;
             }
             if ((MRT_NODE_FLAGS(c) & MRT_F_HASBOX) && !aabb_hit(c.f, c.f + 3, r, tmin, closest)) i += c.b;
             continue;
         }
-        if (leaf_prim_hit<F>(c, ck, r, tmin, closest, rec, full)) {
-            hit = true;
-            closest = rec.t;
-        }
+        const bool h = leaf_prim_hit<F>(c, ck, r, tmin, closest, tr, false);
+        t_before = h ? closest : t_before;
+        best = h ? i : best;
+        closest = h ? tr.t : closest;
     }
-    return hit;
+    if (best == ~0u) return false;
+    if (!full) {
+        rec.t = closest;
+        return true;
+    }
+    const mrt_node c = ld_node_v(run + best);
+    const uint32_t ck = MRT_NODE_KIND(c);
+    if (MRT_FAST_BOX && ck == MRT_K_LIST) (void)box6_leaf_hit(c, r, tmin, t_before, rec, true);
+    else (void)leaf_prim_hit<F>(c, ck, r, tmin, t_before, rec, true);
+    return true;
 }
 
 // bvh_node::hit (scene_object.h:208-244) over wide nodes: the root's own box, then depth-first,
