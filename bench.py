@@ -345,14 +345,16 @@ def main():
         from miniraytracer_amd.dist import TileGather
         eg = TileGather(args.width, args.height, args.samples, args.depth, d_world, 0, dev, tile_size=args.tile_size)
         n_rows = eg.n_max
-    outs = [torch.zeros((n_rows, 4), dtype=torch.float32, device=dev) for _ in range(npipe)]
-    out = outs[0]
+    # output buffers: one per context, two per context when a gather reads them (world > 1) so a
+    # render never waits for the previous gather of its own buffer (one context, C2 on 1-2 ranks)
+    nbuf = npipe * (2 if world > 1 else 1)
+    outs = [torch.zeros((n_rows, 4), dtype=torch.float32, device=dev) for _ in range(nbuf)]
     rays = torch.zeros(1, dtype=torch.int64, device=dev)  # every context adds its rays here (device atomics)
     stream = torch.cuda.current_stream(dev)
     streams = [stream] + [torch.cuda.Stream(dev) for _ in range(npipe - 1)]
 
     pending = [None]
-    sent = [None] * npipe  # the gather that last read context j's output buffer
+    sent = [None] * nbuf  # the gather that last read output buffer b
     it = [0]
     ctx = [rnds]  # the render contexts measure() uses (the other-walk timing swaps in its own)
 
@@ -360,17 +362,18 @@ def main():
         # step i renders with context i % npipe on its stream; nothing orders it after step i-1's
         # kernels, so its waves start on the CUs that step i-1's finished waves leave idle
         j = it[0] % npipe
+        b = it[0] % nbuf
         it[0] += 1
         with torch.cuda.stream(streams[j]):
-            if sent[j] is not None:  # the gather of this buffer's previous render has read it
-                sent[j].wait()
-            ctx[0][j].render_device(d, outs[j].data_ptr(), rays.data_ptr(), streams[j].cuda_stream)
+            if sent[b] is not None:  # the gather of this buffer's previous render has read it
+                sent[b].wait()
+            ctx[0][j].render_device(d, outs[b].data_ptr(), rays.data_ptr(), streams[j].cuda_stream)
             if world > 1:
                 # the one RCCL collective of the data path (tile shards -> rank 0), overlapped with
                 # the next render: finish the previous step's gather, then start this one's
                 if pending[0] is not None:
                     tg.finish(pending[0])
-                pending[0] = sent[j] = tg.start(outs[j])
+                pending[0] = sent[b] = tg.start(outs[b])
             elif eg is not None:
                 eg.scatter()  # rehearsal: rank 0's device-side share of the gather
 
@@ -443,7 +446,7 @@ def main():
         if world > 1:
             return tg.full.view(args.height, args.width, 4).cpu().numpy() if rank == 0 else None
         full = np.zeros((args.width * args.height, 4), dtype=np.float32)
-        full[px] = outs[(it[0] - 1) % npipe][:n_local].cpu().numpy()
+        full[px] = outs[(it[0] - 1) % nbuf][:n_local].cpu().numpy()
         return full.reshape(args.height, args.width, 4)
 
     # parity of the timed render (after the timed region): the last step's image against the

@@ -111,6 +111,13 @@ typedef struct mrt_render_desc {
     uint32_t chunk_samples;  /* samples per launch (0 = auto, bounded by HBM budget) */
     uint32_t flags;          /* MRT_RF_* */
     uint32_t threads;        /* CPU backend: worker threads (0 = every core); the GPU backend ignores it */
+    /* Optional pixel list (an addition; the reference always renders the whole buffer): when
+     * non-NULL this call renders exactly these n_pixels row-major pixel indices (row 0 = bottom,
+     * each < width*height, no repeats), in this order as its local pixels, instead of the tiles
+     * dealt to `rank` -- every sample of each, the same per-path streams, so a listed pixel equals
+     * the same pixel of a whole-image render bit for bit.  Caller-owned; read during the call. */
+    const uint32_t* pixels;
+    uint32_t n_pixels;
 } mrt_render_desc;
 #define MRT_RF_PATH_DEBUG 0x1u /* also keep per-path radiance + ray counts (mrt_render_debug) */
 #define MRT_RF_FAST 0x2u       /* tolerance numerics contract: FMA contraction, hardware rcp/sqrt/rsq,
@@ -137,7 +144,7 @@ typedef struct mrt_render_desc {
 void mrt_default_render_desc(const mrt_params* p, mrt_render_desc* d);
 
 /* Number of pixels this rank owns and their row-major indices (row 0 = bottom, like
- * G_linearBackBuffer main.cpp:58) in the order mrt_render_device writes them. */
+ * G_linearBackBuffer main.cpp:58) in the order mrt_render_device writes them (d->pixels when set). */
 mrt_status mrt_local_pixels(const mrt_render_desc* d, uint32_t* n_out, uint32_t* pixels_out /* may be NULL */);
 
 /* Render into a host W*H*4 float buffer (x,y,z,0 per pixel; only owned pixels are written).

@@ -38,7 +38,7 @@ class MrtRenderDesc(C.Structure):
                 ("max_bounces", C.c_uint32), ("max_luminance", C.c_float), ("mode", C.c_uint32),
                 ("seed", C.c_uint64), ("tile_size", C.c_uint32), ("rank", C.c_uint32),
                 ("world", C.c_uint32), ("chunk_samples", C.c_uint32), ("flags", C.c_uint32),
-                ("threads", C.c_uint32)]
+                ("threads", C.c_uint32), ("pixels", C.c_void_p), ("n_pixels", C.c_uint32)]
 
 
 class MrtCamera(C.Structure):

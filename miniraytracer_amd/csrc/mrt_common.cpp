@@ -278,23 +278,50 @@ std::vector<uint32_t> mrt_internal_tile_owners(size_t ntiles, uint32_t world) {
     return own;
 }
 
+std::vector<mrt_tile> mrt_internal_render_tiles(const mrt_render_desc* d) {
+    std::vector<mrt_tile> out;
+    if (d->pixels) {  // a pixel list: one 1x1 "tile" per listed pixel, in list order
+        out.reserve(d->n_pixels);
+        for (uint32_t i = 0; i < d->n_pixels; i++) {
+            const uint32_t x = d->pixels[i] % d->width, y = d->pixels[i] / d->width;
+            out.push_back(mrt_tile{x, x + 1u, y, y + 1u});
+        }
+        return out;
+    }
+    const std::vector<mrt_tile> all = mrt_internal_tiles(d->width, d->height, d->tile_size ? d->tile_size : 32u);
+    const std::vector<uint32_t> own = mrt_internal_tile_owners(all.size(), d->world ? d->world : 1u);
+    for (size_t k = 0; k < all.size(); k++)
+        if (own[k] == d->rank) out.push_back(all[k]);
+    return out;
+}
+
 std::vector<uint32_t> mrt_internal_local_pixels(const mrt_render_desc* d) {
-    std::vector<mrt_tile> tiles = mrt_internal_tiles(d->width, d->height, d->tile_size ? d->tile_size : 32);
+    if (d->pixels) return std::vector<uint32_t>(d->pixels, d->pixels + d->n_pixels);
     std::vector<uint32_t> px;
-    uint32_t world = d->world ? d->world : 1;
-    const std::vector<uint32_t> own = mrt_internal_tile_owners(tiles.size(), world);
-    for (size_t k = 0; k < tiles.size(); k++) {
-        if (own[k] != d->rank) continue;
-        const mrt_tile& t = tiles[k];
+    for (const mrt_tile& t : mrt_internal_render_tiles(d))
         for (uint32_t y = t.ymin; y < t.ymax; y++)
             for (uint32_t x = t.xmin; x < t.xmax; x++) px.push_back(x + y * d->width);
-    }
     return px;
+}
+
+mrt_status mrt_internal_check_pixels(const mrt_render_desc* d) {
+    if (!d->pixels) return MRT_OK;
+    if (d->n_pixels == 0) return mrt_internal_fail(MRT_ERR_INVALID, "render desc: empty pixel list");
+    const uint64_t wh = (uint64_t)d->width * d->height;
+    std::vector<bool> seen(wh, false);
+    for (uint32_t i = 0; i < d->n_pixels; i++) {
+        const uint32_t p = d->pixels[i];
+        if (p >= wh) return mrt_internal_fail(MRT_ERR_INVALID, "render desc: pixel index outside the image");
+        if (seen[p]) return mrt_internal_fail(MRT_ERR_INVALID, "render desc: pixel listed twice");
+        seen[p] = true;
+    }
+    return MRT_OK;
 }
 
 extern "C" mrt_status mrt_local_pixels(const mrt_render_desc* d, uint32_t* n_out, uint32_t* pixels_out) {
     if (!d || !n_out || d->width == 0 || d->height == 0 || (d->world && d->rank >= d->world))
         return mrt_internal_fail(MRT_ERR_INVALID, "mrt_local_pixels: bad desc");
+    if (mrt_status st = mrt_internal_check_pixels(d)) return st;
     std::vector<uint32_t> px = mrt_internal_local_pixels(d);
     *n_out = (uint32_t)px.size();
     if (pixels_out) memcpy(pixels_out, px.data(), px.size() * 4);

@@ -308,22 +308,19 @@ mrt_status mrt_cpu_render(mrt_cpu_scene* c, const mrt_render_desc* d, float* rgb
     if (d->flags & MRT_RF_FAST)
         return mrt_internal_fail(MRT_ERR_INVALID, "the CPU backend implements the exact numerics contract only");
     if (d->flags & MRT_RF_PATH_DEBUG) return mrt_internal_fail(MRT_ERR_INVALID, "MRT_RF_PATH_DEBUG is a GPU-backend render flag");
+    if (mrt_status st = mrt_internal_check_pixels(d)) return st;
     const bool ref_order = (d->flags & MRT_RF_REF_ORDER) != 0;
     if (ref_order) {
-        if (d->world > 1) return mrt_internal_fail(MRT_ERR_INVALID, "MRT_RF_REF_ORDER renders the whole image (the reference has no ranks)");
+        if (d->world > 1 || d->pixels)
+            return mrt_internal_fail(MRT_ERR_INVALID, "MRT_RF_REF_ORDER renders the whole image (the reference has no ranks or pixel lists)");
         if (c->seed_state.empty()) return mrt_internal_fail(MRT_ERR_INVALID, "MRT_RF_REF_ORDER needs mrt_set_worker_seeds first");
         if (d->threads && d->threads != c->seed_state.size())
             return mrt_internal_fail(MRT_ERR_INVALID, "MRT_RF_REF_ORDER: desc.threads must equal the worker seeds given");
     }
     const auto t0 = std::chrono::steady_clock::now();
-    const uint32_t world = d->world ? d->world : 1u, ns = d->sqrt_samples * d->sqrt_samples;
-    std::vector<mrt_tile> tiles;  // this rank's tiles, in work_queue order
-    {
-        const std::vector<mrt_tile> all = mrt_internal_tiles(d->width, d->height, d->tile_size ? d->tile_size : 32u);
-        const std::vector<uint32_t> own = mrt_internal_tile_owners(all.size(), world);
-        for (size_t k = 0; k < all.size(); k++)
-            if (own[k] == d->rank) tiles.push_back(all[k]);
-    }
+    const uint32_t ns = d->sqrt_samples * d->sqrt_samples;
+    // this rank's tiles in work_queue order (or one 1x1 tile per listed pixel)
+    const std::vector<mrt_tile> tiles = mrt_internal_render_tiles(d);
     uint64_t px = 0;
     for (const mrt_tile& t : tiles) px += (uint64_t)(t.xmax - t.xmin) * (t.ymax - t.ymin);
     c->done.store(0, std::memory_order_relaxed);

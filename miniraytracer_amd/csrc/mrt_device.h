@@ -117,6 +117,17 @@ MRT_DFN f3 divf(f3 a, float f) { return f3{a.x / f, a.y / f, a.z / f}; }
 #endif
 MRT_DFN float dot(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 MRT_DFN float sdot(f3 a) { return (a.x * a.x + a.y * a.y) + a.z * a.z; }
+// a*b + c rounded the same way wherever it is inlined: one fma in the tolerance build, where
+// contraction is decided per use site (a product with other uses may stay unfused), so a hit
+// predicate inlined twice -- a leaf's t-only test and its record's second test -- could otherwise
+// round two ways; a product then a sum in the exact build (no contraction there)
+MRT_DFN float madd_det(float a, float b, float c) {
+#if MRT_FAST
+    return __builtin_fmaf(a, b, c);
+#else
+    return a * b + c;
+#endif
+}
 // sphere::hit's quadratic (sphere.cpp:20-26): b = dot(oc, d), c = |oc|^2 - r^2, disc = b*b - c.
 // Never FMA-contracted, also in the tolerance-contract build (the CPU restatement built with
 // contraction loses 0.08% of book2's rays through this quadratic; DESIGN.md "Numerics contracts").

@@ -20,3 +20,8 @@ std::vector<uint32_t> mrt_internal_tile_owners(size_t ntiles, uint32_t world);
 // mrt_internal_tile_owners gives it, each scanned row by row (the order draw() visits them,
 // main.cpp:148-149).
 std::vector<uint32_t> mrt_internal_local_pixels(const mrt_render_desc* d);
+// The work items of one render call: the rank's tiles in work_queue order, or (d->pixels) one 1x1
+// tile per listed pixel in list order.
+std::vector<mrt_tile> mrt_internal_render_tiles(const mrt_render_desc* d);
+// d->pixels, if set, is non-empty, inside the image and free of repeats
+mrt_status mrt_internal_check_pixels(const mrt_render_desc* d);

@@ -282,6 +282,7 @@ struct mrt_scene {
     uint32_t n_nodes = 0;
     // workspace
     mrt_render_desc wdesc{};
+    std::vector<uint32_t> wpixels;   // the pixel list of wdesc (mrt_render_desc.pixels), copied
     bool have_ws = false;
     uint32_t npix = 0, chunk = 0;
     uint2* d_pixels = nullptr;
@@ -1075,8 +1076,10 @@ static uint32_t auto_chunk(uint32_t npix, uint32_t ns) {
     return (uint32_t)std::min<size_t>(c, ns);
 }
 
-static bool same_layout(const mrt_render_desc& a, const mrt_render_desc& b) {
-    return a.width == b.width && a.height == b.height && a.tile_size == b.tile_size && a.rank == b.rank && a.world == b.world;
+static bool same_layout(const mrt_render_desc& a, const std::vector<uint32_t>& a_px, const mrt_render_desc& b) {
+    if (a.width != b.width || a.height != b.height || (a.pixels != nullptr) != (b.pixels != nullptr)) return false;
+    if (b.pixels) return a_px.size() == b.n_pixels && std::equal(a_px.begin(), a_px.end(), b.pixels);
+    return a.tile_size == b.tile_size && a.rank == b.rank && a.world == b.world;
 }
 
 // Before the workspace is rewritten or reallocated: wait for the last enqueued render of this
@@ -1111,9 +1114,13 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
     // the path kernel's u = (x + dx) / W by one reciprocal is exact up to 2^24 (mrt_kernels.hip)
     if (d->width > (1u << 24) || d->height > (1u << 24))
         return mrt_internal_fail(MRT_ERR_INVALID, "mrt_prepare: width / height above 2^24 pixels");
-    HIPCHK(hipSetDevice(s->device));
+    // every GPU entry point renders in per-path stream order (mrt_render_device and mrt_render come here)
+    if (d->flags & MRT_RF_REF_ORDER)
+        return mrt_internal_fail(MRT_ERR_INVALID, "MRT_RF_REF_ORDER is a CPU-backend mode (the GPU keys its PCG streams per path)");
     mrt_status st;
-    bool relayout = !s->have_ws || !same_layout(s->wdesc, *d);
+    if ((st = mrt_internal_check_pixels(d))) return st;
+    HIPCHK(hipSetDevice(s->device));
+    bool relayout = !s->have_ws || !same_layout(s->wdesc, s->wpixels, *d);
     uint32_t ns = d->sqrt_samples * d->sqrt_samples;
     if (relayout) {
         std::vector<uint32_t> px = mrt_internal_local_pixels(d);
@@ -1205,7 +1212,10 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
         HIPCHK(hipHostMalloc((void**)&s->h_one, sizeof(int), hipHostMallocPortable));
         *s->h_one = 1;
     }
+    if (relayout) s->wpixels = d->pixels ? std::vector<uint32_t>(d->pixels, d->pixels + d->n_pixels) : std::vector<uint32_t>();
     s->wdesc = *d;
+    s->wdesc.pixels = nullptr;  // (the caller's list is not kept; wpixels holds a copy)
+    if (d->pixels) s->wdesc.pixels = s->wpixels.data();
     s->have_ws = true;
     return MRT_OK;
 }
@@ -1336,8 +1346,6 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
 extern "C" mrt_status mrt_render(mrt_scene* s, const mrt_render_desc* d, float* rgb_out, uint64_t* rays_out, const volatile int* cancel) {
     if (!s || !d || !rgb_out) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_render: null");
     if (s->cpu) return mrt_cpu_render(s->cpu, d, rgb_out, rays_out, cancel);
-    if (d->flags & MRT_RF_REF_ORDER)
-        return mrt_internal_fail(MRT_ERR_INVALID, "MRT_RF_REF_ORDER is a CPU-backend mode (the GPU keys its PCG streams per path)");
     s->n_chunks.store(0, std::memory_order_release);
     if (cancel && *cancel) return mrt_internal_fail(MRT_ERR_CANCELLED, "cancelled");
     mrt_render_desc dc = *d;  // a cancellable render runs as >= 16 launches; cancel lands between them

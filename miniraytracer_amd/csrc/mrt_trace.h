@@ -343,8 +343,11 @@ MRT_DFN void sphere_uv(f3 p, float* u, float* v) {
 template <uint32_t F>
 MRT_DFN f3 sphere_center(const mrt_node& n, float time) {
     f3 c0 = ld3(n.f);
-    if ((F & FT_MOVING) && (MRT_NODE_FLAGS(n) & MRT_F_MOVING))
-        return add(c0, fmul((time - n.f[6]) / (n.f[7] - n.f[6]), sub(ld3(n.f + 3), c0)));
+    if ((F & FT_MOVING) && (MRT_NODE_FLAGS(n) & MRT_F_MOVING)) {
+        const float s = (time - n.f[6]) / (n.f[7] - n.f[6]);
+        const f3 dc = sub(ld3(n.f + 3), c0);
+        return f3{madd_det(s, dc.x, c0.x), madd_det(s, dc.y, c0.y), madd_det(s, dc.z, c0.z)};
+    }
     return c0;
 }
 
@@ -393,8 +396,8 @@ MRT_DFN bool rect_hit(const mrt_node& n, const Ray& r, float tmin, float tmax, H
     if (t < tmin || t > tmax) return false;
     float ob = AX == 0 ? r.o.y : r.o.x, db = AX == 0 ? r.d.y : r.d.x;
     float oc = AX == 2 ? r.o.y : r.o.z, dc = AX == 2 ? r.d.y : r.d.z;
-    float pb = ob + t * db;
-    float pc = oc + t * dc;
+    float pb = madd_det(t, db, ob);  // (the predicate's arithmetic: see madd_det)
+    float pc = madd_det(t, dc, oc);
     if (pb < n.f[0] || pb > n.f[1] || pc < n.f[2] || pc > n.f[3]) return false;
     rec.t = t;
     if (full) {
@@ -727,6 +730,8 @@ MRT_DFN bool bvhw_leaf(const DScene& S, uint32_t ref, const Ray& r, float tmin, 
             rec.t = tr.t;
             return true;
         }
+        // the second test repeats the first's predicate with the same operands and range: its
+        // arithmetic is contraction-proof (sphere_disc unfused, madd_det), so it hits again
         (void)leaf_prim_hit<F>(n, k, r, tmin, tmax, rec, true);
         return true;
     }

@@ -56,3 +56,11 @@ build() {  # name extra-flags
 
 build mrt_ref
 build mrt_ref_exact -ffp-contract=off -DMRT_MATHMATCH
+# numerics-diagnosis builds (MRT_REF_VARIANTS=1): which difference between the two builds above
+# makes their images differ -- contraction alone (shipped flags, project libm) or libm alone
+# (no contraction, glibc) -- and what unrestricted contraction (-ffp-contract=fast) does
+if [ -n "${MRT_REF_VARIANTS:-}" ]; then
+    build mrt_ref_mm -DMRT_MATHMATCH
+    build mrt_ref_glibc -ffp-contract=off
+    build mrt_ref_fastc -ffp-contract=fast
+fi

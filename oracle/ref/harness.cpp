@@ -11,6 +11,8 @@
 //                      reference PCG with the path key (see path_key below), call the reference
 //                      camera::get_ray + trace() unchanged, accumulate with draw() (mode 0,
 //                      main.cpp:151-175) or draw2() (mode 1, main.cpp:207-231) rules.
+//                      --h-pixels FILE (raw uint32 pixel indices) renders only those pixels and
+//                      --h-px-out FILE writes their values (raw float32 n x 3, list order).
 //   --h-mode kat       PCG / sampler known-answer vectors (pcg.cpp).
 //   --h-mode scene     dump the scene graph select_scene() builds (types, parameters as float
 //                      bits, BVH topology incl. node_order) and the camera.
@@ -505,13 +507,31 @@ static int mode_stream(int argc, char** argv) {
         pathrays.resize((size_t)W * H * ns);
         nthreads = 1;  // per-path ray counts come from the shared counter
     }
+    // --h-pixels: render only the listed pixels (raw little-endian uint32 row-major indices) and
+    // write their values to --h-px-out (raw float32, n x 3, list order); rays = the listed pixels'
+    std::vector<uint32_t> plist;
+    const char* plist_in = harg(argc, argv, "--h-pixels", nullptr);
+    const char* plist_out = harg(argc, argv, "--h-px-out", nullptr);
+    if (plist_in) {
+        FILE* f = fopen(plist_in, "rb");
+        if (!f) { fprintf(stderr, "cannot read %s\n", plist_in); return 2; }
+        uint32_t v;
+        while (fread(&v, 4, 1, f) == 1) {
+            if (v >= W * H) { fprintf(stderr, "pixel %u outside the image\n", v); return 2; }
+            plist.push_back(v);
+        }
+        fclose(f);
+        if (paths_out) { fprintf(stderr, "--h-pixels and --h-paths are exclusive\n"); return 2; }
+    }
     std::atomic<uint32_t> next_row{0};
     uint64_t t0 = MRT_GetTime();
     auto worker = [&]() {
         for (;;) {
             uint32_t y = next_row.fetch_add(1);
-            if (y >= H) break;
-            for (uint32_t x = 0; x < W; x++) {
+            if (plist_in ? y >= plist.size() : y >= H) break;
+            const uint32_t x0 = plist_in ? plist[y] % W : 0u, x1 = plist_in ? x0 + 1u : W;
+            if (plist_in) y = plist[y] / W;
+            for (uint32_t x = x0; x < x1; x++) {
                 uint64_t pix = (uint64_t)x + (uint64_t)y * W;
                 Vec3 color(0, 0, 0);
                 for (uint32_t s = 0; s < ns; s++) {
@@ -554,6 +574,17 @@ static int mode_stream(int argc, char** argv) {
     double secs = MRT_TimeDelta(t0, MRT_GetTime());
     size_t rays = G_rayCounter.load();
     if (out) write_pfm(out, img.data(), W, H);
+    if (plist_out) {
+        std::vector<float> v(plist.size() * 3);
+        for (size_t i = 0; i < plist.size(); i++) {
+            v[i * 3 + 0] = img[plist[i]].r;
+            v[i * 3 + 1] = img[plist[i]].g;
+            v[i * 3 + 2] = img[plist[i]].b;
+        }
+        FILE* f = fopen(plist_out, "wb");
+        if (!f || fwrite(v.data(), 4, v.size(), f) != v.size()) { fprintf(stderr, "cannot write %s\n", plist_out); return 2; }
+        fclose(f);
+    }
     if (paths_out) {
         std::string a = std::string(paths_out) + ".rgb.npy", b = std::string(paths_out) + ".rays.npy";
         write_npy(a.c_str(), "<f4", {(size_t)W * H * ns, 3}, paths.data(), paths.size() * 4);

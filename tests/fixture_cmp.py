@@ -8,6 +8,7 @@ Two fixture shapes:
   shipped_stream_5.npz   the whole C2 image (500x500, 1024 spp): per-pixel RMSE over every pixel
   shipped_full_<id>.npz  C3 / C4 / C5 at full resolution: a 32x32 grid of block means, channel means,
                          a band of rows and a seeded pixel sample; per-pixel RMSE over band + sample
+  shipped_ownspp_<id>.npz  C3 / C4 / C5 at their own spp, a pixel list only (compare_pixels)
 """
 import os
 
@@ -60,3 +61,13 @@ def compare(img, rays, path):
         out["block"] = f"{bh}x{bw} px"
     out["mean_delta"] = float(np.abs(im.reshape(-1, 3).mean(axis=0, dtype=np.float64) - g["mean"]).max())
     return out
+
+
+def compare_pixels(img, rays, g):
+    """A pixel-list render (mrt_render_desc.pixels = g["pixels"]) against shipped_ownspp_<id>.npz:
+    per-pixel RMSE over the list, max |channel-mean delta| of the list, ray ratio of the list."""
+    vals = np.asarray(img, np.float32).reshape(-1, img.shape[-1])[g["pixels"], :3]
+    d = vals.astype(np.float64) - g["values"]
+    return {"fixture": f"shipped_ownspp_{int(g['meta'][0])}", "spp": int(g["meta"][3]), "pixels": int(g["pixels"].size),
+            "rmse": float(np.sqrt((d ** 2).mean())), "mean_delta": float(np.abs(d.mean(axis=0)).max()),
+            "ray_ratio": float(rays / float(g["rays"][0]))}

@@ -65,6 +65,27 @@ def test_cpu_backend_independent_of_threads_and_ranks(mrt):
     assert total == ra and np.array_equal(full, a)
 
 
+def test_cpu_backend_pixel_list_equals_whole_image(mrt):
+    """mrt_render_desc.pixels: a render of a listed pixel subset gives those pixels of the whole-image
+    render bit for bit, the rest untouched (0), local_pixels = the list; the ray total is the subset's
+    (the sum over listed pixels of the per-pixel totals of one-pixel renders).  Bad lists fail."""
+    sc, r = cpu_renderer(mrt, 8, 40, 24)
+    full, _ = r.render(mrt.render_desc(40, 24, 9, threads=4))
+    px = np.array([5, 40 * 23 + 39, 0, 333, 17], dtype=np.uint32)
+    d = mrt.render_desc(40, 24, 9, threads=3, pixels=px)
+    assert np.array_equal(mrt.local_pixels(d), px)
+    part, rays = r.render(d)
+    flat = part.reshape(-1, 4)
+    assert np.array_equal(flat[px].view(np.uint32), full.reshape(-1, 4)[px].view(np.uint32))
+    rest = np.ones(40 * 24, dtype=bool)
+    rest[px] = False
+    assert not flat[rest].any()
+    assert rays == sum(r.render(mrt.render_desc(40, 24, 9, threads=1, pixels=[p]))[1] for p in px)
+    for bad in ([40 * 24], [3, 3], []):
+        with pytest.raises(mrt.MrtError):
+            r.render(mrt.render_desc(40, 24, 9, pixels=np.array(bad, dtype=np.uint32)))
+
+
 def test_cpu_backend_progress_cancel_and_gpu_only_calls(mrt):
     sc, r = cpu_renderer(mrt, 0, 64, 32)
     d = mrt.render_desc(64, 32, 16, depth=8, tile_size=8, threads=2)

@@ -16,10 +16,14 @@ Fixtures (all small; data only -- inputs and expected outputs):
                           (SURVEY 8(d) parity 2).  Full C2 (500x500, 1024 spp): the whole image, rows 200-299, 25x25
                           block means, channel means, ray count; and whole small images of scenes 5, 8, 9, 7
                           (SHIPPED_SMALL).
-                          `--only-shipped-stream` regenerates just these two.
+                          `--only-shipped-stream` regenerates just these two
+                          (`--only-shipped-small`: the small ones).
   shipped_full_<id>.npz   the same at the full resolution of C3 / C4 / C5 (1024 spp): block means,
                           channel means, a band of rows, a seeded pixel sample, ray total
                           (`--only-fullres`; FULLRES)
+  shipped_ownspp_<id>.npz C3 / C4 / C5 at their OWN spp (4096, 2025, 8100): the reference as shipped
+                          on a pixel list (a row band + seeded pixels), values + the list's ray total
+                          (`--only-ownspp`; OWNSPP)
   refseq_<id>_m<mode>.npz the exact reference build with -threads 1 (its own deterministic mode:
                           one worker PCG stream, work_queue tile order), image + G_rayCounter
                           (`--only-refseq`)
@@ -44,7 +48,9 @@ CWD = os.path.join(REF, "clang")  # the reference resolves ../obj and ../earthma
 STREAM_CASES = [(0, 40, 20, 16, 8), (1, 40, 20, 9, 8), (2, 32, 16, 9, 8), (3, 32, 16, 9, 8), (4, 32, 16, 9, 8),
                 (5, 32, 32, 16, 32), (6, 32, 32, 9, 32), (7, 32, 32, 4, 32), (8, 32, 32, 9, 32), (9, 32, 32, 9, 32)]
 # shipped-numerics tolerance fixtures (stream-matched): Cornell, bunny, teapot-in-Cornell, book2
-SHIPPED_SMALL = [(5, 128, 128, 256), (8, 128, 128, 256), (9, 128, 128, 256), (7, 64, 64, 4096)]
+# (the north-star spp of C2, 1024, for the Cornell / mesh cases: the per-pixel bar is then 1e-3
+# everywhere, no scaled small-fixture bar)
+SHIPPED_SMALL = [(5, 128, 128, 1024), (8, 128, 128, 1024), (9, 128, 128, 1024), (7, 64, 64, 4096)]
 SCENE_SIZES = {0: (200, 100), 1: (200, 100), 2: (200, 100), 3: (200, 100), 4: (200, 100), 5: (500, 500),
                6: (500, 500), 7: (2048, 2048), 8: (1024, 1024), 9: (800, 800)}
 
@@ -79,9 +85,11 @@ def read_pfm(p, w, h):
     return np.frombuffer(raw[3], dtype="<f4").reshape(h, w, 3)
 
 
-def shipped_stream(tmp):
+def shipped_stream(tmp, small_only=False):
     """The shipped build, stream-matched (same per-path key as the GPU), full C2 and a small case."""
     img = os.path.join(tmp, "ss.pfm")
+    if small_only:
+        return shipped_small(tmp, img)
     meta = json.loads(run(SHIPPED, ["--h-mode", "stream", "-width", 500, "-height", 500, "-samples", 1024, "-depth", 32,
                                     "--h-threads", 8, "--h-out", img, "-scene", 5]))
     im = read_pfm(img, 500, 500)
@@ -90,6 +98,10 @@ def shipped_stream(tmp):
                         mean=im.reshape(-1, 3).mean(axis=0, dtype=np.float64), rays=np.array([meta["rays"]], dtype=np.int64),
                         meta=np.array([5, 500, 500, 1024, 32], dtype=np.int64))
     print("shipped stream C2", meta)
+    shipped_small(tmp, img)
+
+
+def shipped_small(tmp, img):
     for sid, w, h, spp in SHIPPED_SMALL:
         meta = json.loads(run(SHIPPED, ["--h-mode", "stream", "-width", w, "-height", h, "-samples", spp, "-depth", 32,
                                         "--h-threads", 8, "--h-out", img] + scene_args(sid)))
@@ -133,6 +145,38 @@ def fullres(tmp, only=None, threads=8):
         print("shipped full", sid, w, h, spp, meta, flush=True)
 
 
+# The same configs at their OWN sample counts (BASELINE.json configs 3-5; -samples floored to a
+# square by main.cpp:319-320: 4096 -> 64^2, 2048 -> 45^2 = 2025, 8192 -> 90^2 = 8100): the reference as
+# shipped, stream-matched, on a pixel subset only (the band of FULLRES_BAND rows at H/2 plus the
+# FULLRES_SAMPLE seeded pixels of fullres_reduce, deduplicated): their values and the subset's ray
+# total.  The product renders the same pixel list (mrt_render_desc.pixels) at the same spp.
+OWNSPP = [(9, 800, 800, 4096), (8, 1024, 1024, 2048), (7, 2048, 2048, 8192)]
+
+
+def ownspp_pixels(sid, w, h):
+    rng = np.random.default_rng(1000 + sid)
+    idx = rng.choice(w * h, size=FULLRES_SAMPLE, replace=False).astype(np.int64)
+    r0 = h // 2
+    band = np.arange(r0 * w, (r0 + FULLRES_BAND) * w, dtype=np.int64)
+    return np.unique(np.concatenate([band, idx])).astype(np.uint32)
+
+
+def ownspp(tmp, only=None, threads=8):
+    plist, pout = os.path.join(tmp, "px.u32"), os.path.join(tmp, "px.f32")
+    for sid, w, h, spp in OWNSPP:
+        if only is not None and sid not in only:
+            continue
+        px = ownspp_pixels(sid, w, h)
+        px.tofile(plist)
+        meta = json.loads(run(SHIPPED, ["--h-mode", "stream", "-width", w, "-height", h, "-samples", spp, "-depth", 32,
+                                        "--h-threads", threads, "--h-pixels", plist, "--h-px-out", pout] + scene_args(sid)))
+        vals = np.fromfile(pout, dtype="<f4").reshape(-1, 3)
+        assert vals.shape[0] == px.size
+        np.savez_compressed(os.path.join(OUT, f"shipped_ownspp_{sid}.npz"), pixels=px, values=vals,
+                            rays=np.array([meta["rays"]], dtype=np.int64), meta=np.array([sid, w, h, spp, 32], dtype=np.int64))
+        print("shipped own-spp", sid, w, h, spp, px.size, meta, flush=True)
+
+
 # the reference's own deterministic mode: -threads 1, one worker stream, work_queue tile order
 # (scene id, width, height, samples, depth, tile size); both -mode 0 (draw) and -mode 1 (draw2)
 REFSEQ_CASES = [(0, 60, 30, 16, 8, 16), (5, 48, 40, 16, 32, 16), (7, 40, 40, 4, 32, 16), (8, 40, 40, 9, 32, 16)]
@@ -156,14 +200,19 @@ def main():
         with tempfile.TemporaryDirectory() as tmp:
             refseq(tmp)
         return
+    if "--only-ownspp" in sys.argv:
+        only = [int(a) for a in os.environ.get("MRT_FULLRES_SCENES", "").split(",") if a]
+        with tempfile.TemporaryDirectory() as tmp:
+            ownspp(tmp, only or None, int(os.environ.get("MRT_FULLRES_THREADS", "8")))
+        return
     if "--only-fullres" in sys.argv:
         only = [int(a) for a in os.environ.get("MRT_FULLRES_SCENES", "").split(",") if a]
         with tempfile.TemporaryDirectory() as tmp:
             fullres(tmp, only or None, int(os.environ.get("MRT_FULLRES_THREADS", "8")))
         return
-    if "--only-shipped-stream" in sys.argv:
+    if "--only-shipped-stream" in sys.argv or "--only-shipped-small" in sys.argv:
         with tempfile.TemporaryDirectory() as tmp:
-            shipped_stream(tmp)
+            shipped_stream(tmp, small_only="--only-shipped-small" in sys.argv)
         return
     if not (os.path.exists(EXACT) and os.path.isdir(REF)):
         sys.exit("needs oracle/_ref (run oracle/ref/build_ref.sh) and /root/reference")
