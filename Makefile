@@ -42,10 +42,13 @@ $(OBJDIR)/mrt_kernels_fastz.o: $(CSRC)/mrt_kernels.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(HIPDEV) $(FASTFLAGS) $(FTZFLAGS) -c $< -o $@
 
-# the CPU backend: the same hot-path headers compiled for the host only (exact contract)
+# the CPU backend: the same hot-path headers compiled for the host only (exact contract).
+# -mfma: the reference's fused multiply-adds (mrt_device.h ref_fma) as one instruction instead of a
+# libm fmaf call (same result; the reference's own build is x86 FMA too, -march=native)
+HOSTFMA ?= -mfma
 $(OBJDIR)/mrt_cpu.o: $(CSRC)/mrt_cpu.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) --offload-host-only -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(HOSTFMA) --offload-host-only -c $< -o $@
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -63,7 +66,7 @@ bin/mrt: $(CSRC)/mrt_cli.cpp miniraytracer_amd/libmrt.so include/mrt.h
 	$(HIPCC) -O2 -std=c++17 -ffp-contract=off $(CSRC)/mrt_cli.cpp -Lminiraytracer_amd -lmrt -Wl,-rpath,'$$ORIGIN/../miniraytracer_amd' -o $@
 
 oracle/liboracle.so: oracle/mrt_oracle.c oracle/mrt_oracle.h include/mrt_scene.h
-	$(CC) -O2 -std=c11 -fPIC -shared -ffp-contract=off -fno-fast-math -Wall -o $@ oracle/mrt_oracle.c -lm -lpthread
+	$(CC) -O2 -std=c11 -fPIC -shared -ffp-contract=off -fno-fast-math $(HOSTFMA) -Wall -o $@ oracle/mrt_oracle.c -lm -lpthread
 
 clean:
 	rm -rf build miniraytracer_amd/libmrt.so bin oracle/liboracle.so

@@ -33,7 +33,8 @@ MRT_HD unsigned int mrt_argb_channel(float v) {
 MRT_HD unsigned int mrt_tonemap_pixel(const mrt_tonemap_params* tp, const float* c) {
     const float lum = mrt_luminance(c);
     const float loglw = mrt_logf(lum + 1.0f);
-    const float lum_new = tp->scale * (loglw / mrt_logf(2.0f + mrt_powf(lum * tp->invmax, tp->bias) * 8.0f));
+    /* logf(2 + powf(..) * 8): one scalar expression, fused as shipped (x86 FMA, main.cpp:437) */
+    const float lum_new = tp->scale * (loglw / mrt_logf(fmaf(mrt_powf(lum * tp->invmax, tp->bias), 8.0f, 2.0f)));
     const float d = lum + 0.00001f;
     const unsigned int r = mrt_argb_channel((lum_new * c[0]) / d);
     const unsigned int g = mrt_argb_channel((lum_new * c[1]) / d);

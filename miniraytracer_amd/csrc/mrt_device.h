@@ -120,7 +120,8 @@ MRT_DFN float sdot(f3 a) { return (a.x * a.x + a.y * a.y) + a.z * a.z; }
 // a*b + c rounded the same way wherever it is inlined: one fma in the tolerance build, where
 // contraction is decided per use site (a product with other uses may stay unfused), so a hit
 // predicate inlined twice -- a leaf's t-only test and its record's second test -- could otherwise
-// round two ways; a product then a sum in the exact build (no contraction there)
+// round two ways; a product then a sum in the exact build (no contraction there).  For sums the
+// reference computes with SSE Vec3 operators (never fused there).
 MRT_DFN float madd_det(float a, float b, float c) {
 #if MRT_FAST
     return __builtin_fmaf(a, b, c);
@@ -128,26 +129,28 @@ MRT_DFN float madd_det(float a, float b, float c) {
     return a * b + c;
 #endif
 }
+// The reference's own fused multiply-adds.  Built as shipped (clang -O3 -march=native: FMA,
+// -ffp-contract=on), it fuses a*b+c exactly where ONE scalar source expression holds a product
+// as an operand of a sum or difference -- clang's fmuladd rule: the left operand is tried first,
+// `x*y - z` -> fma(x, y, -z), `z - x*y` -> fma(-x, y, z) -- and nowhere else (its Vec3 operators are
+// SSE intrinsics, never fused).  Every such site on the hot path calls one of these, naming the
+// reference line; everything else is compiled with -ffp-contract=off (exact contract), so the
+// exact contract reproduces the reference as shipped bit for bit (with the project's
+// transcendentals, include/mrt_mathfn.h).  The tolerance contract fuses them too.
+// ref_fma(a, b, c) = a*b + c; ref_fms(a, b, c) = a*b - c; ref_fnma(a, b, c) = c - a*b
+MRT_DFN float ref_fma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+MRT_DFN float ref_fms(float a, float b, float c) { return __builtin_fmaf(a, b, -c); }
+MRT_DFN float ref_fnma(float a, float b, float c) { return __builtin_fmaf(-a, b, c); }
 // sphere::hit's quadratic (sphere.cpp:20-26): b = dot(oc, d), c = |oc|^2 - r^2, disc = b*b - c.
-// Never FMA-contracted, also in the tolerance-contract build (the CPU restatement built with
-// contraction loses 0.08% of book2's rays through this quadratic; DESIGN.md "Numerics contracts").
-#ifndef MRT_FAST_DISC_FMA
-#define MRT_FAST_DISC_FMA 0
-#endif
 MRT_DFN float sphere_disc(f3 oc, f3 d, float radius, float* bout) {
 #pragma clang fp contract(off)
     const float b = (oc.x * d.x + oc.y * d.y) + oc.z * d.z;
     const float s = (oc.x * oc.x + oc.y * oc.y) + oc.z * oc.z;
     *bout = b;
-#if MRT_FAST && MRT_FAST_DISC_FMA
-    // as clang contracts the reference's scalar tail (x86 -ffp-contract=on; the dot products are
-    // SSE intrinsics and stay unfused): c = fnmadd(r, r, s), disc = fmsub(b, b, c)
-    const float c = __builtin_fmaf(-radius, radius, s);
-    return __builtin_fmaf(b, b, -c);
-#else
-    const float c = s - radius * radius;
-    return b * b - c;
-#endif
+    // the reference's scalar tail, fused as shipped (the dot products are SSE, unfused):
+    // c = sdot(oc) - radius*radius, discriminant = b*b - c (sphere.cpp:20-21)
+    const float c = ref_fnma(radius, radius, s);
+    return ref_fms(b, b, c);
 }
 // ---- exact f32 division on a short path (tools/numcheck/markstein_check.hip) ----------------------
 // IEEE a/b compiles to 11 VALU (div_scale x2, rcp, 6 fma, div_fmas, div_fixup).  With y = RN(1/b)
@@ -337,9 +340,9 @@ MRT_DFN f3 random_cosine_direction_pre(float r1, float r2) {
 }
 // random_towards_sphere (pcg.cpp:125-133) given its two draws r1, r2 (sphere::pdf_generate, sphere.cpp:63-78)
 MRT_DFN f3 random_towards_sphere_pre(float r1, float r2, float radius, float dist_sq) {
-    float z = 1 + r2 * (sqrt_(1 - (radius * radius) / dist_sq) - 1);
+    float z = ref_fma(r2, sqrt_(1 - (radius * radius) / dist_sq) - 1, 1);  // pcg.cpp:128
     float phi = (2 * PI_F) * r1;
-    float q = sqrt_(1 - z * z);
+    float q = sqrt_(ref_fnma(z, z, 1));  // pcg.cpp:130-131
     float sp, cp;
     sincos_(phi, &sp, &cp);
     return f3{cp * q, sp * q, z};

@@ -93,8 +93,8 @@ MRT_DFN bool lin_prim_t(const OP& o, const Ray& r, float tmin, float tmax, float
         }
         const float ob = AX == 0 ? r.o.y : r.o.x, db = AX == 0 ? r.d.y : r.d.x;
         const float oc = AX == 2 ? r.o.y : r.o.z, dc = AX == 2 ? r.d.y : r.d.z;
-        const float pb = ob + t * db;
-        const float pc = oc + t * dc;
+        const float pb = ref_fma(t, db, ob);  // rect.cpp:32-33, 77-78, 138-139 (fused as shipped)
+        const float pc = ref_fma(t, dc, oc);
         *tout = t;
         return !back & !((t < tmin) | (t > tmax)) & !((pb < o.f[0]) | (pb > o.f[1]) | (pc < o.f[2]) | (pc > o.f[3]));
     }
@@ -121,15 +121,15 @@ MRT_DFN void lin_prim_rec_op(const MRT_CONST_AS LinOp& o, const Ray& r, float t,
         if constexpr (KIND == MRT_K_XY) {
             rec.n = f3{0, 0, ns};
             if (MRT_FAST_SNAP) rec.p.z = o.f[4];
-            if (needuv) { pb = r.o.x + t * r.d.x; pc = r.o.y + t * r.d.y; }
+            if (needuv) { pb = ref_fma(t, r.d.x, r.o.x); pc = ref_fma(t, r.d.y, r.o.y); }
         } else if constexpr (KIND == MRT_K_XZ) {
             rec.n = f3{0, ns, 0};
             if (MRT_FAST_SNAP) rec.p.y = o.f[4];
-            if (needuv) { pb = r.o.x + t * r.d.x; pc = r.o.z + t * r.d.z; }
+            if (needuv) { pb = ref_fma(t, r.d.x, r.o.x); pc = ref_fma(t, r.d.z, r.o.z); }
         } else {
             rec.n = f3{ns, 0, 0};
             if (MRT_FAST_SNAP) rec.p.x = o.f[4];
-            if (needuv) { pb = r.o.y + t * r.d.y; pc = r.o.z + t * r.d.z; }
+            if (needuv) { pb = ref_fma(t, r.d.y, r.o.y); pc = ref_fma(t, r.d.z, r.o.z); }
         }
         if (needuv) {
             rec.u = (pb - o.f[0]) / (o.f[1] - o.f[0]);
@@ -167,13 +167,13 @@ MRT_DFN void lin_prim_rec(const DScene& S, uint32_t node, const Ray& r, float t,
         return;
     }
     const float ns = nf[5];
-    // the rect's in-plane hit coordinates (rect.cpp:34-38: o + t * d on its two axes) are the
-    // record's point before any snapping, chosen by selects (a kind-indexed choice had become a
+    // the rect's in-plane hit coordinates (rect.cpp:32-33: o + t * d on its two axes, one fused
+    // scalar expression each as shipped), chosen by selects (a kind-indexed choice had become a
     // per-lane lookup table in scratch memory)
     const f3 p0 = rec.p;
-    const float pb = kind == MRT_K_YZ ? p0.y : p0.x;
-    const float pc = kind == MRT_K_XY ? p0.y : p0.z;
     const bool xy = kind == MRT_K_XY, xz = kind == MRT_K_XZ;
+    const float pb = kind == MRT_K_YZ ? ref_fma(t, r.d.y, r.o.y) : ref_fma(t, r.d.x, r.o.x);
+    const float pc = xy ? ref_fma(t, r.d.y, r.o.y) : ref_fma(t, r.d.z, r.o.z);
     rec.n = f3{xy || xz ? 0.0f : ns, xz ? ns : 0.0f, xy ? ns : 0.0f};
     if (MRT_FAST_SNAP) {
         rec.p.x = xy || xz ? p0.x : nf[4];

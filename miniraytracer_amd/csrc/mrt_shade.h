@@ -22,7 +22,7 @@ MRT_DFN float perlin_noise(const DScene& S, f3 p) {
             f3 ijk{(float)di, (float)dj, (float)dk};
             f3 weights = sub(f3{u, v, w}, ijk);
             f3 a = add(mul(ijk, uvw), mul(sub(f3{1, 1, 1}, ijk), sub(f3{1, 1, 1}, uvw)));
-            acc += ((a.x * a.y) * a.z) * dot(c, weights);
+            acc = ref_fma((a.x * a.y) * a.z, dot(c, weights), acc);  // texture.cpp:82-97
         }
     }
     return acc;
@@ -30,7 +30,7 @@ MRT_DFN float perlin_noise(const DScene& S, f3 p) {
 MRT_DFN float turbulence(const DScene& S, f3 p) {
     float acc = 0, weight = 1.0f;
     for (int i = 0; i < 7; i++) {
-        acc += weight * perlin_noise(S, p);
+        acc = ref_fma(weight, perlin_noise(S, p), acc);  // texture.cpp:160
         weight *= 0.5f;
         p = mulf(p, 2);
     }
@@ -155,9 +155,9 @@ MRT_DFN f3 leaf_pdf_generate(const DScene& S, const mrt_node& n, f3 origin, floa
     uint32_t k = MRT_NODE_KIND(n);
     if (k == MRT_K_XZ) {
         float a = dr.next(rng);
-        float x = n.f[0] + a * (n.f[1] - n.f[0]);
+        float x = ref_fma(a, n.f[1] - n.f[0], n.f[0]);  // rect.cpp:105 (left to right)
         float b = dr.next(rng);
-        float z = n.f[2] + b * (n.f[3] - n.f[2]);
+        float z = ref_fma(b, n.f[3] - n.f[2], n.f[2]);
         return sub(f3{x, n.f[4], z}, origin);
     }
     if ((F & FT_BSPHERE) && k == MRT_K_SPHERE) {
@@ -280,7 +280,7 @@ MRT_DFN Ray camera_ray(const DScene& S, Pcg& rng, float s, float t) {
     const MRT_CONST_AS mrt_camera& C = *cp;
     f3 rd = fmul(C.lens_radius, random_in_disk(rng));
     f3 offset = add(mulf(ld3(C.u), rd.x), mulf(ld3(C.v), rd.y));
-    float time = C.time0 + (C.time1 - C.time0) * randf(rng);
+    float time = ref_fma(C.time1 - C.time0, randf(rng), C.time0);  // camera.h:41
     f3 origin = ld3(C.origin);
     f3 dir = sub(sub(add(add(ld3(C.llcorner), fmul(s, ld3(C.horz))), fmul(t, ld3(C.vert))), origin), offset);
     return make_ray(add(origin, offset), dir, time, 0);
@@ -297,7 +297,7 @@ MRT_DFN void camera_ray_args(const DScene& S, Pcg& rng, float s, float t, f3* o,
     const MRT_CONST_AS mrt_camera& C = *cp;
     f3 rd = fmul(C.lens_radius, random_in_disk(rng));
     f3 offset = add(mulf(ld3(C.u), rd.x), mulf(ld3(C.v), rd.y));
-    *time = C.time0 + (C.time1 - C.time0) * randf(rng);
+    *time = ref_fma(C.time1 - C.time0, randf(rng), C.time0);  // camera.h:41
     f3 origin = ld3(C.origin);
     *dir = sub(sub(add(add(ld3(C.llcorner), fmul(s, ld3(C.horz))), fmul(t, ld3(C.vert))), origin), offset);
     *o = add(origin, offset);
@@ -356,14 +356,16 @@ MRT_DFN bool shade_hit(const DScene& S, PathState& ps, uint32_t max_bounces, con
         int inside = r.inside;
         // refract (vec3.h:185-198)
         const float ncosI = dot(r.d, facing);
-        const float sinT2 = (nio * nio) * (1.0f - ncosI * ncosI);
+        // the scalar expressions of refract / dielectric::scatter / fresnel_schlick, fused as
+        // shipped (vec3.h:187, 191; material.h:146, 109)
+        const float sinT2 = (nio * nio) * ref_fnma(ncosI, ncosI, 1.0f);
         if (sinT2 <= 1.0f) {
             const float cosT = sqrt_(1.0f - sinT2);
-            const float cs = cosI < 0 ? sqrt_(1.0f - (nio * nio) * (1.0f - cosI * cosI)) : cosI;
+            const float cs = cosI < 0 ? sqrt_(ref_fnma(nio * nio, ref_fnma(cosI, cosI, 1.0f), 1.0f)) : cosI;
             const float r0 = M.col[1];  // ((1 - ref) / (1 + ref))^2, computed on upload
-            const float reflect_prob = r0 + (1 - r0) * pow5_((1 - cs));
+            const float reflect_prob = ref_fma(1 - r0, pow5_((1 - cs)), r0);
             if (!(randf(ps.rng) < reflect_prob)) {
-                nd = add(fmul(nio, r.d), fmul(nio * -ncosI - cosT, facing));
+                nd = add(fmul(nio, r.d), fmul(ref_fms(nio, -ncosI, cosT), facing));
                 if (cosI < 0) {
                     inside--;
                     if (inside < 0) inside = 0;
@@ -511,14 +513,16 @@ MRT_DFN bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, c
         f3 nd = sub(r.d, fmul(2.0f * dot(r.d, rec.n), rec.n));  // reflect (vec3.h:178-181)
         int inside = r.inside;
         const float ncosI = dot(r.d, facing);
-        const float sinT2 = (nio * nio) * (1.0f - ncosI * ncosI);
+        // the scalar expressions of refract / dielectric::scatter / fresnel_schlick, fused as
+        // shipped (vec3.h:187, 191; material.h:146, 109)
+        const float sinT2 = (nio * nio) * ref_fnma(ncosI, ncosI, 1.0f);
         if (sinT2 <= 1.0f) {
             const float cosT = sqrt_(1.0f - sinT2);
-            const float cs = cosI < 0 ? sqrt_(1.0f - (nio * nio) * (1.0f - cosI * cosI)) : cosI;
+            const float cs = cosI < 0 ? sqrt_(ref_fnma(nio * nio, ref_fnma(cosI, cosI, 1.0f), 1.0f)) : cosI;
             const float r0 = M.col[1];  // ((1 - ref) / (1 + ref))^2, computed on upload
-            const float reflect_prob = r0 + (1 - r0) * pow5_((1 - cs));
+            const float reflect_prob = ref_fma(1 - r0, pow5_((1 - cs)), r0);
             if (!(randf(ps.rng) < reflect_prob)) {
-                nd = add(fmul(nio, r.d), fmul(nio * -ncosI - cosT, facing));
+                nd = add(fmul(nio, r.d), fmul(ref_fms(nio, -ncosI, cosT), facing));
                 if (cosI < 0) {
                     inside--;
                     if (inside < 0) inside = 0;

@@ -336,8 +336,8 @@ MRT_DFN WideNode mesh_wide(const DScene& S, uint32_t ref, const LStack& L) {
 MRT_DFN void sphere_uv(f3 p, float* u, float* v) {
     float phi = atan2_(p.z, p.x);
     float theta = asin_(p.y);
-    *u = 0.5f - phi * (1.0f / (2.0f * PI_F));
-    *v = 0.5f + theta * (1.0f / PI_F);
+    *u = ref_fnma(phi, 1.0f / (2.0f * PI_F), 0.5f);  // sphere.cpp:9
+    *v = ref_fma(theta, 1.0f / PI_F, 0.5f);           // sphere.cpp:10
 }
 
 template <uint32_t F>
@@ -396,8 +396,8 @@ MRT_DFN bool rect_hit(const mrt_node& n, const Ray& r, float tmin, float tmax, H
     if (t < tmin || t > tmax) return false;
     float ob = AX == 0 ? r.o.y : r.o.x, db = AX == 0 ? r.d.y : r.d.x;
     float oc = AX == 2 ? r.o.y : r.o.z, dc = AX == 2 ? r.d.y : r.d.z;
-    float pb = madd_det(t, db, ob);  // (the predicate's arithmetic: see madd_det)
-    float pc = madd_det(t, dc, oc);
+    float pb = ref_fma(t, db, ob);  // rect.cpp:32-33, 77-78, 138-139
+    float pc = ref_fma(t, dc, oc);
     if (pb < n.f[0] || pb > n.f[1] || pc < n.f[2] || pc > n.f[3]) return false;
     rec.t = t;
     if (full) {
@@ -731,7 +731,7 @@ MRT_DFN bool bvhw_leaf(const DScene& S, uint32_t ref, const Ray& r, float tmin, 
             return true;
         }
         // the second test repeats the first's predicate with the same operands and range: its
-        // arithmetic is contraction-proof (sphere_disc unfused, madd_det), so it hits again
+        // arithmetic is contraction-proof (explicit ref_f* / madd_det fusions, the rest unfused), so it hits again
         (void)leaf_prim_hit<F>(n, k, r, tmin, tmax, rec, true);
         return true;
     }
@@ -964,19 +964,19 @@ MRT_DFN void pop_ray(const LStack& L, uint32_t slot, Ray& r) {
 template <bool U = MRT_FAST_UNIT>
 MRT_DFN Ray rotate_ray(const Ray& ray, float s, float c) {
     f3 o = ray.o, d = ray.d;
-    o.x = c * ray.o.x - s * ray.o.z;
-    o.z = c * ray.o.z + s * ray.o.x;
-    d.x = c * ray.d.x - s * ray.d.z;
-    d.z = c * ray.d.z + s * ray.d.x;
+    o.x = ref_fms(c, ray.o.x, s * ray.o.z);  // scene_object.cpp:77-80
+    o.z = ref_fma(c, ray.o.z, s * ray.o.x);
+    d.x = ref_fms(c, ray.d.x, s * ray.d.z);
+    d.z = ref_fma(c, ray.d.z, s * ray.d.x);
     return make_ray_unit<U>(o, d, ray.time, 0);
 }
 // ... and the record back (scene_object.cpp:85-93)
 MRT_DFN void unrotate_rec(HitRec& rec, float s, float c) {
     f3 p = rec.p, nn = rec.n;
-    p.x = c * rec.p.x + s * rec.p.z;
-    p.z = c * rec.p.z - s * rec.p.x;
-    nn.x = c * rec.n.x + s * rec.n.z;
-    nn.z = c * rec.n.z - s * rec.n.x;
+    p.x = ref_fma(c, rec.p.x, s * rec.p.z);  // scene_object.cpp:87-91
+    p.z = ref_fms(c, rec.p.z, s * rec.p.x);
+    nn.x = ref_fma(c, rec.n.x, s * rec.n.z);
+    nn.z = ref_fms(c, rec.n.z, s * rec.n.x);
     rec.p = p;
     rec.n = nn;
 }

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cinttypes>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <limits>
@@ -263,11 +264,12 @@ struct Builder {
         for (int i = 0; i < 2; i++)
             for (int j = 0; j < 2; j++)
                 for (int k2 = 0; k2 < 2; k2++) {
-                    float x = (float)i * bb.max.x + (float)(1 - i) * bb.min.x;
-                    float y = (float)j * bb.max.y + (float)(1 - j) * bb.min.y;
-                    float z = (float)k2 * bb.max.z + (float)(1 - k2) * bb.min.z;
-                    float newx = o->cos_t * x + o->sin_t * z;
-                    float newz = o->cos_t * z - o->sin_t * x;
+                    // one scalar expression each, fused as shipped (x86 FMA, scene_object.cpp:54-59)
+                    float x = std::fma((float)i, bb.max.x, (float)(1 - i) * bb.min.x);
+                    float y = std::fma((float)j, bb.max.y, (float)(1 - j) * bb.min.y);
+                    float z = std::fma((float)k2, bb.max.z, (float)(1 - k2) * bb.min.z);
+                    float newx = std::fma(o->cos_t, x, o->sin_t * z);
+                    float newz = std::fma(o->cos_t, z, -(o->sin_t * x));
                     V3 t{newx, y, newz};
                     minbb = vmin(minbb, t);
                     maxbb = vmax(maxbb, t);
@@ -557,9 +559,9 @@ static BuiltScene random_scene(Builder& B, Pcg& rng, int n, float aspect, bool v
         for (int b = -half; b < half; b++) {
             float choose = randf(rng);
             float r1 = randf(rng);
-            float cx = (float)a + 0.9f * r1;
+            float cx = std::fma(0.9f, r1, (float)a);  // scene.cpp:78, fused as shipped
             float r2 = randf(rng);
-            float cz = (float)b + 0.9f * r2;
+            float cz = std::fma(0.9f, r2, (float)b);
             V3 center{cx, 0.2f, cz};
             if (length(center - V3{4, 0.2f, 0}) > 0.9f) {
                 HObj* s;
@@ -689,7 +691,7 @@ static BuiltScene book2_final(Builder& B, Pcg& rng, float aspect) {  // scene.cp
     for (int i = 0; i < nb; i++)
         for (int j = 0; j < nb; j++) {
             float w = 100;
-            float x0 = -1000 + i * w, z0 = -1000 + j * w, y0 = 0;
+            float x0 = std::fma((float)i, w, -1000.0f), z0 = std::fma((float)j, w, -1000.0f), y0 = 0;  // scene.cpp:418-419
             float x1 = x0 + w, y1 = 100 * (randf(rng) + 0.01f), z1 = z0 + w;
             boxes.push_back(B.box(V3{x0, y0, z0}, V3{x1, y1, z1}, green));
         }

@@ -3,7 +3,9 @@
  * Plain-C restatement of the reference render path, written recursively in the shape of the
  * reference's virtual calls so that it shares no structure with the HIP kernel's explicit-stack
  * walk.  Every function cites the reference code it restates.  Float operations follow the
- * reference's order; build with -ffp-contract=off (the reference's SSE intrinsics never fuse).
+ * reference's order; build with -ffp-contract=off (the reference's SSE intrinsics never fuse),
+ * and the reference's scalar expressions that the shipped build fuses (x86 FMA under clang's
+ * -ffp-contract=on: a product operand of a sum in one expression) are explicit fmaf() calls.
  * sin/cos/log/pow/atan2/asin follow the numerics contract of include/mrt_mathfn.h -- the functions
  * the exact reference build (oracle/_ref/mrt_ref_exact) interposes, so the two agree bit for bit.
  */
@@ -88,18 +90,18 @@ static V random_cosine_direction(pcg* r) {
     return v3(x, y, z);
 }
 static V random_on_sphere_uniform(pcg* r) {
-    float x = randf(r) * 2 - 1.0f;
+    float x = fmaf(randf(r), 2, -1.0f); /* pcg.cpp:101-103, fused as shipped */
     float phi = randf(r) * 2 * PI_F;
-    float s = sqrtf(1 - x * x);
+    float s = sqrtf(fmaf(-x, x, 1));
     return v3(x, cos_(phi) * s, sin_(phi) * s);
 }
 static V random_towards_sphere(pcg* r, float radius, float dist_sq) {
     float r1 = randf(r);
     float r2 = randf(r);
-    float z = 1 + r2 * (sqrtf(1 - radius * radius / dist_sq) - 1);
+    float z = fmaf(r2, sqrtf(1 - radius * radius / dist_sq) - 1, 1);
     float phi = 2 * PI_F * r1;
-    float x = cos_(phi) * sqrtf(1 - z * z);
-    float y = sin_(phi) * sqrtf(1 - z * z);
+    float x = cos_(phi) * sqrtf(fmaf(-z, z, 1));
+    float y = sin_(phi) * sqrtf(fmaf(-z, z, 1));
     return v3(x, y, z);
 }
 static uint64_t splitmix64(uint64_t z) {
@@ -168,8 +170,8 @@ static V sphere_center(const mrt_node* n, float time) {
 static void sphere_uv(V p, float* u, float* v) {
     float phi = atan2_(p.z, p.x);
     float theta = asin_(p.y);
-    *u = 0.5f - phi * (1.0f / (2.0f * PI_F));
-    *v = 0.5f + theta * (1.0f / PI_F);
+    *u = fmaf(-phi, 1.0f / (2.0f * PI_F), 0.5f);
+    *v = fmaf(theta, 1.0f / PI_F, 0.5f);
 }
 static int sphere_hit(const mrt_node* n, const ray* r, float tmin, float tmax, hit_record* rec) {
     rec->mat = n->mat;
@@ -177,8 +179,8 @@ static int sphere_hit(const mrt_node* n, const ray* r, float tmin, float tmax, h
     float radius = n->f[8];
     V oc = vsub(r->origin, cen);
     float b = vdot(oc, r->dir);
-    float c = vsdot(oc) - radius * radius;
-    float disc = b * b - c;
+    float c = fmaf(-radius, radius, vsdot(oc));
+    float disc = fmaf(b, b, -c);
     if (disc > 0) {
         float t = (-b - sqrtf(disc));
         if (t < tmax && t > tmin) {
@@ -210,8 +212,8 @@ static int rect_hit(const mrt_node* n, int ax, const ray* r, float tmin, float t
     float t = (n->f[4] - comp(r->origin, ax)) / comp(r->dir, ax);
     if (t < tmin || t > tmax) return 0;
     int ia = ax == 0 ? 1 : 0, ib = ax == 2 ? 1 : 2;
-    float a = comp(r->origin, ia) + t * comp(r->dir, ia);
-    float b = comp(r->origin, ib) + t * comp(r->dir, ib);
+    float a = fmaf(t, comp(r->dir, ia), comp(r->origin, ia));
+    float b = fmaf(t, comp(r->dir, ib), comp(r->origin, ib));
     if (a < n->f[0] || a > n->f[1] || b < n->f[2] || b > n->f[3]) return 0;
     rec->u = (a - n->f[0]) / (n->f[1] - n->f[0]);
     rec->v = (b - n->f[2]) / (n->f[3] - n->f[2]);
@@ -335,17 +337,17 @@ static int obj_hit(ctx* C, uint32_t id, const ray* r, float tmin, float tmax, hi
         if ((FLAGS(n) & MRT_F_HASBOX) && !aabb_hit(n->f, r, tmin, tmax)) return 0;
         float s = n->f[6], c = n->f[7];
         V o = r->origin, d = r->dir;
-        o.x = c * r->origin.x - s * r->origin.z;
-        o.z = c * r->origin.z + s * r->origin.x;
-        d.x = c * r->dir.x - s * r->dir.z;
-        d.z = c * r->dir.z + s * r->dir.x;
+        o.x = fmaf(c, r->origin.x, -(s * r->origin.z));
+        o.z = fmaf(c, r->origin.z, s * r->origin.x);
+        d.x = fmaf(c, r->dir.x, -(s * r->dir.z));
+        d.z = fmaf(c, r->dir.z, s * r->dir.x);
         ray rr = mkray(o, d, r->time, 0);
         if (obj_hit(C, n->a, &rr, tmin, tmax, rec)) {
             V p = rec->p, nn = rec->n;
-            p.x = c * rec->p.x + s * rec->p.z;
-            p.z = c * rec->p.z - s * rec->p.x;
-            nn.x = c * rec->n.x + s * rec->n.z;
-            nn.z = c * rec->n.z - s * rec->n.x;
+            p.x = fmaf(c, rec->p.x, s * rec->p.z);
+            p.z = fmaf(c, rec->p.z, -(s * rec->p.x));
+            nn.x = fmaf(c, rec->n.x, s * rec->n.z);
+            nn.z = fmaf(c, rec->n.z, -(s * rec->n.x));
             rec->p = p;
             rec->n = nn;
             return 1;
@@ -404,7 +406,7 @@ static float perlin_noise(const mrt_scene_view* v, V p) {
         for (int q = 0; q < 4; q++) {
             V weights = vsub(init, ijk[q]);
             V a = vadd(vmul(ijk[q], uvw), vmul(vsub(v3(1, 1, 1), ijk[q]), vsub(v3(1, 1, 1), uvw)));
-            acc += a.x * a.y * a.z * vdot(c[ii][q >> 1][q & 1], weights);
+            acc = fmaf(a.x * a.y * a.z, vdot(c[ii][q >> 1][q & 1], weights), acc);
         }
         for (int q = 0; q < 4; q++) ijk[q] = vadd(ijk[q], v3(1, 0, 0));
     }
@@ -423,7 +425,7 @@ static V tex_sample(const mrt_scene_view* v, uint32_t t, float u, float vv, V p)
         float acc = 0, weight = 1.0f;
         V pc = vscale(T->f[0], p);
         for (int i = 0; i < 7; i++) {
-            acc += weight * perlin_noise(v, pc);
+            acc = fmaf(weight, perlin_noise(v, pc), acc);
             weight *= 0.5f;
             pc = vscale(2, pc);
         }
@@ -491,9 +493,9 @@ static V obj_pdf_generate(ctx* C, uint32_t id, V origin, float time) {
     }
     case MRT_K_XZ: {
         float a = randf(&C->rng);
-        float x = n->f[0] + a * (n->f[1] - n->f[0]);
+        float x = fmaf(a, n->f[1] - n->f[0], n->f[0]);
         float b = randf(&C->rng);
-        float z = n->f[2] + b * (n->f[3] - n->f[2]);
+        float z = fmaf(b, n->f[3] - n->f[2], n->f[2]);
         return vsub(v3(x, n->f[4], z), origin);
     }
     case MRT_K_SPHERE: {
@@ -541,14 +543,14 @@ static V trace(ctx* C, tstate* T, const ray* r, uint32_t depth) {
                 V reflected = vsub(r->dir, vscale(dp, hrec.n));
                 ray sr;
                 float ncosI = vdot(r->dir, facing);
-                float sinT2 = (nio * nio) * (1.0f - ncosI * ncosI);
+                float sinT2 = (nio * nio) * fmaf(-ncosI, ncosI, 1.0f);
                 if (sinT2 <= 1.0f) {
                     float cosT = sqrtf(1.0f - sinT2);
-                    V refracted = vadd(vscale(nio, r->dir), vscale(nio * -ncosI - cosT, facing));
-                    float cs = cosI < 0 ? sqrtf(1.0f - nio * nio * (1.0f - cosI * cosI)) : cosI;
+                    V refracted = vadd(vscale(nio, r->dir), vscale(fmaf(nio, -ncosI, -cosT), facing));
+                    float cs = cosI < 0 ? sqrtf(fmaf(-(nio * nio), fmaf(-cosI, cosI, 1.0f), 1.0f)) : cosI;
                     float r0 = (1 - ref) / (1 + ref);
                     r0 = r0 * r0;
-                    float reflect_prob = r0 + (1 - r0) * pow_((1 - cs), 5);
+                    float reflect_prob = fmaf(1 - r0, pow_((1 - cs), 5), r0);
                     if (randf(&C->rng) < reflect_prob) {
                         sr = mkray(hrec.p, reflected, r->time, r->inside);
                     } else {
@@ -613,7 +615,7 @@ static ray get_ray(ctx* C, float s, float t) {
     const mrt_camera* c = &C->v->camera;
     V rd = vscale(c->lens_radius, random_in_disk(&C->rng));
     V offset = vadd(vscale(rd.x, ld(c->u)), vscale(rd.y, ld(c->v)));
-    float time = c->time0 + (c->time1 - c->time0) * randf(&C->rng);
+    float time = fmaf(c->time1 - c->time0, randf(&C->rng), c->time0);
     V dir = vsub(vsub(vadd(vadd(ld(c->llcorner), vscale(s, ld(c->horz))), vscale(t, ld(c->vert))), ld(c->origin)), offset);
     return mkray(vadd(ld(c->origin), offset), dir, time, 0);
 }

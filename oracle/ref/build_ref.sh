@@ -5,12 +5,16 @@
 # (read-only), together with oracle/ref/harness.cpp into two oracle binaries in oracle/_ref/:
 #
 #   mrt_ref        reference as shipped: clang++ -std=c++20 -O3 -fno-exceptions -fno-rtti
-#                  (clang/clang_build_linux.sh:23-29), default FP contraction, glibc libm.
+#                  (clang/clang_build_linux.sh:23-29), default FP contraction (-ffp-contract=on:
+#                  x86 FMA wherever one scalar expression multiplies and adds), glibc libm.
 #                  -march=x86-64-v3 instead of -march=native so the binary also runs on the GPU
-#                  box's host CPU (it is the cpu_baseline of bench.py).
-#   mrt_ref_exact  same sources with -ffp-contract=off and the float libm calls interposed by
-#                  (float)f((double)x) (harness.cpp, MRT_MATHMATCH).  This is the bit-exact pin for
-#                  the C restatement (oracle/mrt_oracle.c) and, through it, the HIP kernel.
+#                  box's host CPU (it is the cpu_baseline of bench.py); both have FMA.
+#   mrt_ref_exact  the same build (same flags, so the same fused multiply-adds) with the float libm
+#                  calls interposed by (float)f((double)x) (harness.cpp, MRT_MATHMATCH): the
+#                  reference as shipped with the project's transcendentals.  This is the bit-exact
+#                  pin of the exact numerics contract: the C restatement (oracle/mrt_oracle.c), the
+#                  HIP kernel and the CPU backend.  (Rounds 1-3 pinned a -ffp-contract=off build;
+#                  the two differ only by the fused sites)
 #
 # Two compile fixes, both applied without writing into /root/reference and without copying the
 # source tree: mrt_math.h:66 is an '#error INSERT LZCNT INTRINSIC HERE' placeholder for non-MSVC
@@ -55,12 +59,12 @@ build() {  # name extra-flags
 }
 
 build mrt_ref
-build mrt_ref_exact -ffp-contract=off -DMRT_MATHMATCH
-# numerics-diagnosis builds (MRT_REF_VARIANTS=1): which difference between the two builds above
-# makes their images differ -- contraction alone (shipped flags, project libm) or libm alone
-# (no contraction, glibc) -- and what unrestricted contraction (-ffp-contract=fast) does
+build mrt_ref_exact -DMRT_MATHMATCH
+# numerics-diagnosis builds (MRT_REF_VARIANTS=1): the reference with no contraction at all (with
+# the project's transcendentals: the rounds 1-3 pin; with glibc) and with unrestricted contraction
+# (-ffp-contract=fast), to measure what each difference does to the image
 if [ -n "${MRT_REF_VARIANTS:-}" ]; then
-    build mrt_ref_mm -DMRT_MATHMATCH
+    build mrt_ref_nofma -ffp-contract=off -DMRT_MATHMATCH
     build mrt_ref_glibc -ffp-contract=off
     build mrt_ref_fastc -ffp-contract=fast
 fi
