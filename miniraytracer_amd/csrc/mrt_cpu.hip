@@ -106,7 +106,6 @@ mrt_status mrt_cpu_scene_create(const mrt_scene_view* v, mrt_cpu_scene** out) {
     S.mwide = T.wide.data();
     S.mwide_n = (uint32_t)T.wide.size();
     S.bwide = T.bwide.data();
-    S.bwide4 = T.bwide4.data();
     S.bprims = T.bprims.data();
     S.tri_geo = c->tri_geo.data();
     S.tri_nrm = c->tri_nrm.data();

@@ -160,27 +160,20 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
-    // per wave: its stacks and queues ([slot][word][lane]), then (MeshTreeOf) its mesh treelet
-    const uint32_t words = (P.lds_frames * 2 + P.lds_rays * 11 + P.lds_mesh + P.lds_save + LK * 4 + PathQ<F>::words) * 64 +
-                           (MeshTreeOf<F>::on ? P.mtree_n * 16u : 0u);
+    // per wave: its stacks and queues ([slot][word][lane])
+    const uint32_t words = (P.lds_frames * 2 + P.lds_rays * 11 + P.lds_mesh + P.lds_save + LK * 4 + PathQ<F>::words) * 64;
     uint32_t* wb = lds + wave * words;
     uint32_t* const wmesh = wb + P.lds_frames * 128 + P.lds_rays * 704;
     float4* tree = nullptr;
-    if constexpr (MeshTreeOf<F>::on) {
-        // the wave's own copy of the top mesh BVH nodes (one-wave groups: no other wave reads it)
-        tree = reinterpret_cast<float4*>(wb + words - P.mtree_n * 16u);
-        for (uint32_t i = lane; i < P.mtree_n * 4u; i += 64u) tree[i] = reinterpret_cast<const float4*>(P.sc.mwide)[i];
-        __syncthreads();
-    }
     if constexpr (TreeOf<F>::on) {
         // the workgroup's copy of the top wide nodes (after every wave's own region), filled once
         // before any wave starts a path; no other barrier follows in this persistent kernel
         tree = reinterpret_cast<float4*>(lds + (TreeOf<F>::wg / 64u) * words);
-        for (uint32_t i = threadIdx.x; i < P.tree_n * (MRT_BVH4 ? BVH4_Q : 4u); i += blockDim.x) tree[i] = P.tree_src[i];
+        for (uint32_t i = threadIdx.x; i < P.tree_n * 4u; i += blockDim.x) tree[i] = P.tree_src[i];
         __syncthreads();
     }
     const LStack Ls{wb, (float*)(wb + P.lds_frames * 128), wmesh, (float*)(wmesh + P.lds_mesh * 64), lane, tree,
-                    TreeOf<F>::on ? P.tree_n : MeshTreeOf<F>::on ? P.mtree_n : 0u};
+                    TreeOf<F>::on ? P.tree_n : 0u};
     // the wave's queue of path starts ([word][entry], PathQ): after the fold levels
     float* const Lq = (float*)(wmesh + (P.lds_mesh + P.lds_save + LK * 4) * 64);
     const DScene& S = P.sc;
@@ -404,49 +397,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
 #endif
     constexpr bool kShared = (F & FT_MESH) == 0 && (MRT_SHARED_WIDE || !PathOcc<F>::kWide);
     constexpr bool kResume = MRT_SIG_OF(F) == SIG_ROOM_MESH;
-    if constexpr (kResumeLin<F>) {
-        // Linear hit programs with bvh_node subtrees (random spheres, book2): the intersection is
-        // RESUMABLE per lane (mrt_resume.h): one iteration = (1) idle lanes take new paths; (2) the
-        // lanes walking a BVH subtree step until few still walk and enough others have work; (3) one
-        // sweep over the program for the lanes between walks (each from its own op); (4) the lanes
-        // whose intersection is complete shade, and end their path or begin the next segment.
-        ResumeState w;
-        w.st = RS_IDLE;
-        HitRec rec;
-        for (;;) {
-            take_paths([&](float u, float v) {
-                ps.r = camera_ray(S, ps.rng, u, v);
-                rs_begin(w, ps.r, Ls);
-            });
-            if (!__any(active)) break;
-            PH_MARK(ph, 0);
-            while (__any(w.st == RS_WALK)) {
-                if (w.st == RS_WALK) {
-                    const uint32_t res = bvhw_step<F>(S, w, rec, Ls, 0.001f);
-                    if (res != 0u) rs_walk_end<F>(S, w, rec, res);
-                }
-                if ((uint32_t)__popcll(__ballot(w.st == RS_WALK)) <= P.walk_min &&
-                    (uint32_t)__popcll(__ballot(w.st == RS_SWEEP || (!active && !exhausted))) >= MRT_WALK_OTHER)
-                    break;  // others can sweep / start paths
-            }
-            PH_MARK(ph, 11);
-            rs_sweep<F>(S, w, rec, Ls, ps.rng, 0.001f);
-            PH_MARK(ph, 1);
-            if (w.st == RS_DONE) {
-                const bool hit = rs_finish_hit<F>(S, w, ps.r, rec, Ls);
-                f3 L{0.0f, 0.0f, 0.0f};
-                const bool ended = shade_hit<F, LK>(S, ps, P.max_bounces, lev, hit, rec, &L, ph);
-                PH_MARK(ph, 2);
-                if (ended) {
-                    finish_path(L);
-                    w.st = RS_IDLE;
-                } else {
-                    rs_begin(w, ps.r, Ls);
-                }
-            }
-            PH_MARK(ph, 3);
-        }
-    } else if constexpr (kShared) {
+    if constexpr (kShared) {
         // One iteration: (1) every lane with a ray traces one segment; a path that ends is folded
         // and stored; (2) lanes without a path take new ones (camera ray arguments); (3) ONE
         // make_ray for every lane with a next ray -- camera and scattered rays alike, instead of one
@@ -636,18 +587,9 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
             // at least one step per iteration for every walking lane (no lane starves), then more
             // while enough lanes walk or too few have anything else to do
             while (__any(phase == PH_WALK)) {
-                bool step = phase == PH_WALK;
-                if (P.leaf_min) {
-                    // leaves postponed: a lane holding a leaf waits while other lanes still descend,
-                    // until leaf_min lanes hold one (or none descends), so the triangle test runs
-                    // with more lanes at once instead of beside every inner-node step
-                    const bool leafy = step && (ref & MESH_LEAF) != 0u;
-                    const uint32_t nl = (uint32_t)__popcll(__ballot(leafy)), nw = (uint32_t)__popcll(__ballot(step));
-                    if (nl < P.leaf_min && nl < nw) step = step && !leafy;
-                }
-                if (step) {
+                if (phase == PH_WALK) {
                     const mrt_node mn = ld_node(const_ptr(S.nodes) + prog[kMeshPC].node);
-                    const uint32_t st = mesh_step<MeshTreeOf<F>::on, true>(S, mn, ps.r, 0.001f, w.closest, rec, Ls, ref, msp, w.hdone);
+                    const uint32_t st = mesh_step<false, true>(S, mn, ps.r, 0.001f, w.closest, rec, Ls, ref, msp, w.hdone);
                     if (st == 1u) w.hnode = kMeshPC;  // w.closest = the hit's t, w.hdone set
                     phase = st != 0u ? PH_DONE : PH_WALK;
                 }
@@ -746,9 +688,7 @@ const KernelTable& mrtd::kernel_table_exact() {
         {PathQ<kVariants[0]>::words, PathQ<kVariants[1]>::words, PathQ<kVariants[2]>::words, PathQ<kVariants[3]>::words,
          PathQ<kVariants[4]>::words, PathQ<kVariants[5]>::words, PathQ<kVariants[6]>::words},
         {kBox6Walk<kVariants[0]>, kBox6Walk<kVariants[1]>, kBox6Walk<kVariants[2]>, kBox6Walk<kVariants[3]>,
-         kBox6Walk<kVariants[4]>, kBox6Walk<kVariants[5]>, kBox6Walk<kVariants[6]>},
-        {MeshTreeOf<kVariants[0]>::on, MeshTreeOf<kVariants[1]>::on, MeshTreeOf<kVariants[2]>::on, MeshTreeOf<kVariants[3]>::on,
-         MeshTreeOf<kVariants[4]>::on, MeshTreeOf<kVariants[5]>::on, MeshTreeOf<kVariants[6]>::on}};
+         kBox6Walk<kVariants[4]>, kBox6Walk<kVariants[5]>, kBox6Walk<kVariants[6]>}};
     static_assert(kNumVariants == 7, "one table entry per variant");
     return t;
 }

@@ -4,7 +4,7 @@
 // FMA contraction, hardware reciprocal/sqrt, f32 transcendentals).  DESIGN.md "Numerics contracts".
 #pragma once
 #include <hip/hip_runtime.h>
-#include "mrt_resume.h"
+#include "mrt_shade.h"
 
 namespace mrtd {
 
@@ -41,10 +41,8 @@ struct PathParams {
     uint32_t lev_rows;                    // levels per lane (max_bounces, at least 1)
     uint32_t lds_frames, lds_rays, lds_mesh, lds_save;  // LDS stack slots / words per lane
     uint32_t walk_min;                    // resumable mesh walk: yield once at most this many lanes walk
-    uint32_t leaf_min;                    // ... and its leaves wait until this many lanes hold one (0: off)
     const float4* tree_src;               // TreeOf<F>::on kernels: BvhWide nodes copied to LDS at start
     uint32_t tree_n;                      // how many (the first tree_n of the breadth-first array)
-    uint32_t mtree_n;                     // MeshTreeOf<F>::on kernels: MeshWide nodes each wave copies to its LDS
 };
 
 typedef void (*path_kernel_t)(PathParams);
@@ -61,16 +59,6 @@ typedef void (*path_kernel_t)(PathParams);
 #endif
 // one claim must cover a whole wave's idle lanes (the pool hands out at most 64 at once)
 static_assert(MRT_TAIL_BATCH >= 64u && MRT_BATCH >= MRT_TAIL_BATCH, "claims must be at least a wave wide");
-
-// Linear programs with bvh_node subtrees run the resumable interpreter (mrt_resume.h); its query ray
-// lives in the LDS save area (15 words per lane slot, as instances need).  Measured SLOWER than the
-// lockstep interpreter (book2 3.77 vs 4.64, random spheres 5.82 vs 6.02 Grays/s), so
-// off by default: MRT_RESUME_LIN=1 builds it (A/B)
-#ifndef MRT_RESUME_LIN
-#define MRT_RESUME_LIN 0
-#endif
-template <uint32_t F>
-static constexpr bool kResumeLin = MRT_RESUME_LIN && (F & FT_LIN) != 0 && (F & FT_BVHW) != 0 && MRT_SIG_OF(F) == SIG_NONE;
 
 // kernel variants by scene features (the first instantiated superset is launched); FT_LIN
 // variants need the scene's linear hit program (mrt_lin.h), FT_ALL runs any graph.  The same list
@@ -95,7 +83,6 @@ struct KernelTable {
     uint32_t tree[kNumVariants];  // 1: the kernel reads the top BvhWide nodes from an LDS treelet
     uint32_t pq[kNumVariants];    // LDS words per lane slot of the kernel's queue of path starts
     uint32_t box6_walk[kNumVariants];  // 1: Cornell shape walked by cornell_fast_hit when op 8 is MRT_F_BOX6
-    uint32_t mtree[kNumVariants];      // 1: each wave keeps a treelet of the top mesh BVH nodes in LDS
 };
 const KernelTable& kernel_table_exact();
 const KernelTable& kernel_table_fast();

@@ -29,10 +29,9 @@ enum : uint32_t {
 };
 
 // one op = the node's own record (no second load): code = op | kind << 8 | flags << 16 | level << 24
-// (the nesting level the op is tested at).  Host-filled extras for the resumable interpreter
-// (mrt_resume.h): prim / mesh / bvh / volume ops carry the enclosing instance's op index in f[11]
-// (MRT_NONE outside instances), a BVHW op its subtree's root ref in skip, an INST_END op its
-// instance op's index in skip.
+// (the nesting level the op is tested at).  Host-filled extras: prim / mesh / bvh / volume ops
+// carry the enclosing instance's op index in f[11] (MRT_NONE outside instances), a BVHW op its
+// subtree's root ref in skip, an INST_END op its instance op's index in skip.
 struct LinOp {
     uint32_t code, node, skip, mat;
     float f[12];
@@ -42,8 +41,6 @@ static_assert(sizeof(LinOp) == 64, "LinOp is one 64 B scalar load");
 #define LOP_OP(o) ((o).code & 0xFFu)
 #define LOP_KIND(o) (((o).code >> 8) & 0xFFu)
 #define LOP_FLAGS(o) (((o).code >> 16) & 0xFFu)
-#define LOP_LVL(o) (((o).code >> 24) & 0xFFu)
-#define LOP_INST_OF(o) (__float_as_uint((o).f[11]))
 
 MRT_DFN uint32_t op_flags(const LinOp& o) { return LOP_FLAGS(o); }
 #if defined(__HIP_DEVICE_COMPILE__)

@@ -239,7 +239,6 @@ struct PathLaunch {
     uint32_t vgprs = 0;
     uint32_t wg = 64;     // threads per workgroup
     uint32_t tree_n = 0;  // BvhWide nodes kept in each workgroup's LDS (treelet kernels)
-    uint32_t mtree_n = 0;  // MeshWide nodes kept in each wave's LDS (mesh treelet kernels)
     uint32_t lds_save = 0;  // LDS words per lane slot for the query ray parked during instances
 };
 
@@ -329,7 +328,6 @@ struct mrt_scene {
     uint32_t features = 0, variant = 0;
     uint32_t lds_frames = 0, lds_rays = 0, lds_mesh = 0, lds_save = 0;
     uint32_t walk_min = 32;  // resumable mesh walk threshold (PathParams::walk_min)
-    uint32_t leaf_min = 0;   // its leaf postponement (PathParams::leaf_min)
     PathLaunch pl[2];            // [0] exact contract, [1] tolerance contract (MRT_RF_FAST)
     size_t max_threads = 0;  // largest path-kernel grid in threads (per-lane level rows)
     std::vector<hipEvent_t> ev;  // [2*k]: start/stop of path-kernel launch k of the last render
@@ -440,8 +438,7 @@ struct LinCompiler {
     std::vector<LinOp> prog;
     int max_lvl = 0;
     uint32_t inst_pc = MRT_NONE;  // op index of the enclosing instance while its subtree is emitted
-    // code = op | kind << 8 | flags << 16 | nesting level << 24 (the level the op is tested at: the
-    // resumable interpreter, mrt_resume.h, restarts a lane mid-program without replaying the levels)
+    // code = op | kind << 8 | flags << 16 | nesting level << 24 (the level the op is tested at)
     LinOp op_of(uint32_t code, uint32_t id, int lvl) {
         const mrt_node& n = nodes[id];
         LinOp o{};
@@ -647,11 +644,11 @@ mrt_status mrt_internal_scene_tables(const mrt_scene_view* v, SceneTables* T) {
         for (mrt_node& n : nodes)
             if ((n.kind & 0xFF) == MRT_K_MESH) n.b = ref_of(n.a);
         if (!ok) return mrt_internal_fail(MRT_ERR_INVALID, "mesh BVH outside the device encoding (leaf > 127 triangles or > 2^24 triangles)");
-        // the top levels first (the per-wave LDS treelet of the mesh kernels, mrt_kernels.hip)
+        // the top 63 nodes first, breadth-first: the hot top levels share cache lines
         std::vector<uint32_t*> mroots;
         for (mrt_node& n : nodes)
             if ((n.kind & 0xFF) == MRT_K_MESH) mroots.push_back(&n.b);
-        bfs_order(wide, mroots, MESH_LEAF, MRT_MESH_TREE_MAX);
+        bfs_order(wide, mroots, MESH_LEAF, 63u);
     }
     // bvh_node subtrees whose leaves are primitives / object_lists of primitives (and of boxes of
     // primitives) -> wide nodes; the subtree root becomes an MRT_K_BVHW node (a = root ref)
@@ -761,66 +758,9 @@ mrt_status mrt_internal_scene_tables(const mrt_scene_view* v, SceneTables* T) {
             if ((n.kind & 0xFF) == MRT_K_BVHW) broots.push_back(&n.a);
         bfs_order(bwide, broots, BVHW_LEAF);
     }
-    // the same subtrees as Bvh4 nodes (mrt_trace.h), breadth-first across all roots (the treelet
-    // holds the top levels); a BVHW node's b = its root Bvh4 node
-    std::vector<float4> bwide4;
-    {
-        const uint32_t nb = (uint32_t)bwide.size();
-        std::vector<uint32_t> id4(nb, MRT_NONE), order;
-        auto enq = [&](uint32_t c) -> uint32_t {
-            if (c & BVHW_LEAF) return c;
-            if (id4[c] == MRT_NONE) { id4[c] = (uint32_t)order.size(); order.push_back(c); }
-            return id4[c];
-        };
-        for (mrt_node& n : nodes)
-            if ((n.kind & 0xFF) == MRT_K_BVHW) n.b = enq(n.a);
-        for (size_t q = 0; q < order.size(); q++) {
-            const BvhWide W = bwide[order[q]];
-            float f[44] = {};
-            uint32_t ref[4] = {0, 0, 0, 0}, ord[3] = {W.order, 0xFFu, 0xFFu}, meta = 0;
-            if (W.flags & 1u) meta |= BVH4_A_BOX;
-            if (W.flags & 2u) meta |= BVH4_B_BOX;
-            if (W.lref == W.rref) meta |= BVH4_B_SAME;
-            for (int k = 0; k < 3; k++) {
-                f[0 + k] = W.lmin[k]; f[4 + k] = W.lmax[k]; f[8 + k] = W.rmin[k]; f[12 + k] = W.rmax[k];
-            }
-            for (int x = 0; x < 2; x++) {
-                const uint32_t X = x ? W.rref : W.lref;
-                if (X & BVHW_LEAF) {  // a leaf child: its first slot, no box of its own
-                    ref[2 * x] = X;
-                    meta |= BVH4_S_VALID(2 * x);
-                    continue;
-                }
-                const BvhWide C = bwide[X];
-                ord[1 + x] = C.order;
-                for (int y = 0; y < 2; y++) {
-                    const int k = 2 * x + y;
-                    if (y == 1 && C.rref == C.lref) continue;  // bvh_node of one object: visited once
-                    ref[k] = enq(y ? C.rref : C.lref);
-                    meta |= BVH4_S_VALID(k);
-                    if (C.flags & (1u << y)) {
-                        meta |= BVH4_S_BOX(k);
-                        for (int a = 0; a < 3; a++) {
-                            f[16 + 6 * k + a] = y ? C.rmin[a] : C.lmin[a];
-                            f[16 + 6 * k + 3 + a] = y ? C.rmax[a] : C.lmax[a];
-                        }
-                    }
-                }
-            }
-            uint32_t w[44];
-            memcpy(w, f, sizeof(w));
-            w[3] = ref[0]; w[7] = ref[1]; w[11] = ref[2]; w[15] = ref[3];
-            w[40] = ord[0]; w[41] = ord[1]; w[42] = ord[2]; w[43] = meta;
-            for (int k = 0; k < 11; k++) {
-                float4 v;
-                memcpy(&v, w + 4 * k, 16);
-                bwide4.push_back(v);
-            }
-        }
-    }
     GraphCheck gc{nodes, v};
-    // stack words: one per level for the binary walk, up to three per Bvh4 level
-    gc.bvhw_depth = std::max(bvhw_depth, 3 * ((bvhw_depth + 1) / 2) + 1);
+    // stack words: one per level for the binary walk
+    gc.bvhw_depth = bvhw_depth;
     gc.walk(v->root, 0, 0, false, 0);
     if (!gc.ok) return mrt_internal_fail(MRT_ERR_INVALID, gc.why.c_str());
     if (v->biased != MRT_NONE) {
@@ -882,7 +822,6 @@ mrt_status mrt_internal_scene_tables(const mrt_scene_view* v, SceneTables* T) {
     T->nodes.swap(nodes);
     T->wide.swap(wide);
     T->bwide.swap(bwide);
-    T->bwide4.swap(bwide4);
     T->bprims.swap(bprims);
     T->dmats.swap(dmats);
     T->bleaf.swap(bleaf);
@@ -916,17 +855,9 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     UP(T.nodes.data(), T.nodes.size(), &S.nodes);
     UP(v->children, v->n_children, &S.children);
     UP(v->mesh_nodes, v->n_mesh_nodes, &S.mnodes);
-#if MRT_MESH_SOA  // layout experiment (mrt_trace.h mesh_wide): four 16-B planes
-    std::vector<float4> msoa(T.wide.size() * 4);
-    for (size_t i = 0; i < T.wide.size(); i++)
-        for (size_t k = 0; k < 4; k++) memcpy(&msoa[k * T.wide.size() + i], reinterpret_cast<const char*>(&T.wide[i]) + 16 * k, 16);
-    UP(msoa.data(), msoa.size(), (const float4**)&S.mwide);
-#else
     UP(T.wide.data(), T.wide.size(), &S.mwide);
-#endif
     S.mwide_n = (uint32_t)T.wide.size();
     UP(T.bwide.data(), T.bwide.size(), &S.bwide);
-    UP(T.bwide4.data(), T.bwide4.size(), &S.bwide4);
     UP(T.bprims.data(), T.bprims.size(), &S.bprims);
     UP((const float4*)v->tri_geo, (size_t)v->n_tris * 3, &S.tri_geo);
     UP((const float4*)v->tri_nrm, (size_t)v->n_tris * 3, &S.tri_nrm);
@@ -963,17 +894,12 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     s->lds_frames = lin_kernel ? 0 : (uint32_t)std::max(T.max_frames - 1, 0);
     s->lds_rays = lin_kernel ? 0 : (uint32_t)T.max_rays;
     s->lds_mesh = (uint32_t)T.max_mesh;
-    // the query ray parked in LDS: instances (scene_hit_lin) and the resumable interpreter (mrt_resume.h)
-    s->lds_save = (lin_kernel && (kVariants[s->variant] & (FT_INST | (MRT_RESUME_LIN ? FT_BVHW : 0u)))) ? 15u : 0u;
+    // the query ray parked in LDS: instances (scene_hit_lin)
+    s->lds_save = (lin_kernel && (kVariants[s->variant] & FT_INST)) ? 15u : 0u;
     // resumable mesh walk: deeper pod_bvh trees keep the wave walking longer
     s->walk_min = T.wide.size() >= 2048 ? 40u : 32u;  // inner nodes: bunny 2937, teapot ~1045
     if (const char* e = getenv("MRT_WALK_MIN"))  // sweep hook (tools/ab_walk.sh)
         if (*e) s->walk_min = (uint32_t)atoi(e);
-    // leaves postponed (off): at 16 lanes bunny +1.6% in one session, +-0.3% in the next; teapot
-    // -4%; 8 lanes -2% / -3% (profiles/r03_ab_session2.txt)
-    s->leaf_min = 0u;
-    if (const char* e = getenv("MRT_LEAF_MIN"))  // sweep hook
-        if (*e) s->leaf_min = (uint32_t)atoi(e);
     const std::vector<BvhWide>& bwide = T.bwide;
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
@@ -1006,8 +932,8 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
         if (tabs[k]->tree[s->variant]) {
             // the LDS the resident groups leave free, split among them: the treelet of each group
             const size_t per = std::min<size_t>((160u * 1024u) / nb, (size_t)prop.sharedMemPerBlock);
-            const uint32_t node_bytes = MRT_BVH4 ? BVH4_Q * 16u : 64u;  // (Bvh4 / BvhWide)
-            const uint32_t n_nodes = MRT_BVH4 ? (uint32_t)(T.bwide4.size() / BVH4_Q) : (uint32_t)bwide.size();
+            const uint32_t node_bytes = 64u;  // BvhWide
+            const uint32_t n_nodes = (uint32_t)bwide.size();
             uint32_t cap = per > L.lds_bytes ? (uint32_t)((per - L.lds_bytes) / node_bytes) : 0u;
 #ifdef MRT_EXPERIMENTS
             if (const char* e = getenv("MRT_TREELET_NODES"))  // sweep hook
@@ -1015,19 +941,6 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
 #endif
             L.tree_n = std::min(cap, n_nodes);
             L.lds_bytes += (size_t)L.tree_n * node_bytes;
-        }
-        if (tabs[k]->mtree[s->variant]) {
-            // each wave's copy of the top mesh nodes, in the LDS its resident groups leave free
-            // (so the treelet never costs occupancy)
-            const size_t per = (160u * 1024u) / (size_t)nb;
-            const uint32_t node_bytes = 64u;  // MeshWide
-            uint32_t cap = per > L.lds_bytes ? (uint32_t)((per - L.lds_bytes) / node_bytes) : 0u;
-#ifdef MRT_EXPERIMENTS
-            if (const char* e = getenv("MRT_MESH_TREE_NODES"))  // sweep hook
-                if (*e) cap = std::min<uint32_t>(cap, (uint32_t)atoi(e));
-#endif
-            L.mtree_n = std::min<uint32_t>({cap, MRT_MESH_TREE_MAX, (uint32_t)T.wide.size()});
-            L.lds_bytes += (size_t)L.mtree_n * 64u;
         }
         L.vgprs = (uint32_t)fa.numRegs;
 #ifdef MRT_EXPERIMENTS
@@ -1262,10 +1175,8 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.lds_mesh = s->lds_mesh;
         P.lds_save = PL.lds_save;
         P.walk_min = s->walk_min;
-        P.leaf_min = s->leaf_min;
-        P.tree_src = MRT_BVH4 ? s->S.bwide4 : reinterpret_cast<const float4*>(s->S.bwide);
+        P.tree_src = reinterpret_cast<const float4*>(s->S.bwide);
         P.tree_n = PL.tree_n;
-        P.mtree_n = PL.mtree_n;
         P.pixels = s->d_pixels;
         P.sdist = s->d_sdist;
         P.npix = s->npix;
@@ -1485,7 +1396,7 @@ extern "C" mrt_status mrt_scene_kernel_info(const mrt_scene* s, mrt_kernel_info*
     out->prog_ops = s->prog_ops;
     out->vgprs = L.vgprs;
     out->wg = L.wg;
-    out->tree_nodes = L.tree_n ? L.tree_n : L.mtree_n;  // BvhWide per workgroup, or MeshWide per wave
+    out->tree_nodes = L.tree_n;  // BvhWide nodes per workgroup
     return MRT_OK;
 }
 

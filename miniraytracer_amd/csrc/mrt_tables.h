@@ -10,7 +10,6 @@ struct SceneTables {
     std::vector<mrt_node> nodes;        // the view's nodes (+ NEEDUV / SLOWDIV flags, fused TRROTY, BVHW roots)
     std::vector<mrtd::MeshWide> wide;   // pod_bvh inner nodes, both child boxes inline
     std::vector<mrtd::BvhWide> bwide;   // bvh_node subtrees as wide nodes, breadth-first
-    std::vector<float4> bwide4;         // the same as Bvh4 nodes (BVH4_Q float4 each, mrt_trace.h)
     std::vector<mrt_node> bprims;       // their leaves' primitive runs
     std::vector<mrtd::DMat> dmats;      // materials (+ inline constant colour, dielectric quotients)
     std::vector<mrt_node> bleaf;        // leaves of scene.biased_objects

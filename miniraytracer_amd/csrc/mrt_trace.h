@@ -51,24 +51,6 @@ struct BvhWide {
 #define BVHW_MAX_RUN 0x7Fu
 #define BVHW_FIRST_MASK 0xFFFFFFu
 
-// Two levels of a bvh_node subtree in one node (MRT_BVH4): a bvh_node N, its children A and B
-// (their boxes, as N's wide node holds them) and their children -- four slots s0, s1 (A's) and s2,
-// s3 (B's), each a leaf run or another Bvh4 node, with its box when it has one.  A child that is a
-// leaf itself takes its first slot, no box of its own (its box is A's / B's).  One visit replaces two
-// dependent ones of the binary walk: the four slots are tested together and visited in the order the
-// reference's recursion visits them (N's order, then A's / B's; the first subtree that hits ends).
-// float4 q[0..3] = Amin|ref0, Amax|ref1, Bmin|ref2, Bmax|ref3; q[4..9] = the slots' boxes
-// (min.xyz, max.xyz each); q[10] = N's order, A's order, B's order, meta.
-#define BVH4_Q 11u
-#define BVH4_A_BOX 0x1u          // A has a box
-#define BVH4_B_BOX 0x2u
-#define BVH4_S_BOX(k) (0x4u << (k))    // slot k has a box
-#define BVH4_S_VALID(k) (0x40u << (k))
-#define BVH4_B_SAME 0x400u       // B == A (bvh_node with one object): its slots are never visited
-#ifndef MRT_BVH4
-#define MRT_BVH4 0
-#endif
-
 // A wide node (MeshWide / BvhWide: both children's boxes, refs, order, flags) fetched whole: four
 // 16-byte loads issued together, so one memory round trip per node visit.  (Read field by field,
 // the compiler split the node into dependent loads -- left box, right box, order, then the child
@@ -149,7 +131,7 @@ struct DScene {
     const mrt_node* __restrict__ nodes;
     const uint32_t* __restrict__ children;
     const mrt_mesh_node* __restrict__ mnodes;
-    const MeshWide* __restrict__ mwide;   // (MRT_MESH_SOA device upload: four float4 planes of mwide_n nodes each)
+    const MeshWide* __restrict__ mwide;
     uint32_t mwide_n;
     const BvhWide* __restrict__ bwide;
     const mrt_node* __restrict__ bprims;  // leaf primitive runs of the wide subtrees
@@ -168,7 +150,6 @@ struct DScene {
     uint32_t root, biased, sky;
     mrt_camera cam;
     const mrt_camera* __restrict__ camp;  // the camera in HBM, read at each path start (scalar loads)
-    const float4* __restrict__ bwide4;    // the bvh_node subtrees as Bvh4 nodes (MRT_BVH4), BVH4_Q float4 each
 };
 
 
@@ -231,20 +212,6 @@ struct TreeOf {
                                ((F & (FT_BVHW | FT_TEX | FT_VOLUME)) != 0 || !(F & FT_LIN));
     static constexpr uint32_t wg = on ? MRT_TREE_WG : 64u;  // threads per path-kernel workgroup
 };
-// Hot pod_bvh nodes in LDS for the resumable mesh kernels (room + mesh, 7 one-wave groups per
-// SIMD): each wave keeps its OWN copy of the top MeshWide nodes (the upload numbers the first
-// MRT_MESH_TREE_MAX of them breadth-first) in the LDS its stacks leave free at that occupancy --
-// copied once at kernel start, no workgroup barrier, no occupancy given up.
-#ifndef MRT_MESH_TREE_MAX
-#define MRT_MESH_TREE_MAX 63u
-#endif
-#ifndef MRT_MESH_TREE
-#define MRT_MESH_TREE 0  // measured: bunny -2.6%, teapot -4.6%; kept as an option
-#endif
-template <uint32_t F>
-struct MeshTreeOf {
-    static constexpr bool on = MRT_MESH_TREE && (F & FT_MESH) != 0 && ((F >> 16) & 0xFFu) == 2u /* SIG_ROOM_MESH (mrt_sig.h) */;
-};
 // A treelet node through LDS instructions (ds_read_b128: LDS latency, lgkmcnt only), instead of
 // the flat load that can reach LDS or memory per lane (a flat access waits on both counters)
 #ifndef MRT_TREE_DS
@@ -301,35 +268,11 @@ MRT_DFN bool is_prim(uint32_t kind) {
            ((F & FT_BVHW) && kind == MRT_K_BVHW);
 }
 
-// Layout experiment (north star: "BVH node array ... flattened to SoA in HBM"): with MRT_MESH_SOA
-// the device copy of the mesh wide nodes is four planes -- piece k (16 B: a child's min + ref,
-// max + ref, ...) of node i at plane k, index i -- instead of one 64-B record per node.  A visit
-// then reads four lines, one per plane, instead of one; A/B in DESIGN.md (N3).
-#ifndef MRT_MESH_SOA
-#define MRT_MESH_SOA 0
-#endif
+// a mesh wide node (one 64-B record, four 16-B loads in flight together; a four-plane SoA layout
+// was measured slower)
 template <bool TREE>
 MRT_DFN WideNode mesh_wide(const DScene& S, uint32_t ref, const LStack& L) {
-#if MRT_MESH_SOA && defined(__HIP_DEVICE_COMPILE__)
-    (void)L;
-    const float4* b = reinterpret_cast<const float4*>(S.mwide);
-    const size_t n = S.mwide_n;
-    float4 a = b[ref], c1 = b[n + ref], c2 = b[2 * n + ref], d = b[3 * n + ref];
-    asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(a.z), "+v"(a.w), "+v"(c1.x), "+v"(c1.y), "+v"(c1.z), "+v"(c1.w));
-    asm volatile("" : "+v"(c2.x), "+v"(c2.y), "+v"(c2.z), "+v"(c2.w), "+v"(d.x), "+v"(d.y), "+v"(d.z), "+v"(d.w));
-    WideNode w;
-    w.lmin = f3{a.x, a.y, a.z};
-    w.lref = __float_as_uint(a.w);
-    w.lmax = f3{c1.x, c1.y, c1.z};
-    w.rref = __float_as_uint(c1.w);
-    w.rmin = f3{c2.x, c2.y, c2.z};
-    w.order = __float_as_uint(c2.w);
-    w.rmax = f3{d.x, d.y, d.z};
-    w.flags = __float_as_uint(d.w);
-    return w;
-#else
     return wide_at<TREE>(S.mwide, ref, L);
-#endif
 }
 
 // get_sphere_uv (sphere.cpp:6-11)
@@ -837,92 +780,10 @@ MRT_DFN bool bvhw_hit(const DScene& S, const mrt_node& n, const Ray& r, float tm
 #endif
 }
 
-// bvh_node::hit over Bvh4 nodes (MRT_BVH4): the walk of bvhw_hit, two levels per node visit.
-// n.b = the root Bvh4 node, n.f[0..5] = the root bvh_node's box.
-struct Node4 {
-    float4 a0, a1, b0, b1, s0, s1, s2, s3, s4, s5, m;
-};
-template <typename P>
-MRT_DFN Node4 node4_from(P q) {
-    Node4 n{q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7], q[8], q[9], q[10]};
-#if defined(__HIP_DEVICE_COMPILE__)
-    // all eleven 16-B pieces in flight together (see load_wide_q)
-    asm volatile("" : "+v"(n.a0.x), "+v"(n.a0.y), "+v"(n.a0.z), "+v"(n.a0.w), "+v"(n.a1.x), "+v"(n.a1.y), "+v"(n.a1.z), "+v"(n.a1.w));
-    asm volatile("" : "+v"(n.b0.x), "+v"(n.b0.y), "+v"(n.b0.z), "+v"(n.b0.w), "+v"(n.b1.x), "+v"(n.b1.y), "+v"(n.b1.z), "+v"(n.b1.w));
-    asm volatile("" : "+v"(n.s0.x), "+v"(n.s0.y), "+v"(n.s0.z), "+v"(n.s0.w), "+v"(n.s1.x), "+v"(n.s1.y), "+v"(n.s1.z), "+v"(n.s1.w));
-    asm volatile("" : "+v"(n.s2.x), "+v"(n.s2.y), "+v"(n.s2.z), "+v"(n.s2.w), "+v"(n.s3.x), "+v"(n.s3.y), "+v"(n.s3.z), "+v"(n.s3.w));
-    asm volatile("" : "+v"(n.s4.x), "+v"(n.s4.y), "+v"(n.s4.z), "+v"(n.s4.w), "+v"(n.s5.x), "+v"(n.s5.y), "+v"(n.s5.z), "+v"(n.s5.w));
-    asm volatile("" : "+v"(n.m.x), "+v"(n.m.y), "+v"(n.m.z), "+v"(n.m.w));
-#endif
-    return n;
-}
-// Bvh4 node `ref`: from the LDS treelet (LDS instructions) when it holds it
-template <bool TREE>
-MRT_DFN Node4 node4_at(const DScene& S, uint32_t ref, const LStack& L) {
-    if constexpr (TREE) {
-        if (ref < L.tree_b) {
-#if defined(__HIP_DEVICE_COMPILE__)
-            return node4_from((const MRT_LDS_AS float4*)L.tree + (size_t)ref * BVH4_Q);
-#else
-            return node4_from(L.tree + (size_t)ref * BVH4_Q);
-#endif
-        }
-    }
-    return node4_from(S.bwide4 + (size_t)ref * BVH4_Q);
-}
-template <uint32_t F>
-MRT_DFN bool bvhw4_hit(const DScene& S, const mrt_node& n, const Ray& r, float tmin, float tmax, HitRec& rec, bool full,
-                                          const LStack& L) {
-    if (!aabb_hit(n.f, n.f + 3, r, tmin, tmax)) return false;
-    uint32_t ref = n.b, sp = 0;
-    for (;;) {
-        while (!(ref & BVHW_LEAF)) {
-            const Node4 Q = node4_at<TreeOf<F>::on>(S, ref, L);
-            const float4 &a0 = Q.a0, &a1 = Q.a1, &b0 = Q.b0, &b1 = Q.b1, &m = Q.m;
-            const float4 &s0 = Q.s0, &s1 = Q.s1, &s2 = Q.s2, &s3 = Q.s3, &s4 = Q.s4, &s5 = Q.s5;
-            const uint32_t meta = __float_as_uint(m.w);
-            const float bA[6] = {a0.x, a0.y, a0.z, a1.x, a1.y, a1.z}, bB[6] = {b0.x, b0.y, b0.z, b1.x, b1.y, b1.z};
-            const float sb[24] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w, s2.x, s2.y, s2.z, s2.w,
-                                  s3.x, s3.y, s3.z, s3.w, s4.x, s4.y, s4.z, s4.w, s5.x, s5.y, s5.z, s5.w};
-            const bool hA = !(meta & BVH4_A_BOX) || aabb_hit(bA, bA + 3, r, tmin, tmax);
-            const bool hB = !(meta & BVH4_B_SAME) && (!(meta & BVH4_B_BOX) || aabb_hit(bB, bB + 3, r, tmin, tmax));
-            auto slot_hit = [&](int k) {
-                return (meta & BVH4_S_VALID(k)) && (!(meta & BVH4_S_BOX(k)) || aabb_hit(sb + 6 * k, sb + 6 * k + 3, r, tmin, tmax));
-            };
-            const bool h0 = slot_hit(0) && hA, h1 = slot_hit(1) && hA, h2 = slot_hit(2) && hB, h3 = slot_hit(3) && hB;
-            const uint32_t r0 = __float_as_uint(a0.w), r1 = __float_as_uint(a1.w), r2 = __float_as_uint(b0.w), r3 = __float_as_uint(b1.w);
-            // the reference's visiting order: N's closer child first, inside it that child's closer
-            // child (selects, not indexed arrays: a per-lane index into a private array is scratch)
-            const bool nA = (__float_as_uint(m.x) & r.mask) != 0;
-            const bool aL = (__float_as_uint(m.y) & r.mask) != 0, bL = (__float_as_uint(m.z) & r.mask) != 0;
-            const bool hAn = aL ? h0 : h1, hAf = aL ? h1 : h0, hBn = bL ? h2 : h3, hBf = bL ? h3 : h2;
-            const uint32_t rAn = aL ? r0 : r1, rAf = aL ? r1 : r0, rBn = bL ? r2 : r3, rBf = bL ? r3 : r2;
-            const bool v0 = nA ? hAn : hBn, v1 = nA ? hAf : hBf, v2 = nA ? hBn : hAn, v3 = nA ? hBf : hAf;
-            const uint32_t c0 = nA ? rAn : rBn, c1 = nA ? rAf : rBf, c2 = nA ? rBn : rAn, c3 = nA ? rBf : rAf;
-            // later subtrees pushed deepest-last so they pop in visiting order
-            if (v3 && (v0 || v1 || v2)) L.mesh[(sp++) * 64 + L.lane] = c3;
-            if (v2 && (v0 || v1)) L.mesh[(sp++) * 64 + L.lane] = c2;
-            if (v1 && v0) L.mesh[(sp++) * 64 + L.lane] = c1;
-            if (v0 || v1 || v2 || v3) {
-                ref = v0 ? c0 : v1 ? c1 : v2 ? c2 : c3;
-            } else {
-                if (sp == 0) return false;
-                ref = L.mesh[(--sp) * 64 + L.lane];
-            }
-        }
-        if (bvhw_leaf<F>(S, ref, r, tmin, tmax, rec, full)) return true;
-        if (sp == 0) return false;
-        ref = L.mesh[(--sp) * 64 + L.lane];
-    }
-}
 template <uint32_t F>
 MRT_DFN bool bvhw_walk(const DScene& S, const mrt_node& n, const Ray& r, float tmin, float tmax, HitRec& rec, bool full,
                                           const LStack& L) {
-#if MRT_BVH4
-    return bvhw4_hit<F>(S, n, r, tmin, tmax, rec, full, L);
-#else
     return bvhw_hit<F>(S, n, r, tmin, tmax, rec, full, L);
-#endif
 }
 
 template <uint32_t F>
