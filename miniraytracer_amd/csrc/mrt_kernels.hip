@@ -152,8 +152,12 @@ template <uint32_t F> struct PathLevLds {
 template <uint32_t F> struct PathQ {
     static constexpr bool on = MRT_PATHQ && (F & FT_MESH) == 0 && !TreeOf<F>::on;
     // LDS words per lane slot: o, dir, time, PCG state + inc, index (12); + the wave's claim state
-    static constexpr uint32_t words = on ? 13u : 0u;
+    // (+ a deferred dielectric hit's point, normal, material: MRT_DEFER_DIEL)
+    static constexpr uint32_t words = on ? 13u + (MRT_DEFER_DIEL ? 7u : 0u) : 0u;
 };
+#ifndef MRT_DEFER_K
+#define MRT_DEFER_K 16u  // deferred dielectric lanes that trigger the shared shading (MRT_DEFER_DIEL)
+#endif
 template <uint32_t F>
 __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per_eu(MRT_OCC(F)))) MRT_PATH_KERNEL(PathParams P) {
     constexpr uint32_t LK = PathLevLds<F>::K;
@@ -413,12 +417,24 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
         f3 st_v{0.0f, 0.0f, 0.0f};
         uint32_t st_off = 0;  // byte offset of the path's radiance (a launch chunk is < 4 GiB)
         bool st_pend = false;
+#if MRT_DEFER_DIEL
+        bool dpend = false;  // this lane's hit waits for the shared dielectric shading
+        float* const Ld = Lq + 13u * 64u + lane;  // its parked point, normal, material ([word][lane])
+        auto defer = [&](const HitRec& rec) {
+            Ld[0] = rec.p.x; Ld[64] = rec.p.y; Ld[128] = rec.p.z;
+            Ld[192] = rec.n.x; Ld[256] = rec.n.y; Ld[320] = rec.n.z;
+            Ld[384] = __uint_as_float(rec.mat);
+        };
+#else
+        constexpr bool dpend = false;
+        auto defer = nullptr;
+#endif
         for (;;) {
             bool want_ray = false;
             // the next ray's arguments: written and read within one iteration (declared here, a
             // field a branch leaves unset is dead, not carried round the loop in copied registers)
             PendRay pr;
-            if (active) {
+            if (active && !dpend) {
                 f3 L{0.0f, 0.0f, 0.0f};  // (left undefined, it was carried round the loop in copied registers)
                 // (the held store is issued inside, after the hit, beside the material load)
                 const bool ended = trace_split<F, LK>(S, ps, P.max_bounces, lev, Ls, &L, &pr, ph, [&]() {
@@ -429,7 +445,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                         dst[2] = st_v.z;
                     }
                     st_pend = false;
-                });
+                }, defer);
                 PH_MARK(ph, 2);
                 if (ended) {
                     st_v = end_path(ps, lev, L);
@@ -438,6 +454,10 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                     if (P.path_rays) P.path_rays[idx] = ps.rays();
                     done_rays += ps.rays();
                     active = false;
+#if MRT_DEFER_DIEL
+                } else if (pr.kind == 3u) {
+                    dpend = true;
+#endif
                 } else {
                     want_ray = true;
                 }
@@ -520,6 +540,24 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                 break;
             }
             PH_MARK(ph, 0);
+#if MRT_DEFER_DIEL
+            {
+                // the parked dielectric hits shaded together once enough wait (or nothing else is left)
+                const uint32_t np = (uint32_t)__popcll(__ballot(dpend));
+                if (np != 0u && (np >= MRT_DEFER_K || np == (uint32_t)__popcll(__ballot(active)))) {
+                    if (dpend) {
+                        const f3 p{Ld[0], Ld[64], Ld[128]}, n{Ld[192], Ld[256], Ld[320]};
+                        const DMat M = S.mats[__float_as_uint(Ld[384])];
+                        pr.o = p;
+                        pr.time = ps.r.time;
+                        pr.kind = 0u;
+                        dielectric_scatter(M, ps.r, n, ps.rng, &pr);
+                        want_ray = true;
+                        dpend = false;
+                    }
+                }
+            }
+#endif
             BSTATC(15, active);
             if (want_ray) {
                 BSTATC(12, pr.kind != 0);

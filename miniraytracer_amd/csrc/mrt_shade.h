@@ -1,5 +1,7 @@
 // mrt_shade.h -- textures, materials, pdfs and one trace() segment (main.cpp:66-118)
 #pragma once
+#include <cstddef>
+#include <type_traits>
 #include "mrt_sig.h"
 
 namespace mrtd {
@@ -434,16 +436,64 @@ struct PendRay {
     float time;
     int inside;
     f3 att, n;      // diffuse scatter: attenuation, normal
-    uint32_t kind;  // 0: nothing after the ray; 1: lambertian mix; 2: isotropic
+    uint32_t kind;  // 0: nothing after the ray; 1: lambertian mix; 2: isotropic; 3: dielectric deferred
 };
+
+// dielectric::scatter (material.h:121-175) of a hit with normal n for ray r: the next ray's
+// direction and inside count in *pr (its origin and time are set by the caller)
+MRT_DFN void dielectric_scatter(const DMat& M, const Ray& r, f3 n, Pcg& rng, PendRay* pr) {
+    const float ref = M.p;
+    const float cosI = -dot(r.d, n);
+    f3 facing;
+    float nio;
+    if (cosI < 0) {
+        facing = f3{-n.x, -n.y, -n.z};
+        nio = ref;
+    } else {
+        facing = n;
+        nio = M.col[0];  // 1.0f / ref, computed on upload (the same IEEE quotient)
+    }
+    f3 nd = sub(r.d, fmul(2.0f * dot(r.d, n), n));  // reflect (vec3.h:178-181)
+    int inside = r.inside;
+    const float ncosI = dot(r.d, facing);
+    // the scalar expressions of refract / dielectric::scatter / fresnel_schlick, fused as
+    // shipped (vec3.h:187, 191; material.h:146, 109)
+    const float sinT2 = (nio * nio) * ref_fnma(ncosI, ncosI, 1.0f);
+    if (sinT2 <= 1.0f) {
+        const float cosT = sqrt_(1.0f - sinT2);
+        const float cs = cosI < 0 ? sqrt_(ref_fnma(nio * nio, ref_fnma(cosI, cosI, 1.0f), 1.0f)) : cosI;
+        const float r0 = M.col[1];  // ((1 - ref) / (1 + ref))^2, computed on upload
+        const float reflect_prob = ref_fma(1 - r0, pow5_((1 - cs)), r0);
+        if (!(randf(rng) < reflect_prob)) {
+            nd = add(fmul(nio, r.d), fmul(ref_fms(nio, -ncosI, cosT), facing));
+            if (cosI < 0) {
+                inside--;
+                if (inside < 0) inside = 0;
+            } else {
+                inside++;
+            }
+        }
+    }
+    pr->dir = nd;
+    pr->inside = inside;
+}
+
+// Dielectric deferral (experiment, MRT_DEFER_DIEL): a lane whose hit needs the
+// dielectric branch parks its hit (point, normal) and sits out the next iterations' walks until
+// enough lanes need the branch, which then runs once for all of them.  Same operations, same RNG
+// draws per path: results unchanged.
+#ifndef MRT_DEFER_DIEL
+#define MRT_DEFER_DIEL 0
+#endif
 
 // trace_segment up to the next ray's constructor arguments.  Returns true when the path has
 // ended (radiance in *L); otherwise *pr holds the next ray's arguments.
 // `flush` runs once the hit is known, before the material is read (the path loop issues the
 // previous path's radiance store there).
-template <uint32_t F, uint32_t LK, typename FLUSH>
+template <uint32_t F, uint32_t LK, typename FLUSH, typename DEFER = std::nullptr_t>
 MRT_DFN bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev,
-                                            const LStack& Ls, f3* L, PendRay* pr, PhaseClock& ph, FLUSH&& flush) {
+                                            const LStack& Ls, f3* L, PendRay* pr, PhaseClock& ph, FLUSH&& flush,
+                                            DEFER defer = nullptr) {
     HitRec rec;
     Ray& r = ps.r;
     bool hit;
@@ -499,40 +549,14 @@ MRT_DFN bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, c
     }
     if (M.kind == MRT_M_DIELECTRIC) {  // dielectric::scatter (material.h:121-175)
         BSTAT(5);
-        const float ref = M.p;
-        const float cosI = -dot(r.d, rec.n);
-        f3 facing;
-        float nio;
-        if (cosI < 0) {
-            facing = f3{-rec.n.x, -rec.n.y, -rec.n.z};
-            nio = ref;
-        } else {
-            facing = rec.n;
-            nio = M.col[0];  // 1.0f / ref, computed on upload (the same IEEE quotient)
+#if MRT_DEFER_DIEL
+        if constexpr (!std::is_same<DEFER, std::nullptr_t>::value) {  // shaded later, with other lanes'
+            defer(rec);
+            pr->kind = 3u;
+            return false;
         }
-        f3 nd = sub(r.d, fmul(2.0f * dot(r.d, rec.n), rec.n));  // reflect (vec3.h:178-181)
-        int inside = r.inside;
-        const float ncosI = dot(r.d, facing);
-        // the scalar expressions of refract / dielectric::scatter / fresnel_schlick, fused as
-        // shipped (vec3.h:187, 191; material.h:146, 109)
-        const float sinT2 = (nio * nio) * ref_fnma(ncosI, ncosI, 1.0f);
-        if (sinT2 <= 1.0f) {
-            const float cosT = sqrt_(1.0f - sinT2);
-            const float cs = cosI < 0 ? sqrt_(ref_fnma(nio * nio, ref_fnma(cosI, cosI, 1.0f), 1.0f)) : cosI;
-            const float r0 = M.col[1];  // ((1 - ref) / (1 + ref))^2, computed on upload
-            const float reflect_prob = ref_fma(1 - r0, pow5_((1 - cs)), r0);
-            if (!(randf(ps.rng) < reflect_prob)) {
-                nd = add(fmul(nio, r.d), fmul(ref_fms(nio, -ncosI, cosT), facing));
-                if (cosI < 0) {
-                    inside--;
-                    if (inside < 0) inside = 0;
-                } else {
-                    inside++;
-                }
-            }
-        }
-        pr->dir = nd;
-        pr->inside = inside;
+#endif
+        dielectric_scatter(M, r, rec.n, ps.rng, pr);
         return false;
     }
     // lambertian / isotropic (material.h:48-74): the direction now, the pdfs after the ray exists
