@@ -47,9 +47,10 @@ using namespace mrtd;
 // variant on MI355X (DESIGN.md "Occupancy").
 // (compact variants -- Cornell, Cornell room + mesh, plain interpreter -- reach 80 VGPRs without
 // spills at 6; built without SLP vectorisation (Makefile), the wide-feature variants run best at
-// 4 waves (128 VGPRs) and the room + mesh variant at 7 (72 VGPRs, no LDS fold levels))
+// 6 waves (80 VGPRs; round 4, with MRT_TREE_WG 768: 4 waves before) and the room + mesh variant
+// at 7 (72 VGPRs, no LDS fold levels))
 #ifndef MRT_WPE_WIDE
-#define MRT_WPE_WIDE 4
+#define MRT_WPE_WIDE (MRT_FAST ? 6 : 4)
 #endif
 #ifndef MRT_WPE_LIN
 #define MRT_WPE_LIN (MRT_FWD_FOLD ? 7 : 6)  // forward fold: no LDS levels, 72 VGPRs (C2 +1%)
@@ -62,7 +63,7 @@ using namespace mrtd;
 #endif
 template <uint32_t F> struct PathOcc {
     static constexpr bool kWide = (F & (FT_BVHW | FT_TEX | FT_VOLUME)) != 0 || !(F & FT_LIN);
-    static constexpr int W = kWide ? MRT_WPE_WIDE
+    static constexpr int W = kWide ? (!(F & FT_LIN) ? 4 : MRT_WPE_WIDE)
                              : ((F & FT_MESH) != 0 ? MRT_WPE_MESH : (MRT_SIG_OF(F) != SIG_NONE ? MRT_WPE_LIN : MRT_WPE_LIN_GEN));
 };
 #if defined(MRT_EXPERIMENTS) && defined(MRT_PHASES)  // build ONE of the two TUs with it

@@ -193,24 +193,28 @@ struct LStack {
     uint32_t tree_b;
 };
 
-// Hot BVH nodes in LDS (north star): kernels of the bvh_node scenes run one 16-wave workgroup
-// per CU, and that group keeps the top levels of the scene's bvh_node subtrees (breadth-first
-// wide-node numbering: the first tree_b nodes) in the LDS its waves' stacks leave free.  Measured
-// on MI355X (DESIGN.md "Hot nodes in LDS"): random spheres +14%, book2 +3.6%; for the pod_bvh
-// kernels (7 waves per SIMD, no LDS to spare at one-wave groups) bigger groups cost more than the
-// treelet gained, so they keep one-wave groups and no treelet.
+// Hot BVH nodes in LDS (north star): kernels of the bvh_node scenes run two 12-wave workgroups
+// per CU (6 waves per SIMD, MRT_WPE_WIDE), and each group keeps the top levels of the scene's
+// bvh_node subtrees (breadth-first wide-node numbering: the first tree_b nodes) in the LDS its
+// waves' stacks leave free.  Measured on MI355X (DESIGN.md "Hot nodes in LDS"): random spheres
+// +14%, book2 +3.6%; for the pod_bvh kernels (7 waves per SIMD, no LDS to spare at one-wave
+// groups) bigger groups cost more than the treelet gained, so they keep one-wave groups and no
+// treelet.  (Round 4: 2 x 12 waves over 1 x 16 -- book2 +7.4%, random spheres +9%; 2 x 10, 2 x 14
+// and 2 x 16 waves slower: book2 -29%, -19%, -32%, profiles/r04_ab.txt.)
 #ifndef MRT_TREELET
 #define MRT_TREELET 1
 #endif
 #ifndef MRT_TREE_WG
-#define MRT_TREE_WG 1024
+#define MRT_TREE_WG (MRT_FAST ? 768 : 1024)  // the exact contract's kernels keep 1 x 16 waves (no A/B there)
 #endif
 template <uint32_t F>
 struct TreeOf {
     // the kernels of bvh_node scenes (wide-node walks); the same test as PathOcc::kWide
     static constexpr bool on = MRT_TREELET && (F & FT_BVHW) != 0 &&
                                ((F & (FT_BVHW | FT_TEX | FT_VOLUME)) != 0 || !(F & FT_LIN));
-    static constexpr uint32_t wg = on ? MRT_TREE_WG : 64u;  // threads per path-kernel workgroup
+    // threads per path-kernel workgroup (the generic machine, no linear program, keeps 1 x 16
+    // waves: at 6 waves per SIMD it spills)
+    static constexpr uint32_t wg = !on ? 64u : (F & FT_LIN) ? (uint32_t)(MRT_TREE_WG) : 1024u;
 };
 // A treelet node through LDS instructions (ds_read_b128: LDS latency, lgkmcnt only), instead of
 // the flat load that can reach LDS or memory per lane (a flat access waits on both counters)
