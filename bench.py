@@ -142,6 +142,7 @@ def cpu_baseline(args):
             ra = run(total)
             res["value_all_cores"] = round(ra["mrays_per_s"], 3)
             res["sample_all_cores"] = f"-threads {total} (os.cpu_count()): {ra['rays']} rays in {ra['trace_seconds']:.2f} s"
+        res.update(contention_free(args, used, sample))
         return res
     import miniraytracer_amd as m
     sc = m.select_scene(args.scene, args.width / args.height)
@@ -152,6 +153,23 @@ def cpu_baseline(args):
     return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": used, "cores_used": used,
             "cores_total": total, "cores_quota": quota, "kind": "port",
             "sample": sample + f", C restatement oracle/liboracle.so, {rays} rays in {dt:.2f} s"}
+
+
+def contention_free(args, threads, sample):
+    """The reference's shared std::atomic ray counter (main.cpp:55, 68) throttles its threads (SURVEY
+    0: 14.3 -> 62.5 Mrays/s on 8 cores when removed).  The contention-free figure here is the
+    product's CPU backend (MRT_DEVICE_CPU: the same hot-path source compiled for the host, scalar
+    code, exact contract, per-thread ray counters) on the same threads and sample: a port without
+    the reference's SSE Vec3, so not the reference's own contention-free speed."""
+    import miniraytracer_amd as m
+    sc = m.select_scene(args.scene, args.width / args.height)
+    r = m.Renderer(sc, "cpu")
+    t0 = time.perf_counter()
+    _, rays = r.render(m.render_desc(args.width, args.height, args.cpu_spp, depth=args.depth, threads=threads))
+    dt = time.perf_counter() - t0
+    return {"value_contention_free": round(rays / dt / 1e6, 3), "kind_contention_free": "port",
+            "sample_contention_free": sample + f", the product's CPU backend (per-thread ray counters, scalar host build), "
+                                               f"{rays} rays in {dt:.2f} s on {threads} threads"}
 
 
 def pmc_path(args):
