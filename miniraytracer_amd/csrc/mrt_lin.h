@@ -26,6 +26,11 @@ enum : uint32_t {
     LOP_BVHW = 7,      // bvh_node subtree as wide nodes (per-lane traversal, bvhw_hit)
     LOP_VOLUME = 8,    // constant_volume; the next op (LOP_VBOUND) is its primitive boundary
     LOP_VBOUND = 9,
+    // tolerance-contract program only (lin_rewrite_fast, mrt_sig.h): the inward-facing rects of one
+    // object_list that bound a box (a room's walls) as one slab test; the next op (LOP_ROOMDATA)
+    // holds each face's node
+    LOP_ROOM = 10,
+    LOP_ROOMDATA = 11,
 };
 
 // one op = the node's own record (no second load): code = op | kind << 8 | flags << 16 | level << 24
@@ -233,6 +238,41 @@ MRT_DFN LinOp lin_fetch_op(const MRT_CONST_AS LinOp& o) {
     }
     return r;
 }
+// LOP_ROOM (tolerance contract): the room's walls -- one-sided rects facing into the box
+// [f[0..2], f[3..5]], face k = axis * 2 + side present when bit k of o.node is set -- as one slab
+// test: a ray that meets the box leaves it through the face of its smallest far-plane distance,
+// and that face, if the room has it, is the wall hit (a face crossed going in is back-facing and
+// missed, rect.cpp:26-30).  *face = the exit face.
+MRT_DFN bool lin_room_hit(const MRT_CONST_AS LinOp& o, const Ray& r, float tmin, float tmax, float* t, uint32_t* face) {
+    const float t0x = (o.f[0] - r.o.x) * r.inv.x, t1x = (o.f[3] - r.o.x) * r.inv.x;
+    const float t0y = (o.f[1] - r.o.y) * r.inv.y, t1y = (o.f[4] - r.o.y) * r.inv.y;
+    const float t0z = (o.f[2] - r.o.z) * r.inv.z, t1z = (o.f[5] - r.o.z) * r.inv.z;
+    const float fx = fmaxf(t0x, t1x), fy = fmaxf(t0y, t1y), fz = fmaxf(t0z, t1z);
+    const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+    const float tf = fminf(fminf(fx, fy), fz);
+    const uint32_t a = tf == fz ? 2u : (tf == fy ? 1u : 0u);  // ties to the later axis
+    const float da = a == 2u ? r.d.z : (a == 1u ? r.d.y : r.d.x);
+    const uint32_t k = a * 2u + (da > 0.0f ? 1u : 0u);
+    *t = tf;
+    *face = k;
+    return (tn <= tf) & (((o.node >> k) & 1u) != 0u) & (tf >= tmin) & (tf <= tmax);
+}
+// an object_list flagged MRT_F_BOX6 (box.h:12-20, planes in f[6..11]) as one slab test
+// (tolerance contract, box6_leaf_hit); *child = the entry face's position among its six rects
+// (box.h order: xy at max z, xy at min z, xz at max y, xz at min y, yz at max x, yz at min x)
+MRT_DFN bool lin_box6_hit(const MRT_CONST_AS LinOp& o, const Ray& r, float tmin, float tmax, float* t, uint32_t* child) {
+    const float t0x = (o.f[6] - r.o.x) * r.inv.x, t1x = (o.f[9] - r.o.x) * r.inv.x;
+    const float t0y = (o.f[7] - r.o.y) * r.inv.y, t1y = (o.f[10] - r.o.y) * r.inv.y;
+    const float t0z = (o.f[8] - r.o.z) * r.inv.z, t1z = (o.f[11] - r.o.z) * r.inv.z;
+    const float nx = fminf(t0x, t1x), ny = fminf(t0y, t1y), nz = fminf(t0z, t1z);
+    const float tn = fmaxf(fmaxf(nx, ny), nz);
+    const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+    const uint32_t c = tn == nx ? (r.d.x > 0.0f ? 5u : 4u) : tn == ny ? (r.d.y > 0.0f ? 3u : 2u) : (r.d.z > 0.0f ? 1u : 0u);
+    *t = tn;
+    *child = c;
+    return (tn <= tf) & (tn >= tmin) & (tn <= tmax);
+}
+
 // aabb::hit (invDir = 1/dir of the ray, aabb.h:49)
 MRT_DFN bool lin_box(const MRT_CONST_AS LinOp& o, const Ray& r, float tmin, float tmax) {
     const float b[6] = {o.f[0], o.f[1], o.f[2], o.f[3], o.f[4], o.f[5]};
@@ -344,6 +384,27 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
                 hdone = true;
             }
             PH_MARK(ph, 11);
+        } else if (MRT_FAST_ROOM && op == LOP_ROOM) {
+            float t;
+            uint32_t face;
+            const bool h = on & lin_room_hit(o, cur, tmin, closest, &t, &face);
+            // LOP_ROOMDATA (the next op): each face's node, read at a per-lane index
+            const MRT_CONST_AS uint32_t* fnode = reinterpret_cast<const MRT_CONST_AS uint32_t*>(prog[pc + 1].f);
+            closest = h ? t : closest;
+            hnode = h ? fnode[face] : hnode;
+            hinst = h ? inst : hinst;
+            hdone = h ? false : hdone;
+            pc++;
+        } else if (MRT_FAST_BOX && op == LOP_LIST && (LOP_FLAGS(o) & MRT_F_BOX6)) {  // uniform
+            // box.h's six rects as one slab test (its own box test implied), the list skipped
+            float t;
+            uint32_t c;
+            const bool h = on & lin_box6_hit(o, cur, tmin, closest, &t, &c);
+            closest = h ? t : closest;
+            hnode = h ? prog[pc + 1 + c].node : hnode;
+            hinst = h ? inst : hinst;
+            hdone = h ? false : hdone;
+            pc = o.skip;  // past its LOP_LIST_END
         } else if (op == LOP_LIST) {  // object_list::hit box reject (scene_object.h:83)
             bool in = on;
             if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, cur, tmin, closest);

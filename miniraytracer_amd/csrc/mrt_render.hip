@@ -282,6 +282,7 @@ struct mrt_scene {
     // workspace
     mrt_render_desc wdesc{};
     std::vector<uint32_t> wpixels;   // the pixel list of wdesc (mrt_render_desc.pixels), copied
+    const LinOp* prog_fast = nullptr;  // the tolerance contract's program for the interpreter (lin_rewrite_fast)
     bool have_ws = false;
     uint32_t npix = 0, chunk = 0;
     uint2* d_pixels = nullptr;
@@ -825,6 +826,7 @@ mrt_status mrt_internal_scene_tables(const mrt_scene_view* v, SceneTables* T) {
     T->bprims.swap(bprims);
     T->dmats.swap(dmats);
     T->bleaf.swap(bleaf);
+    if (lin) T->prog_fast = lin_rewrite_fast(lc.prog);
     T->prog.swap(lc.prog);
     return MRT_OK;
 }
@@ -872,6 +874,10 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     UP(v->perlin_perm, 768, &S.perm);
     UP(v->texels, (size_t)v->n_texels, &S.texels);
     UP(T.prog.data(), T.prog.size(), &S.prog);
+    {
+        const char* e = getenv("MRT_NO_REWRITE");  // A/B hook: the interpreter on the program as compiled
+        if (!T.prog_fast.empty() && !(e && *e && *e != '0')) UP(T.prog_fast.data(), T.prog_fast.size(), &s->prog_fast);
+    }
     UP(&v->camera, 1, &S.camp);
 #undef UP
     S.root = v->root;
@@ -1170,6 +1176,10 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         uint32_t s1 = std::min(ns, s0 + s->chunk);
         PathParams P{};
         P.sc = s->S;
+        // the interpreter's tolerance-contract program (rooms and box.h lists as slab tests); the
+        // shape-specialised walks read the program as compiled
+        if ((d->flags & MRT_RF_FAST) && s->prog_fast && (kVariants[s->variant] & FT_LIN) && (kVariants[s->variant] >> 16) == 0)
+            P.sc.prog = s->prog_fast;
         P.lds_frames = s->lds_frames;
         P.lds_rays = s->lds_rays;
         P.lds_mesh = s->lds_mesh;

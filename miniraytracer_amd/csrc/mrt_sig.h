@@ -8,6 +8,8 @@
 // semantics are exactly scene_hit_lin's: same tests, same order, same record.  Programs of any
 // other shape run the scene_hit_lin interpreter.
 #pragma once
+#include <algorithm>
+#include <vector>
 #include "mrt_lin.h"
 
 namespace mrtd {
@@ -106,6 +108,99 @@ inline bool cornell_room_fill(LinOp* prog, uint32_t n) {
     e.node = mask;
     e.skip = face_ops;  // op index of face k in bits 4k..4k+3
     return true;
+}
+
+// host: the tolerance contract's program (the interpreter's, for graphs without a shape-
+// specialised walk): in every object_list, the inward-facing rects that bound one box -- a room's
+// walls, at least three of them -- become ONE LOP_ROOM op (at the first wall's position; closest-
+// hit order only matters for exact ties) followed by LOP_ROOMDATA (each face's node); box.h lists
+// (MRT_F_BOX6) are tested as one slab test by the interpreter itself.  Returns the rewritten
+// program (the input when nothing applies).
+inline std::vector<LinOp> lin_rewrite_fast(const std::vector<LinOp>& prog) {
+    const uint32_t n = (uint32_t)prog.size();
+    std::vector<uint8_t> del(n, 0);
+    std::vector<LinOp> room(n);          // the ROOM op replacing wall op i (when i is a room's first wall)
+    std::vector<LinOp> roomdata(n);
+    std::vector<uint8_t> is_first(n, 0);
+    for (uint32_t L = 0; L < n; L++) {
+        if ((prog[L].code & 0xFFu) != LOP_LIST) continue;
+        // direct children of the list: nested lists / instances skipped whole
+        std::vector<uint32_t> kids;
+        for (uint32_t i = L + 1; i < prog[L].skip && i < n;) {
+            const uint32_t op = prog[i].code & 0xFFu;
+            if (op == LOP_LIST || op == LOP_INST) { i = prog[i].skip + 1; continue; }
+            if (op == LOP_VOLUME) { i += 2; continue; }
+            kids.push_back(i);
+            i++;
+        }
+        // candidate walls per face (axis, side): one-sided rects, no uv, exact divisions; the
+        // widest rect of each face (a light below the ceiling is not the ceiling)
+        int64_t pick[6] = {-1, -1, -1, -1, -1, -1};
+        for (uint32_t i : kids) {
+            const LinOp& o = prog[i];
+            const uint32_t kind = (o.code >> 8) & 0xFFu;
+            if ((o.code & 0xFFu) != LOP_PRIM || (kind != MRT_K_XY && kind != MRT_K_XZ && kind != MRT_K_YZ)) continue;
+            if (((o.code >> 16) & (MRT_F_NEEDUV | MRT_F_SLOWDIV)) != 0 || (o.f[5] != 1.0f && o.f[5] != -1.0f)) continue;
+            const uint32_t a = kind == MRT_K_YZ ? 0u : kind == MRT_K_XZ ? 1u : 2u;
+            const uint32_t k = a * 2u + (o.f[5] > 0.0f ? 0u : 1u);  // normal along +axis: the min plane
+            auto area = [&](const LinOp& x) { return (double)(x.f[1] - x.f[0]) * (double)(x.f[3] - x.f[2]); };
+            if (pick[k] < 0 || area(o) > area(prog[pick[k]])) pick[k] = i;
+        }
+        // the box: along every axis its extent from the in-plane bounds of the walls spanning it,
+        // which must agree, and the planes of the walls there must be its faces
+        float lo[3], hi[3];
+        bool set[3] = {false, false, false}, ok = true;
+        uint32_t mask = 0, walls = 0;
+        for (uint32_t k = 0; k < 6 && ok; k++) {
+            if (pick[k] < 0) continue;
+            const LinOp& o = prog[pick[k]];
+            const uint32_t a = k / 2u, b = a == 0 ? 1u : 0u, c = a == 2 ? 1u : 2u;
+            const float in[2][2] = {{o.f[0], o.f[1]}, {o.f[2], o.f[3]}};
+            const uint32_t ax[2] = {b, c};
+            for (int j = 0; j < 2 && ok; j++) {
+                if (!set[ax[j]]) { lo[ax[j]] = in[j][0]; hi[ax[j]] = in[j][1]; set[ax[j]] = true; }
+                else ok = lo[ax[j]] == in[j][0] && hi[ax[j]] == in[j][1];
+            }
+            mask |= 1u << k;
+            walls++;
+        }
+        for (uint32_t a = 0; a < 3 && ok; a++) ok = set[a] && lo[a] < hi[a];
+        for (uint32_t k = 0; k < 6 && ok; k++)
+            if (pick[k] >= 0) ok = prog[pick[k]].f[4] == ((k & 1u) ? hi[k / 2u] : lo[k / 2u]);
+        if (!ok || walls < 3) continue;
+        uint32_t first = n;
+        for (uint32_t k = 0; k < 6; k++)
+            if (pick[k] >= 0) first = std::min(first, (uint32_t)pick[k]);
+        LinOp r{}, d{};
+        r.code = LOP_ROOM | (prog[first].code & 0xFF000000u);
+        r.node = mask;
+        r.skip = 0;
+        r.mat = MRT_NONE;
+        for (uint32_t a = 0; a < 3; a++) { r.f[a] = lo[a]; r.f[3 + a] = hi[a]; }
+        d.code = LOP_ROOMDATA | (prog[first].code & 0xFF000000u);
+        for (uint32_t k = 0; k < 6; k++) {
+            const uint32_t node = pick[k] >= 0 ? prog[pick[k]].node : MRT_NONE;
+            __builtin_memcpy(&d.f[k], &node, 4);
+            if (pick[k] >= 0) del[pick[k]] = 1;
+        }
+        room[first] = r;
+        roomdata[first] = d;
+        is_first[first] = 1;
+    }
+    // compact: each room's first wall becomes ROOM + ROOMDATA, the other walls go; skips re-linked
+    std::vector<uint32_t> at(n + 1, 0);
+    std::vector<LinOp> out;
+    for (uint32_t i = 0; i < n; i++) {
+        at[i] = (uint32_t)out.size();
+        if (is_first[i]) { out.push_back(room[i]); out.push_back(roomdata[i]); }
+        else if (!del[i]) out.push_back(prog[i]);
+    }
+    at[n] = (uint32_t)out.size();
+    for (LinOp& o : out) {
+        const uint32_t op = o.code & 0xFFu;
+        if ((op == LOP_LIST || op == LOP_INST || op == LOP_INST_END) && o.skip <= n) o.skip = at[o.skip];
+    }
+    return out;
 }
 
 // host: the shape id of a compiled program (SIG_NONE if it matches no entry)

@@ -15,6 +15,7 @@ struct SceneTables {
     std::vector<mrt_node> bleaf;        // leaves of scene.biased_objects
     uint32_t blist = 0, nbleaf = 1;
     std::vector<mrtd::LinOp> prog;      // linear hit program (empty + LOP_END when the graph has none)
+    std::vector<mrtd::LinOp> prog_fast; // its tolerance-contract rewrite (lin_rewrite_fast: rooms, box.h lists)
     uint32_t prog_ops = 0;
     uint32_t features = 0;              // FT_* | FT_LIN | shape id (mrt_sig.h)
     int max_frames = 0, max_rays = 0, max_mesh = 0;  // deepest stacks of the scene graph

@@ -531,6 +531,29 @@ def test_cli_drop_in_writes_reference_image(gpu, tmp_path):
     assert bad.returncode != 0
 
 
+@pytest.mark.parametrize("sid", [5, 8, 9])
+def test_interpreter_program_rewrite_within_tolerance(gpu, sid, monkeypatch):
+    """The tolerance contract's interpreter (the walk of any scene graph without a shape-specialised
+    walk; MRT_NO_SIG=1 forces it on the Cornell shapes) runs a rewritten program: the room's walls
+    as one slab test (LOP_ROOM), box.h lists as one slab test.  Against the reference as shipped on
+    the small fixtures (128x128, 1024 spp): per-pixel RMSE < 1e-3, rays within 0.5%; and it must
+    differ from the program as compiled (MRT_NO_REWRITE=1) only by that tolerance."""
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", f"shipped_stream_{sid}_small.npz"))
+    _, w, h, spp, depth = (int(x) for x in g["meta"])
+    monkeypatch.setenv("MRT_NO_SIG", "1")
+    sc = gpu.select_scene(sid, w / h)
+    r = gpu.Renderer(sc, 0)
+    assert (r.kernel_info()["kernel_features"] >> 16) & 0xFF == 0
+    img, rays = r.render(gpu.render_desc(w, h, spp, depth=depth, numerics="fast"))
+    d = img[..., :3].astype(np.float64) - g["image"]
+    assert float(np.sqrt((d ** 2).mean())) < 1e-3
+    assert abs(rays / float(g["rays"][0]) - 1) < 5e-3
+    monkeypatch.setenv("MRT_NO_REWRITE", "1")
+    img2, rays2 = gpu.Renderer(sc, 0).render(gpu.render_desc(w, h, spp, depth=depth, numerics="fast"))
+    assert not np.array_equal(img, img2)  # the rewrite is in effect
+    assert float(np.sqrt(((img2[..., :3].astype(np.float64) - g["image"]) ** 2).mean())) < 1e-3
+
+
 @pytest.mark.parametrize("sid,w,h,spp,mode", [(5, 64, 64, 64, 0), (7, 48, 48, 16, 1), (8, 48, 48, 16, 0), (0, 200, 100, 16, 1)])
 def test_gpu_equals_cpu_backend(gpu, sid, w, h, spp, mode):
     """The two backends of the same hot-path source (the gfx950 path kernel and its host build,
