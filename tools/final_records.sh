@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 final-tree measurement, one GPU call: GPU suite + smoke; rocprofv3 kernel trace + PMC
+# Final-tree measurement (TAG names the record set, e.g. r04_v1), one GPU call: GPU suite + smoke; rocprofv3 kernel trace + PMC
 # passes of C2 and of C3-C5 at full resolution (tools/profile.sh, tools/prof_configs.sh), summarised
 # on the box (tools/pmc_summary.py) so the bench below prices its roofline by this tree's counters;
 # contract A/B; parity at every config's resolution; the full-size BASELINE configs; the 8-rank
@@ -10,7 +10,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/profiles
 export TMPDIR=/tmp
-TAG=${TAG:-r03_v4}
+TAG=${TAG:-r04_v1}
 step() {
     local name=$1 t=$2; shift 2
     echo "== $name $(date +%T)"
@@ -32,7 +32,7 @@ cp profiles/${TAG}* profiles/pmc_s*.json gpurun_out/profiles/
 step contract_ab 600 python tools/contract_ab.py --measure
 fi
 [ "${PART:-ab}" = a ] && exit 0
-step parity 600 python tools/parity_record.py
+step parity 600 python tools/parity_record.py --out gpurun_out/profiles/${TAG}_parity.json
 step configs 900 bash tools/configs.sh
 CFGS="1,0 2,0 2,1 4,0 4,1 4,2 4,3 8,0 8,1 8,2 8,3 8,4 8,5 8,6 8,7" STEPS=60 step scale 900 bash tools/scale_rehearsal.sh
 step bench 600 python bench.py --steps 20 --warmup 5

@@ -4,8 +4,8 @@ per-path streams, under both numerics contracts -> one JSON record (profiles/r03
 
 Fixtures (tests/golden, tools/make_golden.py): C2 shipped_stream_5.npz (whole 500x500 image,
 1024 spp); C3 / C4 / C5 shipped_full_<id>.npz (full resolution, 1024 spp: block means, channel means,
-a band of rows, a seeded pixel sample).  The same comparison as tests/fixture_cmp.py, which the
-GPU tests assert on.
+a band of rows, a seeded pixel sample) and shipped_ownspp_<id>.npz (the configs' own spp, a pixel
+list).  The same comparisons as tests/fixture_cmp.py, which the GPU tests assert on.
 
 Usage (GPU box): python tools/parity_record.py [--out gpurun_out/parity.json] [--scenes 5,9,8,7]
 """
@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--numerics", default="exact,fast")
     a = ap.parse_args()
     import miniraytracer_amd as m
-    from fixture_cmp import GOLDEN, compare
+    from fixture_cmp import GOLDEN, compare, compare_pixels
     rec = {"what": "GPU render vs the reference as shipped, same per-path streams", "configs": []}
     for sid in (int(x) for x in a.scenes.split(",")):
         path = os.path.join(GOLDEN, f"shipped_stream_{sid}.npz" if sid == 5 else f"shipped_full_{sid}.npz")
@@ -45,6 +45,16 @@ def main():
                      kernel_features=r.kernel_info()["kernel_features"])
             rec["configs"].append(c)
             print(json.dumps(c), flush=True)
+        own = os.path.join(GOLDEN, f"shipped_ownspp_{sid}.npz")
+        if os.path.exists(own):
+            g = np.load(own)
+            _, w, h, spp, depth = (int(x) for x in g["meta"])
+            for numerics in a.numerics.split(","):
+                img, rays = r.render(m.render_desc(w, h, spp, depth=depth, numerics=numerics, pixels=g["pixels"]))
+                c = compare_pixels(img, rays, g)
+                c.update(scene=sid, width=w, height=h, numerics=numerics, rays=int(rays), own_spp=True)
+                rec["configs"].append(c)
+                print(json.dumps(c), flush=True)
         r.close()
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     json.dump(rec, open(a.out, "w"), indent=1)
