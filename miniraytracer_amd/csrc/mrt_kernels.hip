@@ -96,9 +96,11 @@ extern "C" int mrt_debug_phases(unsigned long long* out, int reset) {
 // per wave of the last launch: start, pool exhausted, end (s_memrealtime, 100 MHz), workgroup
 // + time inside successful / failed claim atomics (10-ns ticks) and their counts (ok | fail << 32)
 __device__ unsigned long long g_wtimes[7 * 16384];
+#if MRT_TABLE_FTZ || !MRT_TABLE_FAST  // the reader in one TU only (the FTZ build runs the Cornell kernels)
 extern "C" int mrt_debug_wtimes(unsigned long long* out, int n) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wtimes), sizeof(unsigned long long) * 7 * (size_t)n) != hipSuccess;
 }
+#endif
 #define WT_MARK(v) (v) = __builtin_amdgcn_s_memrealtime()
 #else
 #define WT_MARK(v) (void)0
