@@ -620,7 +620,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                 const MRT_CONST_AS mrt_mesh_node& rt = const_ptr(S.mnodes)[mn.a];
                 const bool enter = in && aabb_hit(f3{rt.bmin[0], rt.bmin[1], rt.bmin[2]}, f3{rt.bmax[0], rt.bmax[1], rt.bmax[2]}, ps.r,
                                                   0.001f, w.closest);
-                ref = mn.b;
+                ref = kMesh4<F> ? __float_as_uint(mn.f[11]) : mn.b;  // (Mesh4 root ref, mrt_render.hip)
                 msp = 0;
                 phase = enter ? PH_WALK : PH_DONE;
             }
@@ -630,7 +630,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
             while (__any(phase == PH_WALK)) {
                 if (phase == PH_WALK) {
                     const mrt_node mn = ld_node(const_ptr(S.nodes) + prog[kMeshPC].node);
-                    const uint32_t st = mesh_step<false, true>(S, mn, ps.r, 0.001f, w.closest, rec, Ls, ref, msp, w.hdone);
+                    const uint32_t st = mesh_step<false, true, (bool)kMesh4<F>>(S, mn, ps.r, 0.001f, w.closest, rec, Ls, ref, msp, w.hdone);
                     if (st == 1u) w.hnode = kMeshPC;  // w.closest = the hit's t, w.hdone set
                     phase = st != 0u ? PH_DONE : PH_WALK;
                 }
@@ -729,7 +729,9 @@ const KernelTable& mrtd::kernel_table_exact() {
         {PathQ<kVariants[0]>::words, PathQ<kVariants[1]>::words, PathQ<kVariants[2]>::words, PathQ<kVariants[3]>::words,
          PathQ<kVariants[4]>::words, PathQ<kVariants[5]>::words, PathQ<kVariants[6]>::words},
         {kBox6Walk<kVariants[0]>, kBox6Walk<kVariants[1]>, kBox6Walk<kVariants[2]>, kBox6Walk<kVariants[3]>,
-         kBox6Walk<kVariants[4]>, kBox6Walk<kVariants[5]>, kBox6Walk<kVariants[6]>}};
+         kBox6Walk<kVariants[4]>, kBox6Walk<kVariants[5]>, kBox6Walk<kVariants[6]>},
+        {kMesh4<kVariants[0]>, kMesh4<kVariants[1]>, kMesh4<kVariants[2]>, kMesh4<kVariants[3]>, kMesh4<kVariants[4]>,
+         kMesh4<kVariants[5]>, kMesh4<kVariants[6]>}};
     static_assert(kNumVariants == 7, "one table entry per variant");
     return t;
 }

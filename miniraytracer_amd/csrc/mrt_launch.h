@@ -83,6 +83,7 @@ struct KernelTable {
     uint32_t tree[kNumVariants];  // 1: the kernel reads the top BvhWide nodes from an LDS treelet
     uint32_t pq[kNumVariants];    // LDS words per lane slot of the kernel's queue of path starts
     uint32_t box6_walk[kNumVariants];  // 1: Cornell shape walked by cornell_fast_hit when op 8 is MRT_F_BOX6
+    uint32_t mesh4[kNumVariants];      // 1: the resumable mesh walk two levels at a time (Mesh4, MRT_MESH4)
 };
 const KernelTable& kernel_table_exact();
 const KernelTable& kernel_table_fast();

@@ -240,6 +240,7 @@ struct PathLaunch {
     uint32_t wg = 64;     // threads per workgroup
     uint32_t tree_n = 0;  // BvhWide nodes kept in each workgroup's LDS (treelet kernels)
     uint32_t lds_save = 0;  // LDS words per lane slot for the query ray parked during instances
+    uint32_t lds_mesh = 0;  // LDS words per lane of the mesh walk's stack (binary or two-level walk)
 };
 
 // Wide nodes renumbered breadth-first over all roots together (level 0 of every tree, then level
@@ -651,6 +652,102 @@ mrt_status mrt_internal_scene_tables(const mrt_scene_view* v, SceneTables* T) {
             if ((n.kind & 0xFF) == MRT_K_MESH) mroots.push_back(&n.b);
         bfs_order(wide, mroots, MESH_LEAF, 63u);
     }
+    // pod_bvh two levels per node (Mesh4, mrt_trace.h), breadth-first from each mesh's root; the
+    // root ref in the MESH node's f[11]
+    {
+        const mrt_mesh_node* mn = v->mesh_nodes;
+        auto inner = [&](uint32_t i) { return (mn[i].count_order & 0xFFFFFFu) == 0; };
+        auto leaf_ref = [&](uint32_t i) { return MESH_LEAF | ((mn[i].count_order & 0xFFFFFFu) << 24) | mn[i].left_or_first; };
+        auto inside = [&](uint32_t c, uint32_t p) {
+            for (int k = 0; k < 3; k++)
+                if (!(mn[c].bmin[k] >= mn[p].bmin[k] && mn[c].bmax[k] <= mn[p].bmax[k])) return false;
+            return true;
+        };
+        std::vector<uint32_t> idx4(v->n_mesh_nodes, MRT_NONE);
+        std::vector<uint32_t> queue;
+        auto alloc = [&](uint32_t i) {
+            if (idx4[i] == MRT_NONE) {
+                idx4[i] = (uint32_t)T->mesh4.size();
+                T->mesh4.push_back(Mesh4{});
+                T->mesh4p.push_back(Mesh4Pair{});
+                queue.push_back(i);
+            }
+            return idx4[i];
+        };
+        for (mrt_node& n : nodes) {
+            if ((n.kind & 0xFF) != MRT_K_MESH) continue;
+            // (the wide build above has checked the mesh's node indices and leaf encodings)
+            const uint32_t root = inner(n.a) ? alloc(n.a) : leaf_ref(n.a);
+            uint32_t bits = root;
+            std::memcpy(&n.f[11], &bits, 4);
+            for (size_t qi = 0; qi < queue.size(); qi++) {
+                const uint32_t i = queue[qi];
+                Mesh4 q{};
+                Mesh4Pair pr{};
+                uint32_t sl[4] = {MRT_NONE, MRT_NONE, MRT_NONE, MRT_NONE};  // binary node of each slot
+                uint32_t meta = mn[i].count_order >> 24;
+                for (uint32_t p = 0; p < 2; p++) {
+                    const uint32_t c = mn[i].left_or_first + p;
+                    float* pmin = p ? pr.bmin : pr.amin;
+                    float* pmax = p ? pr.bmax : pr.amax;
+                    for (int k = 0; k < 3; k++) { pmin[k] = mn[c].bmin[k]; pmax[k] = mn[c].bmax[k]; }
+                    if (!inside(c, i)) T->mesh4_all = 1;
+                    if (inner(c)) {
+                        meta |= (mn[c].count_order >> 24) << (8 + 8 * p);
+                        sl[2 * p] = mn[c].left_or_first;
+                        sl[2 * p + 1] = mn[c].left_or_first + 1;
+                    } else {
+                        meta |= 0xFFu << (8 + 8 * p);  // (one slot: its order is moot)
+                        sl[2 * p] = c;
+                    }
+                }
+                for (uint32_t k = 0; k < 4; k++) {
+                    const uint32_t b = sl[k];
+                    if (b == MRT_NONE) continue;
+                    meta |= 1u << (24 + k);
+                    Mesh4::Slot& S4 = q.s[k];
+                    for (int j = 0; j < 3; j++) { S4.lo[j] = mn[b].bmin[j]; S4.hi[j] = mn[b].bmax[j]; }
+                    S4.ref = inner(b) ? alloc(b) : leaf_ref(b);
+                    const uint32_t par = mn[i].left_or_first + (k >> 1);
+                    if (b != par && !inside(b, par)) T->mesh4_all = 1;
+                }
+                q.s[0].meta = meta;
+                T->mesh4[idx4[i]] = q;
+                T->mesh4p[idx4[i]] = pr;
+            }
+            queue.clear();
+        }
+        // deepest stack of the two-level walk: per ray octant, every box hit; children are
+        // numbered after their parents, so one pass from the back
+        const size_t n4 = T->mesh4.size();
+        std::vector<int> need(n4 * 8, 0);
+        for (size_t j = n4; j-- > 0;) {
+            const uint32_t meta = T->mesh4[j].s[0].meta;
+            for (uint32_t o = 0; o < 8; o++) {
+                const uint32_t mask = 1u << o;
+                const bool nl = (meta & mask) != 0, al = ((meta >> 8) & mask) != 0, bl = ((meta >> 16) & mask) != 0;
+                const uint32_t pa[2] = {al ? 0u : 1u, al ? 1u : 0u}, pb[2] = {bl ? 2u : 3u, bl ? 3u : 2u};
+                const uint32_t seq[4] = {nl ? pa[0] : pb[0], nl ? pa[1] : pb[1], nl ? pb[0] : pa[0], nl ? pb[1] : pa[1]};
+                uint32_t vis[4], nv = 0;
+                for (uint32_t k = 0; k < 4; k++)
+                    if (meta & (1u << (24 + seq[k]))) vis[nv++] = seq[k];
+                int best = 0;
+                for (uint32_t p = 0; p < nv; p++) {
+                    const Mesh4::Slot& S4 = T->mesh4[j].s[vis[p]];
+                    const int below = (S4.ref & MESH_LEAF) ? 0 : need[(size_t)S4.ref * 8 + o];
+                    best = std::max(best, (int)(nv - 1 - p) + below);
+                }
+                need[j * 8 + o] = best;
+            }
+        }
+        for (const mrt_node& n : nodes) {
+            if ((n.kind & 0xFF) != MRT_K_MESH) continue;
+            uint32_t r;
+            std::memcpy(&r, &n.f[11], 4);
+            if (!(r & MESH_LEAF))
+                for (uint32_t o = 0; o < 8; o++) T->max_mesh4 = std::max(T->max_mesh4, need[(size_t)r * 8 + o]);
+        }
+    }
     // bvh_node subtrees whose leaves are primitives / object_lists of primitives (and of boxes of
     // primitives) -> wide nodes; the subtree root becomes an MRT_K_BVHW node (a = root ref)
     std::vector<BvhWide> bwide;
@@ -859,6 +956,9 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     UP(v->mesh_nodes, v->n_mesh_nodes, &S.mnodes);
     UP(T.wide.data(), T.wide.size(), &S.mwide);
     S.mwide_n = (uint32_t)T.wide.size();
+    UP(T.mesh4.data(), T.mesh4.size(), &S.mesh4);
+    UP(T.mesh4p.data(), T.mesh4p.size(), &S.mesh4p);
+    S.mesh4_all = T.mesh4_all;
     UP(T.bwide.data(), T.bwide.size(), &S.bwide);
     UP(T.bprims.data(), T.bprims.size(), &S.bprims);
     UP((const float4*)v->tri_geo, (size_t)v->n_tris * 3, &S.tri_geo);
@@ -921,8 +1021,9 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
         const uint32_t waves_per_wg = L.wg / 64u;
         // the Cornell walk of the tolerance contract (mrt_sig.h cornell_fast_hit) parks no ray
         L.lds_save = tabs[k]->box6_walk[s->variant] ? 0u : s->lds_save;
+        L.lds_mesh = tabs[k]->mesh4[s->variant] ? std::max(s->lds_mesh, (uint32_t)T.max_mesh4) : s->lds_mesh;
         L.lds_bytes = (size_t)waves_per_wg * 64 * 4 *
-                      (s->lds_frames * 2 + s->lds_rays * 11 + s->lds_mesh + L.lds_save + tabs[k]->lev_k[s->variant] * 4 +
+                      (s->lds_frames * 2 + s->lds_rays * 11 + L.lds_mesh + L.lds_save + tabs[k]->lev_k[s->variant] * 4 +
                        tabs[k]->pq[s->variant]);
         if (L.lds_bytes > (size_t)prop.sharedMemPerBlock) {
             mrt_scene_free(s);
@@ -1182,7 +1283,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
             P.sc.prog = s->prog_fast;
         P.lds_frames = s->lds_frames;
         P.lds_rays = s->lds_rays;
-        P.lds_mesh = s->lds_mesh;
+        P.lds_mesh = PL.lds_mesh;
         P.lds_save = PL.lds_save;
         P.walk_min = s->walk_min;
         P.tree_src = reinterpret_cast<const float4*>(s->S.bwide);
