@@ -14,6 +14,7 @@
 // work_queue.cpp:158-166) and run trace() for each lane's path to completion; per-path radiance
 // is written sample-major [s][local pixel] (coalesced).
 #include <hip/hip_runtime.h>
+#include <utility>
 
 #include "mrt_launch.h"
 
@@ -705,33 +706,28 @@ static constexpr path_kernel_t kfn() {
     return MRT_PATH_KERNEL<F>;
 }
 
+// one entry per variant of mrt_launch.h's kVariants
+template <size_t... I>
+static KernelTable make_table(const char* numerics, std::index_sequence<I...>) {
+    return KernelTable{numerics,
+                       {kfn<kVariants[I]>()...},
+                       {PathLevLds<kVariants[I]>::K...},
+                       {TreeOf<kVariants[I]>::wg...},
+                       {TreeOf<kVariants[I]>::on...},
+                       {PathQ<kVariants[I]>::words...},
+                       {kBox6Walk<kVariants[I]>...},
+                       {kMesh4<kVariants[I]>...},
+                       {(uint32_t)(kLinSlabOps<kVariants[I]> && MRT_SIG_OF(kVariants[I]) == SIG_NONE)...}};
+}
 #if MRT_TABLE_FTZ
 const KernelTable& mrtd::kernel_table_fast_ftz() {
-    static const KernelTable t = {
-        "fast",
+    static const KernelTable t = make_table("fast", std::make_index_sequence<kNumVariants>{});
 #elif MRT_TABLE_FAST
 const KernelTable& mrtd::kernel_table_fast() {
-    static const KernelTable t = {
-        "fast",
+    static const KernelTable t = make_table("fast", std::make_index_sequence<kNumVariants>{});
 #else
 const KernelTable& mrtd::kernel_table_exact() {
-    static const KernelTable t = {
-        "exact",
+    static const KernelTable t = make_table("exact", std::make_index_sequence<kNumVariants>{});
 #endif
-        {kfn<kVariants[0]>(), kfn<kVariants[1]>(), kfn<kVariants[2]>(), kfn<kVariants[3]>(), kfn<kVariants[4]>(),
-         kfn<kVariants[5]>(), kfn<kVariants[6]>()},
-        {PathLevLds<kVariants[0]>::K, PathLevLds<kVariants[1]>::K, PathLevLds<kVariants[2]>::K, PathLevLds<kVariants[3]>::K,
-         PathLevLds<kVariants[4]>::K, PathLevLds<kVariants[5]>::K, PathLevLds<kVariants[6]>::K},
-        {TreeOf<kVariants[0]>::wg, TreeOf<kVariants[1]>::wg, TreeOf<kVariants[2]>::wg, TreeOf<kVariants[3]>::wg,
-         TreeOf<kVariants[4]>::wg, TreeOf<kVariants[5]>::wg, TreeOf<kVariants[6]>::wg},
-        {TreeOf<kVariants[0]>::on, TreeOf<kVariants[1]>::on, TreeOf<kVariants[2]>::on, TreeOf<kVariants[3]>::on,
-         TreeOf<kVariants[4]>::on, TreeOf<kVariants[5]>::on, TreeOf<kVariants[6]>::on},
-        {PathQ<kVariants[0]>::words, PathQ<kVariants[1]>::words, PathQ<kVariants[2]>::words, PathQ<kVariants[3]>::words,
-         PathQ<kVariants[4]>::words, PathQ<kVariants[5]>::words, PathQ<kVariants[6]>::words},
-        {kBox6Walk<kVariants[0]>, kBox6Walk<kVariants[1]>, kBox6Walk<kVariants[2]>, kBox6Walk<kVariants[3]>,
-         kBox6Walk<kVariants[4]>, kBox6Walk<kVariants[5]>, kBox6Walk<kVariants[6]>},
-        {kMesh4<kVariants[0]>, kMesh4<kVariants[1]>, kMesh4<kVariants[2]>, kMesh4<kVariants[3]>, kMesh4<kVariants[4]>,
-         kMesh4<kVariants[5]>, kMesh4<kVariants[6]>}};
-    static_assert(kNumVariants == 7, "one table entry per variant");
     return t;
 }

@@ -84,6 +84,7 @@ struct KernelTable {
     uint32_t pq[kNumVariants];    // LDS words per lane slot of the kernel's queue of path starts
     uint32_t box6_walk[kNumVariants];  // 1: Cornell shape walked by cornell_fast_hit when op 8 is MRT_F_BOX6
     uint32_t mesh4[kNumVariants];      // 1: the resumable mesh walk two levels at a time (Mesh4, MRT_MESH4)
+    uint32_t rewrite[kNumVariants];    // 1: the interpreter runs the rewritten program (mrt_sig.h lin_rewrite_fast)
 };
 const KernelTable& kernel_table_exact();
 const KernelTable& kernel_table_fast();

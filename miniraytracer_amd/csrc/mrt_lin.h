@@ -296,6 +296,14 @@ MRT_DFN void lin_untransform(const OP& io, HitRec& rec) {
 // r: the query ray; on return it holds the same values (reloaded from LDS when instances exist).
 // LDS per lane (L.save): [0..8] the query ray, [9..14] origin/direction of the instance ray of
 // the closest hit (written at the instance's END op when that hit lies inside it).
+// The interpreter's slab-test ops (LOP_ROOM of the tolerance contract's program rewrite, an
+// object_list flagged MRT_F_BOX6) are compiled into the kernels of scenes without bvh_node
+// subtrees, volumes, textures or motion only: in the catch-all interpreter kernel their two cases
+// tripled book2's register spills (C5 2.7x slower, profiles/r04_ab.txt).  The other kernels run
+// the program as compiled (the host uploads the rewrite only where KernelTable::rewrite says so).
+template <uint32_t F>
+static constexpr bool kLinSlabOps = MRT_FAST && (F & FT_LIN) != 0 && (F & (FT_BVHW | FT_VOLUME | FT_TEX | FT_MOVING)) == 0;
+
 template <uint32_t F>
 MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, const LStack& L, Pcg& rng, PhaseClock& ph) {
     constexpr bool INST = (F & FT_INST) != 0;
@@ -384,7 +392,7 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
                 hdone = true;
             }
             PH_MARK(ph, 11);
-        } else if (MRT_FAST_ROOM && op == LOP_ROOM) {
+        } else if (MRT_FAST_ROOM && kLinSlabOps<F> && op == LOP_ROOM) {
             float t;
             uint32_t face;
             const bool h = on & lin_room_hit(o, cur, tmin, closest, &t, &face);
@@ -395,7 +403,7 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
             hinst = h ? inst : hinst;
             hdone = h ? false : hdone;
             pc++;
-        } else if (MRT_FAST_BOX && op == LOP_LIST && (LOP_FLAGS(o) & MRT_F_BOX6)) {  // uniform
+        } else if (MRT_FAST_BOX && kLinSlabOps<F> && op == LOP_LIST && (LOP_FLAGS(o) & MRT_F_BOX6)) {  // uniform
             // box.h's six rects as one slab test (its own box test implied), the list skipped
             float t;
             uint32_t c;

@@ -241,6 +241,7 @@ struct PathLaunch {
     uint32_t tree_n = 0;  // BvhWide nodes kept in each workgroup's LDS (treelet kernels)
     uint32_t lds_save = 0;  // LDS words per lane slot for the query ray parked during instances
     uint32_t lds_mesh = 0;  // LDS words per lane of the mesh walk's stack (binary or two-level walk)
+    bool rewrite = false;   // the kernel runs the tolerance-contract program rewrite (s->prog_fast)
 };
 
 // Wide nodes renumbered breadth-first over all roots together (level 0 of every tree, then level
@@ -1022,6 +1023,7 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
         // the Cornell walk of the tolerance contract (mrt_sig.h cornell_fast_hit) parks no ray
         L.lds_save = tabs[k]->box6_walk[s->variant] ? 0u : s->lds_save;
         L.lds_mesh = tabs[k]->mesh4[s->variant] ? std::max(s->lds_mesh, (uint32_t)T.max_mesh4) : s->lds_mesh;
+        L.rewrite = tabs[k]->rewrite[s->variant] != 0;
         L.lds_bytes = (size_t)waves_per_wg * 64 * 4 *
                       (s->lds_frames * 2 + s->lds_rays * 11 + L.lds_mesh + L.lds_save + tabs[k]->lev_k[s->variant] * 4 +
                        tabs[k]->pq[s->variant]);
@@ -1279,8 +1281,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.sc = s->S;
         // the interpreter's tolerance-contract program (rooms and box.h lists as slab tests); the
         // shape-specialised walks read the program as compiled
-        if ((d->flags & MRT_RF_FAST) && s->prog_fast && (kVariants[s->variant] & FT_LIN) && (kVariants[s->variant] >> 16) == 0)
-            P.sc.prog = s->prog_fast;
+        if ((d->flags & MRT_RF_FAST) && s->prog_fast && PL.rewrite) P.sc.prog = s->prog_fast;
         P.lds_frames = s->lds_frames;
         P.lds_rays = s->lds_rays;
         P.lds_mesh = PL.lds_mesh;
