@@ -60,7 +60,10 @@ using namespace mrtd;
 #define MRT_WPE_MESH 7
 #endif
 #ifndef MRT_WPE_LIN_GEN
-#define MRT_WPE_LIN_GEN 6  // the interpreter's compact variants (no program shape): 6 waves (80 VGPRs) +9% over 7 on C2
+// the interpreter's compact variants (no program shape): 5 waves (96 VGPRs, spill-free with the
+// one-step box instances; round 4: 43.3 Grays/s on C2 through the interpreter against 40.3 at 6
+// waves without the step and 33.7 with it and 10 spilled VGPRs, profiles/r04_ab.txt)
+#define MRT_WPE_LIN_GEN 5
 #endif
 template <uint32_t F> struct PathOcc {
     static constexpr bool kWide = (F & (FT_BVHW | FT_TEX | FT_VOLUME)) != 0 || !(F & FT_LIN);

@@ -301,6 +301,9 @@ MRT_DFN void lin_untransform(const OP& io, HitRec& rec) {
 // subtrees, volumes, textures or motion only: in the catch-all interpreter kernel their two cases
 // tripled book2's register spills (C5 2.7x slower, profiles/r04_ab.txt).  The other kernels run
 // the program as compiled (the host uploads the rewrite only where KernelTable::rewrite says so).
+#ifndef MRT_BOXINST
+#define MRT_BOXINST 1  // the one-step box instance (MRT_F_BOXINST)
+#endif
 template <uint32_t F>
 static constexpr bool kLinSlabOps = MRT_FAST && (F & FT_LIN) != 0 && (F & (FT_BVHW | FT_VOLUME | FT_TEX | FT_MOVING)) == 0;
 
@@ -419,6 +422,38 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
             lvl++;
             act = (act & ~(1u << lvl)) | ((uint32_t)in << lvl);
             if (!any_lane(in)) pc = o.skip - 1;
+        } else if (MRT_BOXINST && kLinSlabOps<F> && INST && op == LOP_INST && (LOP_FLAGS(o) & MRT_F_BOXINST)) {  // uniform
+            // an instance of one box.h list, outside instances (cur is the query ray): the instance
+            // ray from it in registers, the instance's box test and the list's slab test, the body
+            // skipped -- the operations of the INST / LIST / LIST_END / INST_END steps below, without
+            // parking and reloading the query ray
+            const uint32_t kind = LOP_KIND(o);
+            Ray ci = cur;
+            bool in = on;
+            if (kind == MRT_K_TRROTY) {
+                ci = moved_ray<kFastUnit<F>>(cur, sub(cur.o, f3{o.f[8], o.f[9], o.f[10]}));
+                if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, ci, tmin, closest);
+                ci = rotate_ray<kFastUnit<F>>(ci, o.f[6], o.f[7]);
+            } else if (kind == MRT_K_ROTY) {
+                if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, ci, tmin, closest);
+                ci = rotate_ray<kFastUnit<F>>(ci, o.f[6], o.f[7]);
+            } else {
+                ci = moved_ray<kFastUnit<F>>(cur, sub(cur.o, f3{o.f[0], o.f[1], o.f[2]}));
+            }
+            const MRT_CONST_AS LinOp& lo = prog[pc + 1];
+            float t;
+            uint32_t c;
+            const bool h = in & lin_box6_hit(lo, ci, tmin, closest, &t, &c);
+            closest = h ? t : closest;
+            hnode = h ? prog[pc + 2 + c].node : hnode;
+            hinst = h ? pc : hinst;
+            hdone = h ? false : hdone;
+            if (h) {  // the instance-frame ray of the hit, for the record (as at LOP_INST_END)
+                float* b = L.save + L.lane + 9 * 64;
+                b[0] = ci.o.x; b[64] = ci.o.y; b[128] = ci.o.z;
+                b[192] = ci.d.x; b[256] = ci.d.y; b[320] = ci.d.z;
+            }
+            pc = o.skip;  // its LOP_INST_END
         } else if (INST && op == LOP_INST) {
             const uint32_t kind = LOP_KIND(o);
             bool in = on;

@@ -9,6 +9,7 @@
 // other shape run the scene_hit_lin interpreter.
 #pragma once
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 #include "mrt_lin.h"
 
@@ -187,13 +188,33 @@ inline std::vector<LinOp> lin_rewrite_fast(const std::vector<LinOp>& prog) {
         roomdata[first] = d;
         is_first[first] = 1;
     }
+    // an instance outside instances whose body is exactly one box.h list (INST, LIST flagged
+    // MRT_F_BOX6, its six rects, LIST_END, INST_END): MRT_F_BOXINST, the interpreter's one-step box
+    const char* nb = getenv("MRT_NO_BOXINST");  // A/B hook
+    std::vector<uint8_t> boxinst(n, 0);
+    for (uint32_t i = 0, depth = 0; i < n && !(nb && *nb && *nb != '0'); i++) {
+        const uint32_t op = prog[i].code & 0xFFu;
+        if (op == LOP_INST) {
+            const uint32_t e = prog[i].skip;
+            const bool ok = depth == 0 && e == i + 9 && e < n && (prog[i + 1].code & 0xFFu) == LOP_LIST &&
+                            ((prog[i + 1].code >> 16) & MRT_F_BOX6) && prog[i + 1].skip == i + 8 &&
+                            (prog[i + 8].code & 0xFFu) == LOP_LIST_END && (prog[e].code & 0xFFu) == LOP_INST_END;
+            boxinst[i] = ok;
+            depth++;
+        } else if (op == LOP_INST_END && depth > 0) {
+            depth--;
+        }
+    }
     // compact: each room's first wall becomes ROOM + ROOMDATA, the other walls go; skips re-linked
     std::vector<uint32_t> at(n + 1, 0);
     std::vector<LinOp> out;
     for (uint32_t i = 0; i < n; i++) {
         at[i] = (uint32_t)out.size();
         if (is_first[i]) { out.push_back(room[i]); out.push_back(roomdata[i]); }
-        else if (!del[i]) out.push_back(prog[i]);
+        else if (!del[i]) {
+            out.push_back(prog[i]);
+            if (boxinst[i]) out.back().code |= MRT_F_BOXINST << 16;
+        }
     }
     at[n] = (uint32_t)out.size();
     for (LinOp& o : out) {

@@ -189,6 +189,7 @@ struct DScene {
 #define MRT_NODE_FLAGS(n) (((n).kind >> 16) & 0xFFu)
 #define MRT_F_NEEDUV 0x4u   /* set on upload when the node's material samples uv */
 #define MRT_F_BOX6 0x10u    /* set on upload on an object_list that is box.h's six rects (planes in f[6..11]) */
+#define MRT_F_BOXINST 0x20u /* tolerance-contract program: an instance outside instances whose body is one MRT_F_BOX6 list */
 #define MRT_K_TRROTY 11u    /* upload fuses translate(rotate_y(x)) into one instance node */
 #define MRT_K_BVHW 12u      /* upload: a bvh_node subtree over primitives / object_lists as wide nodes */
 

@@ -554,6 +554,21 @@ def test_interpreter_program_rewrite_within_tolerance(gpu, sid, monkeypatch):
     assert float(np.sqrt(((img2[..., :3].astype(np.float64) - g["image"]) ** 2).mean())) < 1e-3
 
 
+@pytest.mark.parametrize("sid", [5, 7])
+def test_interpreter_box_instance_step_is_bit_identical(gpu, sid, monkeypatch):
+    """The rewrite flags an instance whose body is one box.h list (MRT_F_BOXINST) and the interpreter
+    runs it as one step (instance ray in registers, box and slab tests, body skipped): the same
+    bits as stepping through INST, LIST, LIST_END, INST_END (MRT_NO_BOXINST=1)."""
+    monkeypatch.setenv("MRT_NO_SIG", "1")
+    sc = gpu.select_scene(sid, 1.0)
+    d = gpu.render_desc(64, 64, 64, numerics="fast")
+    img, rays = gpu.Renderer(sc, 0).render(d)
+    monkeypatch.setenv("MRT_NO_BOXINST", "1")
+    img2, rays2 = gpu.Renderer(sc, 0).render(d)
+    assert rays == rays2
+    assert np.array_equal(img.view(np.uint32), img2.view(np.uint32))
+
+
 @pytest.mark.parametrize("sid,w,h,spp,mode", [(5, 64, 64, 64, 0), (7, 48, 48, 16, 1), (8, 48, 48, 16, 0), (0, 200, 100, 16, 1)])
 def test_gpu_equals_cpu_backend(gpu, sid, w, h, spp, mode):
     """The two backends of the same hot-path source (the gfx950 path kernel and its host build,
