@@ -17,6 +17,7 @@ CSRC     = miniraytracer_amd/csrc
 OBJDIR   = build/obj
 
 LIB_OBJS = $(OBJDIR)/mrt_render.o $(OBJDIR)/mrt_kernels_exact.o $(OBJDIR)/mrt_kernels_fast.o $(OBJDIR)/mrt_kernels_fastz.o \
+           $(OBJDIR)/mrt_kernels_pex.o \
            $(OBJDIR)/mrt_cpu.o $(OBJDIR)/scene_builder.o $(OBJDIR)/mrt_common.o
 # the path kernels twice: exact contract (no contraction, IEEE division) and tolerance contract
 # (FMA contraction, reciprocal division, hardware rcp/sqrt/rsq, f32 transcendentals)
@@ -41,6 +42,12 @@ FTZFLAGS = -fgpu-flush-denormals-to-zero -DMRT_TABLE_FTZ=1
 $(OBJDIR)/mrt_kernels_fastz.o: $(CSRC)/mrt_kernels.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(HIPDEV) $(FASTFLAGS) $(FTZFLAGS) -c $< -o $@
+
+# the tolerance contract's path-exact variants (mrt_launch.h kPathExact): the exact build's
+# arithmetic with the forward fold
+$(OBJDIR)/mrt_kernels_pex.o: $(CSRC)/mrt_kernels.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) $(HIPDEV) -DMRT_FAST=0 -DMRT_FWD_FOLD=1 -DMRT_TABLE_PEX=1 -c $< -o $@
 
 # the CPU backend: the same hot-path headers compiled for the host only (exact contract).
 # -mfma: the reference's fused multiply-adds (mrt_device.h ref_fma) as one instruction instead of a

@@ -29,7 +29,13 @@ using namespace mrtd;
 #ifndef MRT_TABLE_FTZ
 #define MRT_TABLE_FTZ 0
 #endif
-#if MRT_TABLE_FTZ
+// the fourth: exact arithmetic + forward fold, the tolerance contract's kPathExact variants
+#ifndef MRT_TABLE_PEX
+#define MRT_TABLE_PEX 0
+#endif
+#if MRT_TABLE_PEX
+#define MRT_PATH_KERNEL mrt_path_kernel_pex
+#elif MRT_TABLE_FTZ
 #define MRT_PATH_KERNEL mrt_path_kernel_fastz
 #elif MRT_TABLE_FAST
 #define MRT_PATH_KERNEL mrt_path_kernel_fast
@@ -100,7 +106,7 @@ extern "C" int mrt_debug_phases(unsigned long long* out, int reset) {
 // per wave of the last launch: start, pool exhausted, end (s_memrealtime, 100 MHz), workgroup
 // + time inside successful / failed claim atomics (10-ns ticks) and their counts (ok | fail << 32)
 __device__ unsigned long long g_wtimes[7 * 16384];
-#if MRT_TABLE_FTZ || !MRT_TABLE_FAST  // the reader in one TU only (the FTZ build runs the Cornell kernels)
+#if (MRT_TABLE_FTZ || !MRT_TABLE_FAST) && !MRT_TABLE_PEX  // the reader in one TU only (the FTZ build runs the Cornell kernels)
 extern "C" int mrt_debug_wtimes(unsigned long long* out, int n) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wtimes), sizeof(unsigned long long) * 7 * (size_t)n) != hipSuccess;
 }
@@ -702,7 +708,10 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
 
 template <uint32_t F>
 static constexpr path_kernel_t kfn() {
-#if MRT_TABLE_FTZ
+#if MRT_TABLE_PEX
+    if constexpr (!kPathExact<F>) return nullptr;  // (not instantiated: another build runs it)
+    else
+#elif MRT_TABLE_FTZ
     if constexpr (!kFtzVariant<F>) return nullptr;  // (not instantiated: the plain fast build runs it)
     else
 #endif
@@ -722,7 +731,10 @@ static KernelTable make_table(const char* numerics, std::index_sequence<I...>) {
                        {kMesh4<kVariants[I]>...},
                        {(uint32_t)(kLinSlabOps<kVariants[I]> && MRT_SIG_OF(kVariants[I]) == SIG_NONE)...}};
 }
-#if MRT_TABLE_FTZ
+#if MRT_TABLE_PEX
+const KernelTable& mrtd::kernel_table_fast_pex() {
+    static const KernelTable t = make_table("fast", std::make_index_sequence<kNumVariants>{});
+#elif MRT_TABLE_FTZ
 const KernelTable& mrtd::kernel_table_fast_ftz() {
     static const KernelTable t = make_table("fast", std::make_index_sequence<kNumVariants>{});
 #elif MRT_TABLE_FAST

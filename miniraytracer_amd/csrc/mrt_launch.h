@@ -64,6 +64,7 @@ static_assert(MRT_TAIL_BATCH >= 64u && MRT_BATCH >= MRT_TAIL_BATCH, "claims must
 // variants need the scene's linear hit program (mrt_lin.h), FT_ALL runs any graph.  The same list
 // in both numerics builds.
 static constexpr uint32_t kVariants[] = {FT_LIN | FT_INST | FT_BIASED | MRT_SIG_BITS(SIG_CORNELL),
+                                         FT_LIN | FT_MESH | FT_BIASED | MRT_SIG_BITS(SIG_ROOM_MESH),
                                          FT_LIN | FT_MESH | FT_METAL | FT_BIASED | MRT_SIG_BITS(SIG_ROOM_MESH),
                                          FT_LIN | FT_INST | FT_BIASED,
                                          FT_LIN | FT_MESH | FT_METAL | FT_BIASED,
@@ -96,9 +97,25 @@ const KernelTable& kernel_table_fast();
 #ifndef MRT_FAST_FTZ
 #define MRT_FAST_FTZ 1
 #endif
+// Tolerance-contract variants that run the exact arithmetic with the forward fold (a fourth build,
+// mrt_kernels_pex.o / mrt_path_kernel_pex<F>): scenes with volumes, and the room + mesh scenes with
+// metal.  In them ANY change of rounding sends paths elsewhere -- book2 diverges on 2.9% of its
+// paths under the fast arithmetic, and no single switch of it is the cause (each one reverted
+// alone leaves 2.3-2.9%), the bunny on 0.015% -- and the diverged paths carry their scenes'
+// fireflies (fog scattering next to the light; the light's caustics through the metal bunny): at
+// the configs' own spp the fast arithmetic misses the per-pixel bar (C4 2.3e-3, one pixel 90% of
+// it; C5 1.6e-3) where the exact arithmetic holds it (2.0e-5, 9.2e-6).  DESIGN.md section 2.
+#ifndef MRT_PATH_EXACT
+#define MRT_PATH_EXACT 1
+#endif
 template <uint32_t F>
-static constexpr bool kFtzVariant = MRT_FAST_FTZ && (F & FT_VOLUME) == 0;
+static constexpr bool kPathExact =
+    MRT_PATH_EXACT && ((F & FT_VOLUME) != 0 || (MRT_SIG_OF(F) == SIG_ROOM_MESH && (F & FT_METAL) != 0));
+template <uint32_t F>
+static constexpr bool kFtzVariant = MRT_FAST_FTZ && (F & FT_VOLUME) == 0 && !kPathExact<F>;
 // the FTZ build's table: a kernel for the kFtzVariant variants, null for the others
 const KernelTable& kernel_table_fast_ftz();
+// the path-exact build's table: a kernel for the kPathExact variants, null for the others
+const KernelTable& kernel_table_fast_pex();
 
 }  // namespace mrtd

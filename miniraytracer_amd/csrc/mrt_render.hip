@@ -39,14 +39,32 @@ using namespace mrtd;
 // The tolerance contract's kernels: the plain fast build, with the kFtzVariant variants taken
 // from the denormal-flushing build (mrt_launch.h); MRT_FTZ=0 in the environment keeps the plain
 // build for every variant (A/B).
+// the tolerance contract's kernels: per variant the path-exact build (kPathExact), else the
+// denormal-flushing build (kFtzVariant), else the plain fast build -- the variant's whole column
+// (a build's workgroup shape, LDS fold levels and walk flags follow its own switches)
+static void take_variant(KernelTable& m, const KernelTable& s, uint32_t i) {
+    m.kernel[i] = s.kernel[i];
+    m.lev_k[i] = s.lev_k[i];
+    m.wg[i] = s.wg[i];
+    m.tree[i] = s.tree[i];
+    m.pq[i] = s.pq[i];
+    m.box6_walk[i] = s.box6_walk[i];
+    m.mesh4[i] = s.mesh4[i];
+    m.rewrite[i] = s.rewrite[i];
+}
 static const KernelTable& fast_table() {
     static const KernelTable t = [] {
         KernelTable m = kernel_table_fast();
-        const char* e = getenv("MRT_FTZ");
-        if (e && *e && atoi(e) == 0) return m;
+        auto off = [](const char* name) {  // A/B hooks: MRT_FTZ=0, MRT_PATH_EXACT=0
+            const char* e = getenv(name);
+            return e && *e && atoi(e) == 0;
+        };
         const KernelTable& z = kernel_table_fast_ftz();
-        for (uint32_t i = 0; i < kNumVariants; i++)
-            if (z.kernel[i]) m.kernel[i] = z.kernel[i];
+        const KernelTable& x = kernel_table_fast_pex();
+        for (uint32_t i = 0; i < kNumVariants; i++) {
+            if (x.kernel[i] && !off("MRT_PATH_EXACT")) take_variant(m, x, i);
+            else if (z.kernel[i] && !off("MRT_FTZ")) take_variant(m, z, i);
+        }
         return m;
     }();
     return t;
