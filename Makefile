@@ -44,10 +44,13 @@ $(OBJDIR)/mrt_kernels_fastz.o: $(CSRC)/mrt_kernels.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) $(HIPDEV) $(FASTFLAGS) $(FTZFLAGS) -c $< -o $@
 
 # the tolerance contract's path-exact variants (mrt_launch.h kPathExact): the exact build's
-# arithmetic with the forward fold
+# arithmetic with the forward fold; its bvh_node kernels in two 12-wave groups per CU (6 waves per
+# SIMD, 80 VGPRs): book2 4.83 against 4.19 Grays/s in one 16-wave group, 2.90 in two 10-wave groups
+# (profiles/r04_ab.txt)
+PEXFLAGS = -DMRT_FAST=0 -DMRT_FWD_FOLD=1 -DMRT_TABLE_PEX=1 -DMRT_TREE_WG=768 -DMRT_WPE_WIDE=6
 $(OBJDIR)/mrt_kernels_pex.o: $(CSRC)/mrt_kernels.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) $(HIPDEV) -DMRT_FAST=0 -DMRT_FWD_FOLD=1 -DMRT_TABLE_PEX=1 -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(HIPDEV) $(PEXFLAGS) -c $< -o $@
 
 # the CPU backend: the same hot-path headers compiled for the host only (exact contract).
 # -mfma: the reference's fused multiply-adds (mrt_device.h ref_fma) as one instruction instead of a

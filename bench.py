@@ -184,11 +184,11 @@ def roofline(args, k_ms, rays_per_launch, numerics, kinfo):
     WRITE_SIZE, MI355X_MICROARCH.md) -> hbm_frac.  Per-ray figures, so a rank's share (world > 1)
     is priced by its own rays; they do not depend on spp."""
     k_s = k_ms * 1e-3
-    # the kernel's name in rocprofv3 traces: the tolerance contract's variants without volumes run
-    # the denormal-flushing build (mrt_launch.h kFtzVariant; MRT_FTZ=0 turns it off)
-    FT_VOLUME = 1 << 2
-    ftz = numerics == "fast" and not (kinfo.get("kernel_features", 0) & FT_VOLUME) and os.environ.get("MRT_FTZ", "1") != "0"
-    kname = "mrt_path_kernel" + (("_fastz" if ftz else "_fast") if numerics == "fast" else "")
+    # the kernel's name in rocprofv3 traces: per variant the tolerance contract runs the fast, the
+    # denormal-flushing or the path-exact build (mrt_launch.h kFtzVariant / kPathExact)
+    from miniraytracer_amd._lib import BUILDS
+    build = BUILDS[kinfo.get("build", 0)]
+    kname = "mrt_path_kernel" + ("" if build == "exact" else "_" + build)
     out = {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_G, 1), "unit": "G VALU wave-instr/s", "frac": None,
            "traffic": None, "kernel": kname, "kernel_ms": round(k_ms, 3),
            "rays_per_launch": int(rays_per_launch),

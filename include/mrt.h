@@ -175,9 +175,15 @@ mrt_status mrt_kernel_ms(mrt_scene* s, float* path_ms, uint32_t* launches);
 
 /* Which path kernel the scene runs: feature bits of the scene (FT_* of mrt_trace.h; bit 11 =
  * linear hit program, DESIGN.md "Kernels"), dynamic LDS bytes per workgroup, grid size in
- * workgroups, threads per workgroup and the BVH nodes each workgroup keeps in LDS. */
+ * workgroups, threads per workgroup, the BVH nodes each workgroup keeps in LDS, and the build of
+ * the kernel for the last render's numerics: MRT_BUILD_* (the tolerance contract runs the fast,
+ * the denormal-flushing or the path-exact build per kernel variant). */
+#define MRT_BUILD_EXACT 0u
+#define MRT_BUILD_FAST 1u
+#define MRT_BUILD_FAST_FTZ 2u
+#define MRT_BUILD_PATH_EXACT 3u
 typedef struct mrt_kernel_info {
-    uint32_t features, kernel_features, lds_bytes, grid, prog_ops, vgprs, wg, tree_nodes;
+    uint32_t features, kernel_features, lds_bytes, grid, prog_ops, vgprs, wg, tree_nodes, build;
 } mrt_kernel_info;
 mrt_status mrt_scene_kernel_info(const mrt_scene* s, mrt_kernel_info* out);
 

@@ -62,7 +62,8 @@ class MrtSceneView(C.Structure):
 class KernelInfo(C.Structure):
     _fields_ = [("features", C.c_uint32), ("kernel_features", C.c_uint32), ("lds_bytes", C.c_uint32),
                 ("grid", C.c_uint32), ("prog_ops", C.c_uint32), ("vgprs", C.c_uint32), ("wg", C.c_uint32),
-                ("tree_nodes", C.c_uint32)]
+                ("tree_nodes", C.c_uint32), ("build", C.c_uint32)]
+BUILDS = ("exact", "fast", "fastz", "pex")  # MRT_BUILD_*: the kernel build (mrt_path_kernel[_fast|_fastz|_pex])
 
 
 FT_LIN = 1 << 11  # kernel feature bit: linear hit program (mrt_lin.h)

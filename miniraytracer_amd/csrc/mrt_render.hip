@@ -1527,6 +1527,10 @@ extern "C" mrt_status mrt_scene_kernel_info(const mrt_scene* s, mrt_kernel_info*
     out->vgprs = L.vgprs;
     out->wg = L.wg;
     out->tree_nodes = L.tree_n;  // BvhWide nodes per workgroup
+    out->build = s->last_numerics == 0 ? MRT_BUILD_EXACT
+               : L.fn == kernel_table_fast_pex().kernel[s->variant] ? MRT_BUILD_PATH_EXACT
+               : L.fn == kernel_table_fast_ftz().kernel[s->variant] ? MRT_BUILD_FAST_FTZ
+                                                                     : MRT_BUILD_FAST;
     return MRT_OK;
 }
 

@@ -181,6 +181,18 @@ def test_kernel_selection(gpu):
         assert bool(info["kernel_features"] & gpu._lib.FT_LIN) == want_lin, (sid, info)
 
 
+def test_tolerance_contract_builds(gpu):
+    """The tolerance contract runs the path-exact build (exact arithmetic, forward fold) for volume
+    scenes and the metal room + mesh scene, the denormal-flushing fast build for the others; the
+    exact contract the exact build (mrt_kernel_info.build)."""
+    for sid, want in [(5, "fastz"), (9, "fastz"), (0, "fastz"), (8, "pex"), (7, "pex"), (6, "pex")]:
+        r = gpu.Renderer(gpu.select_scene(sid, 1.0), 0)
+        r.render(gpu.render_desc(16, 16, 1, numerics="fast"))
+        assert gpu._lib.BUILDS[r.kernel_info()["build"]] == want, sid
+        r.render(gpu.render_desc(16, 16, 1, numerics="exact"))
+        assert gpu._lib.BUILDS[r.kernel_info()["build"]] == "exact", sid
+
+
 @pytest.mark.parametrize("sid,w,h,spp", [(5, 64, 64, 16), (9, 40, 40, 9), (8, 40, 40, 9)])
 def test_shape_specialised_walk_equals_interpreter(gpu, sid, w, h, spp, monkeypatch):
     """Reference scenes whose linear program has a known shape (mrt_sig.h) run a walk unrolled at

@@ -245,13 +245,14 @@ def test_bench_roofline_prices_pmc_per_ray(tmp_path):
                                "by_numerics": {"fast": {"valu_insts_per_ray": 9.0, "hbm_bytes_per_ray": 7.0, "valu_lane_util": 0.6,
                                                         "valu_busy": 0.7}}}))
     args = types.SimpleNamespace(scene=5, width=500, height=500, depth=32, pmc_json=str(pmc))
-    ki = dict(grid=1, wg=64, lds_bytes=0, vgprs=72, tree_nodes=0, kernel_features=0x2000 | 0x800 | 0x8 | (1 << 16))
+    ki = dict(grid=1, wg=64, lds_bytes=0, vgprs=72, tree_nodes=0, kernel_features=0x2000 | 0x800 | 0x8 | (1 << 16), build=2)
     r = bench.roofline(args, 8.0, 778e6, "fast", ki)
     assert r["bound"] == "valu" and r["peak"] == pytest.approx(1228.8)
-    # the kernel's rocprofv3 name: the Cornell variant (no volumes) runs the denormal-flushing build
+    # the kernel's rocprofv3 name from the build the library reports (mrt_kernel_info.build)
     assert r["kernel"] == "mrt_path_kernel_fastz"
-    assert bench.roofline(args, 8.0, 778e6, "fast", dict(ki, kernel_features=0x3FFF))["kernel"] == "mrt_path_kernel_fast"
-    assert bench.roofline(args, 8.0, 778e6, "exact", ki)["kernel"] == "mrt_path_kernel"
+    assert bench.roofline(args, 8.0, 778e6, "fast", dict(ki, build=1))["kernel"] == "mrt_path_kernel_fast"
+    assert bench.roofline(args, 8.0, 778e6, "fast", dict(ki, build=3))["kernel"] == "mrt_path_kernel_pex"
+    assert bench.roofline(args, 8.0, 778e6, "exact", dict(ki, build=0))["kernel"] == "mrt_path_kernel"
     assert r["achieved"] == pytest.approx(9.0 * 778e6 / 8e-3 / 1e9, rel=1e-3)
     assert 0 < r["frac"] <= 1 and r["traffic"] == round(7.0 * 778e6)
     half = bench.roofline(args, 4.0, 389e6, "fast", ki)  # a rank's half: same rates

@@ -31,6 +31,10 @@ if [ -n "${HOST_FLAGS:-}" ]; then  # host TU too (e.g. -DMRT_PATH_WG=..., which 
 fi
 PX=build/obj/mrt_kernels_pex.o  # the path-exact variants as in the Makefile (run MRT_PATH_EXACT=0 to A/B them)
 make -s $PX
+if [ -n "${PEX_FLAGS:-}" ]; then  # ... or built with extra flags
+  /opt/rocm/bin/hipcc $BASE -ffp-contract=off $(make -s -f Makefile -p 2>/dev/null | sed -n 's/^PEXFLAGS = //p') $PEX_FLAGS -c miniraytracer_amd/csrc/mrt_kernels.hip -o exp/obj_$tag/mrt_kernels_pex.o
+  PX=exp/obj_$tag/mrt_kernels_pex.o
+fi
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $RO $EX $PX exp/obj_$tag/mrt_kernels_fast.o exp/obj_$tag/mrt_kernels_fastz.o \
     build/obj/mrt_cpu.o build/obj/scene_builder.o build/obj/mrt_common.o -ldl -o exp/libmrt_$tag.so
 echo "built exp/libmrt_$tag.so"

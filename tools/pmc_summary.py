@@ -33,8 +33,13 @@ N_SIMD = 1024  # 256 CUs x 4 SIMDs
 
 
 def kernel_key(name):
+    """one key per numerics contract: the tolerance contract's builds (mrt_path_kernel_fast, _fastz,
+    _pex: mrt_launch.h kFtzVariant / kPathExact) under mrt_path_kernel_fast, the exact build under
+    mrt_path_kernel"""
     base = name.split("(")[0]
-    return "mrt_path_kernel_fast" if "mrt_path_kernel_fast" in base else ("mrt_path_kernel" if "mrt_path_kernel" in base else base)
+    if "mrt_path_kernel_fast" in base or "mrt_path_kernel_pex" in base:
+        return "mrt_path_kernel_fast"
+    return "mrt_path_kernel" if "mrt_path_kernel" in base else base
 
 
 def per_dispatch(path):
