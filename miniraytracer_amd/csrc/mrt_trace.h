@@ -774,8 +774,15 @@ MRT_DFN bool bvhw_leaf(const DScene& S, uint32_t ref, const Ray& r, float tmin, 
             return true;
         }
         // the second test repeats the first's predicate with the same operands and range: its
-        // arithmetic is contraction-proof (explicit ref_f* / madd_det fusions, the rest unfused), so it hits again
-        (void)leaf_prim_hit<F>(n, k, r, tmin, tmax, rec, true);
+        // arithmetic is contraction-proof (explicit ref_f* / madd_det fusions, the rest unfused), so it
+        // hits again.  (Returning its result instead of true changed the register allocation of the
+        // whole walk: book2's fast kernel 40 -> 204 spilled VGPRs, round 4.  MRT_CHECK_LEAF builds
+        // assert it.)
+        const bool again = leaf_prim_hit<F>(n, k, r, tmin, tmax, rec, true);
+#ifdef MRT_CHECK_LEAF
+        if (!again) __builtin_trap();
+#endif
+        (void)again;
         return true;
     }
     // The run's primitives are tested for t alone; the closest one's full record is computed once
@@ -812,8 +819,13 @@ MRT_DFN bool bvhw_leaf(const DScene& S, uint32_t ref, const Ray& r, float tmin, 
     }
     const mrt_node c = ld_node_v(run + best);
     const uint32_t ck = MRT_NODE_KIND(c);
-    if (MRT_FAST_BOX && ck == MRT_K_LIST) (void)box6_leaf_hit(c, r, tmin, t_before, rec, true);
-    else (void)leaf_prim_hit<F>(c, ck, r, tmin, t_before, rec, true);
+    bool again;  // (the same test with the same range: it hits again; see the one-primitive case)
+    if (MRT_FAST_BOX && ck == MRT_K_LIST) again = box6_leaf_hit(c, r, tmin, t_before, rec, true);
+    else again = leaf_prim_hit<F>(c, ck, r, tmin, t_before, rec, true);
+#ifdef MRT_CHECK_LEAF
+    if (!again) __builtin_trap();
+#endif
+    (void)again;
     return true;
 }
 
