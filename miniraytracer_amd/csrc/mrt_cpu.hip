@@ -468,3 +468,18 @@ extern "C" int mrt_debug_mesh4_walks(const mrt_scene_view* v, uint32_t n_rays, u
     mrt_cpu_scene_free(c);
     return 0;
 }
+
+// Test hook (tests/test_host.py): the scene's linear hit program as compiled, or its
+// tolerance-contract rewrite (mrt_sig.h lin_rewrite_fast) -- per op its code word and skip.
+extern "C" int mrt_debug_lin_program(const mrt_scene_view* v, int rewritten, uint32_t* codes, uint32_t* skips, uint32_t cap,
+                                     uint32_t* n) {
+    SceneTables T;
+    if (mrt_internal_scene_tables(v, &T) != MRT_OK) return 1;
+    const std::vector<LinOp>& p = rewritten ? T.prog_fast : T.prog;
+    *n = (uint32_t)p.size();
+    for (uint32_t i = 0; i < p.size() && i < cap; i++) {
+        codes[i] = p[i].code;
+        skips[i] = p[i].skip;
+    }
+    return 0;
+}

@@ -259,3 +259,42 @@ def test_bench_roofline_prices_pmc_per_ray(tmp_path):
     assert half["frac"] == pytest.approx(r["frac"], rel=1e-3) and half["hbm_frac"] == pytest.approx(r["hbm_frac"], rel=1e-3)
     args.width = 640
     assert bench.roofline(args, 8.0, 778e6, "fast", ki)["frac"] is None
+
+
+def _lin_program(mrt, sid, rewritten):
+    import ctypes as C
+    sc = mrt.select_scene(sid, 1.0)
+    fn = mrt.lib().mrt_debug_lin_program
+    fn.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]
+    fn.restype = C.c_int
+    codes = np.zeros(4096, dtype=np.uint32)
+    skips = np.zeros(4096, dtype=np.uint32)
+    n = np.zeros(1, dtype=np.uint32)
+    assert fn(C.byref(sc.view), int(rewritten), codes.ctypes.data, skips.ctypes.data, 4096, n.ctypes.data) == 0
+    sc.close()
+    return codes[:int(n[0])], skips[:int(n[0])]
+
+
+@pytest.mark.parametrize("sid", [5, 8, 9, 0, 7])
+def test_program_rewrite_structure(mrt, sid):
+    """The tolerance contract's program rewrite (mrt_sig.h lin_rewrite_fast): the Cornell rooms'
+    inward-facing walls become one LOP_ROOM + LOP_ROOMDATA pair, an instance of one box.h list is
+    flagged MRT_F_BOXINST, nothing else changes, and every LIST / INST skip still lands on its END
+    op.  Scenes without rooms (0, 7) keep their program."""
+    LIST, LIST_END, INST, INST_END, ROOM, ROOMDATA = 3, 4, 5, 6, 10, 11
+    c0, s0 = _lin_program(mrt, sid, False)
+    c1, s1 = _lin_program(mrt, sid, True)
+    op0, op1 = c0 & 0xFF, c1 & 0xFF
+    assert ROOM not in op0 and ROOMDATA not in op0
+    rooms = int((op1 == ROOM).sum())
+    if sid in (5, 8, 9):
+        assert rooms == 1 and op1[list(op1).index(ROOM) + 1] == ROOMDATA
+        # the room's walls (five rects in these scenes) replaced by the pair
+        assert len(op1) == len(op0) - 5 + 2
+    else:
+        assert rooms == 0 and np.array_equal(c0 & ~np.uint32(0x20 << 16), c1 & ~np.uint32(0x20 << 16))
+    boxinst = [(c >> 16) & 0x20 for c, o in zip(c1, op1) if o == INST]
+    assert sum(1 for b in boxinst if b) == (1 if sid == 5 else 0)
+    for i, (o, k) in enumerate(zip(op1, s1)):
+        if o in (LIST, INST):
+            assert i < k < len(op1) and op1[k] == (LIST_END if o == LIST else INST_END), (i, o, k)
