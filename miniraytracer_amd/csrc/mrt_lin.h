@@ -485,7 +485,6 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
             hnode = h ? prog[pc + 2 + c].node : hnode;
             hinst = h ? pc : hinst;
             hdone = h ? false : hdone;
-            if constexpr (RR) hrc = h ? 0u : hrc;  // (an instance's record: through the node load)
             if (h) {  // the instance-frame ray of the hit, for the record (as at LOP_INST_END)
                 float* b = L.save + L.lane + 9 * 64;
                 b[0] = ci.o.x; b[64] = ci.o.y; b[128] = ci.o.z;
