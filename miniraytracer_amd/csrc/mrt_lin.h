@@ -301,9 +301,6 @@ MRT_DFN void lin_untransform(const OP& io, HitRec& rec) {
 // subtrees, volumes, textures or motion only: in the catch-all interpreter kernel their two cases
 // tripled book2's register spills (C5 2.7x slower, profiles/r04_ab.txt).  The other kernels run
 // the program as compiled (the host uploads the rewrite only where KernelTable::rewrite says so).
-#ifndef MRT_LIN_RECREG
-#define MRT_LIN_RECREG 1  // the interpreter's rect records from registers (scene_hit_lin)
-#endif
 #ifndef MRT_BOXINST
 #define MRT_BOXINST 1  // the one-step box instance (MRT_F_BOXINST)
 #endif
@@ -325,12 +322,6 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
     uint32_t hnode = MRT_NONE;    // node of the closest hit so far (MRT_NONE: none)
     uint32_t hinst = MRT_NONE;    // op index of the instance it lies in (MRT_NONE: world frame)
     bool hdone = false;           // rec already holds the closest hit (mesh_hit writes it)
-    // kernels with the slab ops: a world-frame rect hit (room wall, box.h face, rect without uv)
-    // keeps its record's inputs in registers -- 1 + axis, plane, normal sign, material -- so the
-    // record needs no per-lane load of the hit node after the walk (hrc 0: that load, as before)
-    constexpr bool RR = MRT_LIN_RECREG && kLinSlabOps<F> && MRT_FAST_SNAP;
-    uint32_t hrc = 0u, hmat = 0u;
-    float hk = 0.0f, hns = 0.0f;
     const MRT_CONST_AS LinOp* prog = const_ptr(S.prog);
     for (uint32_t pc = 0;; pc++) {
         const MRT_CONST_AS LinOp& o = prog[pc];
@@ -351,15 +342,6 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
             hnode = h ? o.node : hnode;
             hinst = h ? inst : hinst;
             hdone = h ? false : hdone;
-            if constexpr (RR) {
-                const uint32_t kd = LOP_KIND(o);  // uniform
-                const uint32_t rc = (kd == MRT_K_SPHERE || (LOP_FLAGS(o) & MRT_F_NEEDUV) || inst != MRT_NONE) ? 0u
-                                  : kd == MRT_K_XY ? 3u : kd == MRT_K_XZ ? 2u : 1u;
-                hrc = h ? rc : hrc;
-                hk = h ? o.f[4] : hk;
-                hns = h ? o.f[5] : hns;
-                hmat = h ? o.mat : hmat;
-            }
             PH_MARK(ph, 9);
         } else if ((F & FT_MESH) && op == LOP_MESH) {
             if (on && mesh_hit<true>(S, ld_node(const_ptr(S.nodes) + o.node), cur, tmin, closest, rec, true, L)) {
@@ -426,14 +408,6 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
             hnode = h ? fnode[face] : hnode;
             hinst = h ? inst : hinst;
             hdone = h ? false : hdone;
-            if constexpr (RR) {  // face = axis * 2 + side: side 0 the min plane, normal +axis
-                const uint32_t a = face >> 1;
-                const bool hi = (face & 1u) != 0u;
-                hrc = h ? (inst != MRT_NONE ? 0u : a + 1u) : hrc;
-                hk = h ? (a == 0u ? (hi ? o.f[3] : o.f[0]) : a == 1u ? (hi ? o.f[4] : o.f[1]) : (hi ? o.f[5] : o.f[2])) : hk;
-                hns = h ? (hi ? -1.0f : 1.0f) : hns;
-                hmat = h ? fnode[6 + face] : hmat;
-            }
             pc++;
         } else if (MRT_FAST_BOX && kLinSlabOps<F> && op == LOP_LIST && (LOP_FLAGS(o) & MRT_F_BOX6)) {  // uniform
             // box.h's six rects as one slab test (its own box test implied), the list skipped
@@ -444,14 +418,6 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
             hnode = h ? prog[pc + 1 + c].node : hnode;
             hinst = h ? inst : hinst;
             hdone = h ? false : hdone;
-            if constexpr (RR) {  // child c: xy at max z, at min z, xz at max y, min y, yz at max x, min x
-                const uint32_t a = 2u - (c >> 1);
-                const bool mn = (c & 1u) != 0u;
-                hrc = h ? (inst != MRT_NONE ? 0u : a + 1u) : hrc;
-                hk = h ? (a == 0u ? (mn ? o.f[6] : o.f[9]) : a == 1u ? (mn ? o.f[7] : o.f[10]) : (mn ? o.f[8] : o.f[11])) : hk;
-                hns = h ? (mn ? -1.0f : 1.0f) : hns;
-                hmat = h ? o.mat : hmat;
-            }
             pc = o.skip;  // past its LOP_LIST_END
         } else if (op == LOP_LIST) {  // object_list::hit box reject (scene_object.h:83)
             bool in = on;
@@ -527,17 +493,6 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
     }
     if (INST) r = park ? lin_load_ray(L) : cur;
     if (hnode == MRT_NONE) return false;
-    if constexpr (RR) {
-        if (hrc != 0u && !hdone) {  // lin_prim_rec's rect record from the registers
-            const uint32_t a = hrc - 1u;
-            rec.t = closest;
-            rec.mat = hmat;
-            const f3 p0 = eval(r, closest);
-            rec.p = f3{a == 0u ? hk : p0.x, a == 1u ? hk : p0.y, a == 2u ? hk : p0.z};
-            rec.n = f3{a == 0u ? hns : 0.0f, a == 1u ? hns : 0.0f, a == 2u ? hns : 0.0f};
-            return true;
-        }
-    }
     if (INST && hinst != MRT_NONE) {
         if (!hdone) {
             const float* b = L.save + L.lane + 9 * 64;

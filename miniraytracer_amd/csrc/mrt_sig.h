@@ -181,9 +181,7 @@ inline std::vector<LinOp> lin_rewrite_fast(const std::vector<LinOp>& prog) {
         d.code = LOP_ROOMDATA | (prog[first].code & 0xFF000000u);
         for (uint32_t k = 0; k < 6; k++) {
             const uint32_t node = pick[k] >= 0 ? prog[pick[k]].node : MRT_NONE;
-            const uint32_t mat = pick[k] >= 0 ? prog[pick[k]].mat : MRT_NONE;
             __builtin_memcpy(&d.f[k], &node, 4);
-            __builtin_memcpy(&d.f[6 + k], &mat, 4);  // (the interpreter's register record, mrt_lin.h)
             if (pick[k] >= 0) del[pick[k]] = 1;
         }
         room[first] = r;
