@@ -118,9 +118,6 @@ mrt_status mrt_cpu_scene_create(const mrt_scene_view* v, mrt_cpu_scene** out) {
     S.perm = c->perm.data();
     S.texels = c->texels.data();
     S.prog = T.prog.data();
-    S.lin_park = 0;
-    for (const LinOp& o : T.prog)
-        if ((o.code & 0xFFu) == LOP_INST) S.lin_park = 1;
     S.bleaf = T.bleaf.data();
     S.nbleaf = T.nbleaf;
     S.nbleaf_f = (float)T.nbleaf;

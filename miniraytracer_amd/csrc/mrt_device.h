@@ -113,8 +113,7 @@ MRT_DFN f3 divf(f3 a, float f) {
     return f3{a.x * y, a.y * y, a.z * y};
 }
 #else
-MRT_DFN float div_x(float a, float b);
-MRT_DFN f3 divf(f3 a, float f) { return f3{div_x(a.x, f), div_x(a.y, f), div_x(a.z, f)}; }
+MRT_DFN f3 divf(f3 a, float f) { return f3{a.x / f, a.y / f, a.z / f}; }
 #endif
 MRT_DFN float dot(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 MRT_DFN float sdot(f3 a) { return (a.x * a.x + a.y * a.y) + a.z * a.z; }
@@ -193,24 +192,6 @@ MRT_DFN uint32_t mag2(float x) { return __float_as_uint(x) << 1; }
 #define MRT_MAG2(e) ((uint32_t)((e) + 127) << 24)
 // |x| in [2^lo, 2^hi)
 #define MRT_MAG_IN(x, lo, hi) ((uint32_t)((mag2(x) - MRT_MAG2(lo)) < (MRT_MAG2(hi) - MRT_MAG2(lo))))
-// a / b, the IEEE quotient, without the IEEE division sequence (div_scale, rcp, 4 fma,
-// div_fmas, div_fixup and the denormal-mode switches): y = RN(1/b) by recip_nr, then div_core's
-// residual correction (Markstein).  Checked exhaustively on the GPU over every normal divisor, with
-// numerators spread over the exponents (tools/numcheck/markstein_check.hip): exact when b and y
-// are normal and a is zero or the quotient normal with |a| >= 2^-100; other lanes take the IEEE
-// division.  The tolerance build divides by reciprocal.
-MRT_DFN float div_x(float a, float b) {
-#if MRT_FAST_DIV || !defined(__HIP_DEVICE_COMPILE__)
-    return a / b;
-#else
-    const float y = recip_nr(b);
-    const float q = div_core(a, b, y);
-    const bool ok = MRT_MAG_IN(b, -126, 128) & MRT_MAG_IN(y, -126, 128) &
-                    ((mag2(a) == 0u) | (MRT_MAG_IN(q, -126, 128) & (mag2(a) >= MRT_MAG2(-100))));
-    if (__builtin_expect(any_lane(!ok), 0)) return ok ? q : a / b;
-    return q;
-#endif
-}
 // Correctly rounded f32 square root.  hipcc's expansion is v_sqrt_f32, a one-ulp neighbour test
 // by fma residuals, and a 2^32 scaling of inputs below 2^-96 (+ zero/inf fix-up); the core alone
 // equals it for every input with |x| >= 2^-96 or x == +-0 (all 2^32 patterns checked on MI355X,
@@ -359,7 +340,7 @@ MRT_DFN f3 random_cosine_direction_pre(float r1, float r2) {
 }
 // random_towards_sphere (pcg.cpp:125-133) given its two draws r1, r2 (sphere::pdf_generate, sphere.cpp:63-78)
 MRT_DFN f3 random_towards_sphere_pre(float r1, float r2, float radius, float dist_sq) {
-    float z = ref_fma(r2, sqrt_(1 - div_x(radius * radius, dist_sq)) - 1, 1);  // pcg.cpp:128
+    float z = ref_fma(r2, sqrt_(1 - (radius * radius) / dist_sq) - 1, 1);  // pcg.cpp:128
     float phi = (2 * PI_F) * r1;
     float q = sqrt_(ref_fnma(z, z, 1));  // pcg.cpp:130-131
     float sp, cp;

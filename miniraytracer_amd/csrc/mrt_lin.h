@@ -61,7 +61,7 @@ MRT_DFN bool lin_prim_t(const OP& o, const Ray& r, float tmin, float tmax, float
     if constexpr (KIND == MRT_K_SPHERE) {  // sphere::hit (sphere.cpp:13-46)
         f3 cen = f3{o.f[0], o.f[1], o.f[2]};
         if ((F & FT_MOVING) && (LOP_FLAGS(o) & MRT_F_MOVING))
-            cen = add(cen, fmul(div_x(r.time - o.f[6], o.f[7] - o.f[6]), sub(f3{o.f[3], o.f[4], o.f[5]}, cen)));
+            cen = add(cen, fmul((r.time - o.f[6]) / (o.f[7] - o.f[6]), sub(f3{o.f[3], o.f[4], o.f[5]}, cen)));
         const float radius = o.f[8];
         const f3 oc = sub(r.o, cen);
         float b;
@@ -114,7 +114,7 @@ MRT_DFN void lin_prim_rec_op(const MRT_CONST_AS LinOp& o, const Ray& r, float t,
     if constexpr (KIND == MRT_K_SPHERE) {
         f3 cen = f3{o.f[0], o.f[1], o.f[2]};
         if ((F & FT_MOVING) && (fl & MRT_F_MOVING))
-            cen = add(cen, fmul(div_x(r.time - o.f[6], o.f[7] - o.f[6]), sub(f3{o.f[3], o.f[4], o.f[5]}, cen)));
+            cen = add(cen, fmul((r.time - o.f[6]) / (o.f[7] - o.f[6]), sub(f3{o.f[3], o.f[4], o.f[5]}, cen)));
         rec.n = divf(sub(rec.p, cen), o.f[8]);
         if (needuv) sphere_uv(rec.n, &rec.u, &rec.v);
     } else {
@@ -134,8 +134,8 @@ MRT_DFN void lin_prim_rec_op(const MRT_CONST_AS LinOp& o, const Ray& r, float t,
             if (needuv) { pb = ref_fma(t, r.d.y, r.o.y); pc = ref_fma(t, r.d.z, r.o.z); }
         }
         if (needuv) {
-            rec.u = div_x(pb - o.f[0], o.f[1] - o.f[0]);
-            rec.v = div_x(pc - o.f[2], o.f[3] - o.f[2]);
+            rec.u = (pb - o.f[0]) / (o.f[1] - o.f[0]);
+            rec.v = (pc - o.f[2]) / (o.f[3] - o.f[2]);
         }
     }
 }
@@ -163,7 +163,7 @@ MRT_DFN void lin_prim_rec(const DScene& S, uint32_t node, const Ray& r, float t,
     if (kind == MRT_K_SPHERE) {
         f3 cen = f3{nf[0], nf[1], nf[2]};
         if ((F & FT_MOVING) && ((code >> 16) & MRT_F_MOVING))
-            cen = add(cen, fmul(div_x(r.time - nf[6], nf[7] - nf[6]), sub(f3{nf[3], nf[4], nf[5]}, cen)));
+            cen = add(cen, fmul((r.time - nf[6]) / (nf[7] - nf[6]), sub(f3{nf[3], nf[4], nf[5]}, cen)));
         rec.n = divf(sub(rec.p, cen), nf[8]);
         if (needuv) sphere_uv(rec.n, &rec.u, &rec.v);
         return;
@@ -183,8 +183,8 @@ MRT_DFN void lin_prim_rec(const DScene& S, uint32_t node, const Ray& r, float t,
         rec.p.z = xy ? nf[4] : p0.z;
     }
     if (needuv) {
-        rec.u = div_x(pb - nf[0], nf[1] - nf[0]);
-        rec.v = div_x(pc - nf[2], nf[3] - nf[2]);
+        rec.u = (pb - nf[0]) / (nf[1] - nf[0]);
+        rec.v = (pc - nf[2]) / (nf[3] - nf[2]);
     }
 }
 
@@ -310,10 +310,7 @@ static constexpr bool kLinSlabOps = MRT_FAST && (F & FT_LIN) != 0 && (F & (FT_BV
 template <uint32_t F>
 MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, const LStack& L, Pcg& rng, PhaseClock& ph) {
     constexpr bool INST = (F & FT_INST) != 0;
-    // the query ray parked in LDS while instance rays occupy the registers -- not needed when the
-    // program's instances are all one-step box instances, which leave `cur` the query ray
-    const bool park = INST && (S.lin_park != 0u || !(MRT_BOXINST && kLinSlabOps<F>));  // uniform
-    if (park) lin_save_ray(L, r);
+    if (INST) lin_save_ray(L, r);
     Ray cur = r;
     float closest = FLT_MAX_;
     uint32_t act = 1u;            // bit l: this lane takes part at nesting level l
@@ -375,7 +372,7 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
                 if (a < b) {
                     if (a < 0) a = 0;
                     const float inside_dist = b - a;
-                    const float hit_dist = -div_x(1.0f, o.f[0]) * log_(randf(rng));
+                    const float hit_dist = -(1 / o.f[0]) * log_(randf(rng));
                     if (hit_dist < inside_dist) {
                         closest = a + hit_dist;
                         rec.t = closest;
@@ -491,7 +488,7 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
         }
         PH_MARK(ph, 8);
     }
-    if (INST) r = park ? lin_load_ray(L) : cur;
+    if (INST) r = lin_load_ray(L);
     if (hnode == MRT_NONE) return false;
     if (INST && hinst != MRT_NONE) {
         if (!hdone) {

@@ -302,7 +302,6 @@ struct mrt_scene {
     // workspace
     mrt_render_desc wdesc{};
     std::vector<uint32_t> wpixels;   // the pixel list of wdesc (mrt_render_desc.pixels), copied
-    uint32_t prog_fast_park = 1;  // lin_park of prog_fast
     const LinOp* prog_fast = nullptr;  // the tolerance contract's program for the interpreter (lin_rewrite_fast)
     bool have_ws = false;
     uint32_t npix = 0, chunk = 0;
@@ -997,15 +996,9 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     {
         const char* e = getenv("MRT_NO_REWRITE");  // A/B hook: the interpreter on the program as compiled
         if (!T.prog_fast.empty() && !(e && *e && *e != '0')) UP(T.prog_fast.data(), T.prog_fast.size(), &s->prog_fast);
-        s->prog_fast_park = 0;
-        for (const LinOp& o : T.prog_fast)
-            if ((o.code & 0xFFu) == LOP_INST && !((o.code >> 16) & MRT_F_BOXINST)) s->prog_fast_park = 1;
     }
     UP(&v->camera, 1, &S.camp);
 #undef UP
-    S.lin_park = 0;
-    for (const LinOp& o : T.prog)
-        if ((o.code & 0xFFu) == LOP_INST) S.lin_park = 1;
     S.root = v->root;
     S.biased = v->biased;
     S.sky = v->sky;
@@ -1306,10 +1299,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.sc = s->S;
         // the interpreter's tolerance-contract program (rooms and box.h lists as slab tests); the
         // shape-specialised walks read the program as compiled
-        if ((d->flags & MRT_RF_FAST) && s->prog_fast && PL.rewrite) {
-            P.sc.prog = s->prog_fast;
-            P.sc.lin_park = s->prog_fast_park;
-        }
+        if ((d->flags & MRT_RF_FAST) && s->prog_fast && PL.rewrite) P.sc.prog = s->prog_fast;
         P.lds_frames = s->lds_frames;
         P.lds_rays = s->lds_rays;
         P.lds_mesh = PL.lds_mesh;

@@ -113,16 +113,16 @@ MRT_DFN float leaf_pdf_value(const DScene& S, const mrt_node& n, f3 origin, f3 d
         const float area = (n.f[1] - n.f[0]) * (n.f[3] - n.f[2]);
         const float dist_sq = t * t;
         const float cosine = fabsf(dot(dir, f3{0, n.f[5], 0}));
-        const float pdf = div_x(dist_sq, cosine * area);
+        const float pdf = dist_sq / (cosine * area);
         return h ? pdf : 0.0f;
     }
     if ((F & FT_BSPHERE) && k == MRT_K_SPHERE) {
         Ray r = make_ray_unit<kFastUnit<F>>(origin, dir, time, 0);
         if (sphere_hit<F>(n, r, 0.001f, FLT_MAX_, rec, false)) {
             float radius = n.f[8];
-            float cos_theta_max = sqrt_(1 - div_x(radius * radius, sdot(sub(sphere_center<F>(n, time), origin))));
+            float cos_theta_max = sqrt_(1 - (radius * radius) / sdot(sub(sphere_center<F>(n, time), origin)));
             float solid_angle = (2 * PI_F) * (1 - cos_theta_max);
-            return div_x(1.0f, solid_angle);
+            return 1 / solid_angle;
         }
         return 0;
     }
@@ -149,7 +149,7 @@ MRT_DFN float biased_pdf_value(const DScene& S, f3 origin, f3 dir, float time) {
 #if MRT_FAST
     return sum * S.inv_nbleaf;  // (-freciprocal-math: the division by the loop-invariant count)
 #else
-    return div_x(sum, S.nbleaf_f);
+    return sum / S.nbleaf_f;
 #endif
 }
 template <uint32_t F>
@@ -263,7 +263,7 @@ MRT_DFN void push_level(PathState& ps, const LevStore<LK>& lev, float4 lv) {
 #if MRT_FWD_FOLD
     (void)lev;
     if (lv.w < 0.0f) ps.T = f3{ps.T.x * lv.x, ps.T.y * lv.y, ps.T.z * lv.z};
-    else ps.T = f3{div_x(ps.T.x * lv.x, lv.w), div_x(ps.T.y * lv.y, lv.w), div_x(ps.T.z * lv.z, lv.w)};
+    else ps.T = f3{(ps.T.x * lv.x) / lv.w, (ps.T.y * lv.y) / lv.w, (ps.T.z * lv.z) / lv.w};
 #else
     lev.put(ps.nlev & ~LEV_LOUD, lv);
     ps.nlev = (ps.nlev + 1) | (quiet_level(lv) ? 0u : LEV_LOUD);
@@ -606,7 +606,7 @@ MRT_DFN void finish_scatter(const DScene& S, PathState& ps, const LevStore<LK>& 
 // are fetched four at a time (one or two cache lines) instead of one dependent load per level
 MRT_DFN f3 fold_level(float4 a, f3 L) {
     if (a.w < 0.0f) return f3{a.x * L.x, a.y * L.y, a.z * L.z};
-    return f3{0.0f + div_x(a.x * L.x, a.w), 0.0f + div_x(a.y * L.y, a.w), 0.0f + div_x(a.z * L.z, a.w)};
+    return f3{0.0f + ((a.x * L.x) / a.w), 0.0f + ((a.y * L.y) / a.w), 0.0f + ((a.z * L.z) / a.w)};
 }
 template <uint32_t LK>
 MRT_DFN f3 fold_levels(const LevStore<LK>& lev, uint32_t nlev, f3 L) {

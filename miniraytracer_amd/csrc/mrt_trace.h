@@ -173,8 +173,6 @@ struct DScene {
     const int32_t* __restrict__ perm;
     const uint8_t* __restrict__ texels;
     const LinOp* __restrict__ prog;  // linear hit program (FT_LIN kernels), mrt_lin.h
-    uint32_t lin_park;               // 1: the program has instance ops the interpreter steps through
-                                     // (they park the query ray in LDS); 0: only one-step box instances
     const mrt_node* __restrict__ bleaf;  // leaves of scene.biased_objects (the list's children, or the object)
     uint32_t nbleaf, blist;              // leaf count; 1 if biased_objects is an object_list
     float nbleaf_f, inv_nbleaf;          // (float)nbleaf and RN(1 / (float)nbleaf), from the host: kernarg
@@ -324,7 +322,7 @@ template <uint32_t F>
 MRT_DFN f3 sphere_center(const mrt_node& n, float time) {
     f3 c0 = ld3(n.f);
     if ((F & FT_MOVING) && (MRT_NODE_FLAGS(n) & MRT_F_MOVING)) {
-        const float s = div_x(time - n.f[6], n.f[7] - n.f[6]);
+        const float s = (time - n.f[6]) / (n.f[7] - n.f[6]);
         const f3 dc = sub(ld3(n.f + 3), c0);
         return f3{madd_det(s, dc.x, c0.x), madd_det(s, dc.y, c0.y), madd_det(s, dc.z, c0.z)};
     }
@@ -372,7 +370,7 @@ MRT_DFN bool rect_hit(const mrt_node& n, const Ray& r, float tmin, float tmax, H
     if (dn > 0.0f) return false;
     float oa = AX == 2 ? r.o.z : AX == 1 ? r.o.y : r.o.x;
     float da = AX == 2 ? r.d.z : AX == 1 ? r.d.y : r.d.x;
-    float t = div_x(n.f[4] - oa, da);
+    float t = (n.f[4] - oa) / da;
     if (t < tmin || t > tmax) return false;
     float ob = AX == 0 ? r.o.y : r.o.x, db = AX == 0 ? r.d.y : r.d.x;
     float oc = AX == 2 ? r.o.y : r.o.z, dc = AX == 2 ? r.d.y : r.d.z;
@@ -382,8 +380,8 @@ MRT_DFN bool rect_hit(const mrt_node& n, const Ray& r, float tmin, float tmax, H
     rec.t = t;
     if (full) {
         if ((F & FT_UV) && (MRT_NODE_FLAGS(n) & MRT_F_NEEDUV)) {
-            rec.u = div_x(pb - n.f[0], n.f[1] - n.f[0]);
-            rec.v = div_x(pc - n.f[2], n.f[3] - n.f[2]);
+            rec.u = (pb - n.f[0]) / (n.f[1] - n.f[0]);
+            rec.v = (pc - n.f[2]) / (n.f[3] - n.f[2]);
         }
         rec.mat = n.mat;
         rec.p = eval(r, t);
@@ -426,7 +424,7 @@ MRT_DFN bool tri_hit(const DScene& S, uint32_t i, const Ray& r, float tmin, floa
 #if MRT_FAST_DIV && defined(__HIP_DEVICE_COMPILE__)
     float invDet = __builtin_amdgcn_rcpf(det);
 #else
-    float invDet = div_x(1.0f, det);
+    float invDet = 1 / det;
 #endif
     float t = (dot(v, qvec) * invDet) * sign;
     const bool ok_t = !((t < tmin) | (t > tmax));
@@ -1110,7 +1108,7 @@ MRT_DFN bool scene_hit(const DScene& S, Ray ray, float tmin0, HitRec& rec, Pcg& 
                     } else {
                         if (t1 < 0) t1 = 0;
                         const float inside_dist = t2 - t1;
-                        const float hit_dist = -div_x(1.0f, N.f[0]) * log_(randf(rng));
+                        const float hit_dist = -(1 / N.f[0]) * log_(randf(rng));
                         ret = hit_dist < inside_dist;
                         if (ret) {
                             rec.t = t1 + hit_dist;
