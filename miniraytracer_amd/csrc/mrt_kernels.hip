@@ -275,26 +275,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
     // work_queue.cpp:158-166).  start(u, v) begins a lane's path at camera coordinates (u, v) with
     // its PCG stream seeded from the path key.
     // path index -> its camera coordinates (u, v) and its PCG stream seeded from the path key
-    auto path_key = [&](uint32_t i, Pcg& rng, float* uo, float* vo) {
-        // i = sl * npix + lp; the double estimate is off by at most one either way
-        uint32_t sl = (uint32_t)((double)i * P.inv_npix);
-        uint32_t lp = i - sl * P.npix;
-        if ((int32_t)lp < 0) { sl--; lp += P.npix; }
-        if (lp >= P.npix) { sl++; lp -= P.npix; }
-        const uint32_t s = P.s0 + sl;
-        const uint2 xy = P.pixels[lp];
-        const uint32_t x = xy.x, y = xy.y;
-        const uint32_t pix = x + y * P.width;
-        const float2 dd = P.sdist[s];  // ((i + 0.5) / sq, (j + 0.5) / sq), s = i*sq + j
-        // (x + dx) / W with RN(1/W) from the host: numerator >= 1/(2 sq) >= 2^-17, W <= 2^24
-        const float nu = (float)x + dd.x, nv = (float)y + dd.y;
-        // exact for every image the host accepts (width, height <= 2^24, mrt_prepare)
-        const float u = div_core(nu, (float)P.width, P.inv_w), v = div_core(nv, (float)P.height, P.inv_h);
-        const uint64_t path_id = (uint64_t)pix * P.ns + s;
-        pcg_seed(rng, splitmix64(P.seed ^ path_id), path_id);
-        *uo = u;
-        *vo = v;
-    };
+    auto path_key = [&](uint32_t i, Pcg& rng, float* uo, float* vo) { path_key_of(P, i, rng, uo, vo); };
     // the next c path indices of the wave's pool, the lane of rank r taking index *i (>= n_paths:
     // none); the pool refilled by one atomic per claim (work_queue::getWork, work_queue.cpp:158-166)
     auto claim = [&](uint32_t c, uint32_t r, bool want, uint64_t* i) {
@@ -706,6 +687,23 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
     if (lane == 0 && my) atomicAdd(P.rays, (unsigned long long)my);
 }
 
+#if MRT_TABLE_PEX
+#include "mrt_wavefront.h"
+#endif
+// the split form (mrt_wavefront.h): the path-exact build's variants with volumes (the plain loop)
+template <uint32_t F>
+static constexpr bool kWfVariant = MRT_TABLE_PEX && kPathExact<F> && (F & FT_VOLUME) != 0;
+template <uint32_t F>
+static constexpr uint32_t kWfWg = MRT_WF_EXT_WG;
+template <uint32_t F>
+static constexpr wf_kernel_t kwf(bool ext) {
+#if MRT_TABLE_PEX
+    if constexpr (kWfVariant<F>) return ext ? mrt_wf_ext<F> : mrt_wf_shade<F>;
+#endif
+    (void)ext;
+    return nullptr;
+}
+
 template <uint32_t F>
 static constexpr path_kernel_t kfn() {
 #if MRT_TABLE_PEX
@@ -729,7 +727,10 @@ static KernelTable make_table(const char* numerics, std::index_sequence<I...>) {
                        {PathQ<kVariants[I]>::words...},
                        {kBox6Walk<kVariants[I]>...},
                        {kMesh4<kVariants[I]>...},
-                       {(uint32_t)(kLinSlabOps<kVariants[I]> && MRT_SIG_OF(kVariants[I]) == SIG_NONE)...}};
+                       {(uint32_t)(kLinSlabOps<kVariants[I]> && MRT_SIG_OF(kVariants[I]) == SIG_NONE)...},
+                       {kwf<kVariants[I]>(true)...},
+                       {kwf<kVariants[I]>(false)...},
+                       {kWfWg<kVariants[I]>...}};
 }
 #if MRT_TABLE_PEX
 const KernelTable& mrtd::kernel_table_fast_pex() {

@@ -47,6 +47,70 @@ struct PathParams {
 
 typedef void (*path_kernel_t)(PathParams);
 
+// path index -> its camera coordinates (u, v) and its PCG stream seeded from the path key
+// (main.cpp:138-149 per (pixel, sample); the stream key of DESIGN.md section 2)
+MRT_DFN void path_key_of(const PathParams& P, uint32_t i, Pcg& rng, float* uo, float* vo) {
+    // i = sl * npix + lp; the double estimate is off by at most one either way
+    uint32_t sl = (uint32_t)((double)i * P.inv_npix);
+    uint32_t lp = i - sl * P.npix;
+    if ((int32_t)lp < 0) { sl--; lp += P.npix; }
+    if (lp >= P.npix) { sl++; lp -= P.npix; }
+    const uint32_t s = P.s0 + sl;
+    const uint2 xy = P.pixels[lp];
+    const uint32_t x = xy.x, y = xy.y;
+    const uint32_t pix = x + y * P.width;
+    const float2 dd = P.sdist[s];  // ((i + 0.5) / sq, (j + 0.5) / sq), s = i*sq + j
+    // (x + dx) / W with RN(1/W) from the host: numerator >= 1/(2 sq) >= 2^-17, W <= 2^24
+    const float nu = (float)x + dd.x, nv = (float)y + dd.y;
+    // exact for every image the host accepts (width, height <= 2^24, mrt_prepare)
+    *uo = div_core(nu, (float)P.width, P.inv_w);
+    *vo = div_core(nv, (float)P.height, P.inv_h);
+    const uint64_t path_id = (uint64_t)pix * P.ns + s;
+    pcg_seed(rng, splitmix64(P.seed ^ path_id), path_id);
+}
+
+// The split ("wavefront") form of the path loop for the bvh_node scenes with volumes (DESIGN.md
+// section 4, "Split kernels"): each path lives in a slot of state arrays in HBM between two
+// kernels that alternate -- mrt_wf_ext<F> runs scene_object::hit for every slot's ray (the walk
+// alone, at the occupancy its registers allow) and mrt_wf_shade<F> runs the rest of trace()'s
+// segment (emission, material::scatter, pdfs), ends paths and starts new ones in the freed slots.
+// Same per-path operations in the same order as the path kernel: the same radiance bit for bit.
+struct WfState {
+    float4* __restrict__ ray0;    // o.xyz, time
+    float4* __restrict__ ray1;    // d.xyz, mask | nice << 8 | inside << 16
+    float4* __restrict__ ray2;    // inv.xyz, depth
+    uint4* __restrict__ rng;      // PCG state, inc
+    float4* __restrict__ thr;     // throughput T.xyz (forward fold)
+    uint32_t* __restrict__ idx;   // path index, MRT_NONE: idle slot
+    float4* __restrict__ hit0;    // t, p.xyz
+    float4* __restrict__ hit1;    // n.xyz, material (MRT_NONE: no hit)
+    float2* __restrict__ hit2;    // u, v
+};
+struct WfParams {
+    PathParams P;
+    WfState W;
+    uint32_t nslots;              // a multiple of 256
+    uint32_t iter;                // iteration of this launch pair
+    uint64_t epoch;               // render-loop serial (the host ignores older h_state words)
+    unsigned long long* __restrict__ cnt;   // MRT_NPART claim counters (paths handed out, relative), MRT_COUNTER_STRIDE apart
+    uint32_t* __restrict__ exh;   // bit k: partition k handed out
+    unsigned long long* __restrict__ ray_acc;  // per 64-slot group: rays of its ended paths
+    uint32_t* __restrict__ gcnt;  // the hit kernel's group claims: MRT_NPART counters, 128 B apart
+    unsigned long long* h_state;  // host-coherent: epoch << 32 | iter | exhausted << 31 (ext kernel, block 0)
+};
+typedef void (*wf_kernel_t)(WfParams);
+// the hit kernel's shape: waves per SIMD it is compiled for, and its workgroup (two groups per CU
+// sharing a treelet each; at 5 waves the book2 walk is spill-free at 96 VGPRs)
+#ifndef MRT_WF_EXT_W
+#define MRT_WF_EXT_W 5
+#endif
+#ifndef MRT_WF_EXT_WG
+#define MRT_WF_EXT_WG (MRT_WF_EXT_W * 128)
+#endif
+#ifndef MRT_WF_CLAIM
+#define MRT_WF_CLAIM 2u  // 64-slot groups a hit-kernel wave claims per atomic
+#endif
+
 // threads per path-kernel workgroup: TreeOf<F>::wg (mrt_trace.h).  One-wave groups by default
 // (each wave owns its own LDS slice; a small group frees its CU slot as soon as its wave finishes,
 // which matters in a launch's tail); the bvh_node kernels run one 16-wave group per CU that
@@ -86,6 +150,9 @@ struct KernelTable {
     uint32_t box6_walk[kNumVariants];  // 1: Cornell shape walked by cornell_fast_hit when op 8 is MRT_F_BOX6
     uint32_t mesh4[kNumVariants];      // 1: the resumable mesh walk two levels at a time (Mesh4, MRT_MESH4)
     uint32_t rewrite[kNumVariants];    // 1: the interpreter runs the rewritten program (mrt_sig.h lin_rewrite_fast)
+    wf_kernel_t wf_ext[kNumVariants];  // split form (WfParams): the hit kernel, or null
+    wf_kernel_t wf_shade[kNumVariants];  // its shade kernel
+    uint32_t wf_ext_wg[kNumVariants];  // threads per hit-kernel workgroup
 };
 const KernelTable& kernel_table_exact();
 const KernelTable& kernel_table_fast();

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <atomic>
 #include <mutex>
+#include <thread>
 
 #include <algorithm>
 #include <functional>
@@ -51,6 +52,9 @@ static void take_variant(KernelTable& m, const KernelTable& s, uint32_t i) {
     m.box6_walk[i] = s.box6_walk[i];
     m.mesh4[i] = s.mesh4[i];
     m.rewrite[i] = s.rewrite[i];
+    m.wf_ext[i] = s.wf_ext[i];
+    m.wf_shade[i] = s.wf_shade[i];
+    m.wf_ext_wg[i] = s.wf_ext_wg[i];
 }
 static const KernelTable& fast_table() {
     static const KernelTable t = [] {
@@ -260,6 +264,11 @@ struct PathLaunch {
     uint32_t lds_save = 0;  // LDS words per lane slot for the query ray parked during instances
     uint32_t lds_mesh = 0;  // LDS words per lane of the mesh walk's stack (binary or two-level walk)
     bool rewrite = false;   // the kernel runs the tolerance-contract program rewrite (s->prog_fast)
+    // the split form (mrt_wavefront.h), where the build has it: hit kernel grid / LDS / treelet
+    wf_kernel_t wf_ext = nullptr, wf_shade = nullptr;
+    int wf_grid = 0;
+    size_t wf_lds = 0;
+    uint32_t wf_wg = 0, wf_tree_n = 0, wf_vgprs = 0;
 };
 
 // Wide nodes renumbered breadth-first over all roots together (level 0 of every tree, then level
@@ -357,6 +366,12 @@ struct mrt_scene {
     uint64_t last_paths = 0;
     uint32_t last_numerics = 0;
     uint32_t prog_ops = 0;  // linear hit program length (0: generic machine)
+    // split-form workspace (mrt_wavefront.h): slot arrays, claim counters, per-group ray words
+    void* d_wf = nullptr;
+    size_t wf_cap = 0;
+    unsigned long long* h_wf = nullptr;  // host-coherent: the hit kernel's iteration / exhaustion word
+    uint64_t wf_epoch = 0;
+    bool last_split = false;  // the last render ran the split form
 };
 
 static mrt_status dev_alloc(mrt_scene* s, void** p, size_t bytes) {
@@ -1075,6 +1090,26 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
             if (*e) nb = std::max(1, atoi(e));
 #endif
         L.grid = prop.multiProcessorCount * nb;
+        if (tabs[k]->wf_ext[s->variant]) {  // the split form: the hit kernel's own occupancy and treelet
+            L.wf_ext = tabs[k]->wf_ext[s->variant];
+            L.wf_shade = tabs[k]->wf_shade[s->variant];
+            L.wf_wg = tabs[k]->wf_ext_wg[s->variant];
+            const uint32_t wwg = L.wf_wg / 64u;
+            L.wf_lds = (size_t)wwg * 64 * 4 * (s->lds_frames * 2 + s->lds_rays * 11 + L.lds_mesh + L.lds_save);
+            hipFuncAttributes wa{};
+            HIPCHK(hipFuncGetAttributes(&wa, reinterpret_cast<const void*>(L.wf_ext)));
+            const int wv = std::max(8, (wa.numRegs + 7) & ~7);
+            int wn = std::max(1, std::min(8, 512 / wv) * 4 / (int)wwg);
+            if (L.wf_lds) wn = std::max(1, std::min<int>(wn, (int)((160u * 1024u) / L.wf_lds)));
+            if (tabs[k]->tree[s->variant]) {
+                const size_t per = std::min<size_t>((160u * 1024u) / wn, (size_t)prop.sharedMemPerBlock);
+                const uint32_t cap = per > L.wf_lds ? (uint32_t)((per - L.wf_lds) / 64u) : 0u;
+                L.wf_tree_n = std::min(cap, (uint32_t)bwide.size());
+                L.wf_lds += (size_t)L.wf_tree_n * 64u;
+            }
+            L.wf_vgprs = (uint32_t)wa.numRegs;
+            L.wf_grid = prop.multiProcessorCount * wn;
+        }
         // every work partition needs waves of its own: a wave leaves its partition only once it is
         // handed out, and visits at most MRT_STEAL_TRIES partitions (mrt_kernels.hip)
         if (L.grid < (int)MRT_NPART) return mrt_internal_fail(MRT_ERR_HIP, "path kernel grid smaller than the work partitions");
@@ -1100,9 +1135,10 @@ extern "C" void mrt_scene_free(mrt_scene* s) {
     if (s->h_one) (void)hipHostFree(s->h_one);
     if (s->h_prev) (void)hipHostFree(s->h_prev);
     if (s->h_seq) (void)hipHostFree(s->h_seq);
+    if (s->h_wf) (void)hipHostFree(s->h_wf);
     if (s->ev_done) (void)hipEventDestroy(s->ev_done);
     for (void* p : {(void*)s->d_counters, (void*)s->d_pixels, (void*)s->d_sdist, (void*)s->d_rad, (void*)s->d_path_rays, (void*)s->d_acc,
-                    (void*)s->d_lev, (void*)s->d_out, (void*)s->d_prev})
+                    (void*)s->d_lev, (void*)s->d_out, (void*)s->d_prev, s->d_wf})
         if (p) (void)hipFree(p);
     delete s;
 }
@@ -1141,6 +1177,103 @@ static mrt_status grow(mrt_scene* s, void** p, size_t* cap, size_t bytes) {
     hipError_t e = hipMalloc(p, bytes ? bytes : 16);
     if (e != hipSuccess) return mrt_internal_fail(MRT_ERR_OOM, "workspace allocation failed");
     *cap = bytes;
+    return MRT_OK;
+}
+
+// the render's ray total from the split form's per-group words
+__global__ void __launch_bounds__(1024) mrt_wf_rays_kernel(unsigned long long* __restrict__ acc, uint32_t n, unsigned long long* __restrict__ rays) {
+    unsigned long long t = 0;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) t += acc[i];
+    for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+    if ((threadIdx.x & 63u) == 0 && t) atomicAdd(rays, t);
+}
+
+// Whether a render runs the split form (mrt_wavefront.h): where the scene's kernel build has it,
+// on MRT_RF_SPLIT; MRT_SPLIT=1 / 0 in the environment turns it on / off for every render (A/B).
+static bool want_split(const PathLaunch& PL, uint32_t flags) {
+    if (!PL.wf_ext) return false;
+    const char* e = getenv("MRT_SPLIT");
+    if (e && *e) return atoi(e) != 0;
+    return (flags & MRT_RF_SPLIT) != 0;
+}
+
+// One launch chunk in the split form: shade / hit kernel pairs over the slot arrays until every
+// path of the chunk has ended.  The host enqueues pairs ahead of the GPU (at most kAhead beyond the
+// iteration the hit kernel last published) until the partitions are handed out; every path then
+// ends within max_bounces + 1 more segments (shade_hit's depth limit), so that many pairs follow.
+static mrt_status wf_run(mrt_scene* s, const PathLaunch& PL, PathParams P, hipStream_t q) {
+    constexpr uint32_t kAhead = 64;
+    P.tree_n = PL.wf_tree_n;
+    uint64_t mult = 16;  // slots per resident hit-kernel lane
+    if (const char* e = getenv("MRT_SPLIT_SLOTS"))  // sweep hook
+        if (*e) mult = std::max(1, atoi(e));
+    const uint64_t want = (uint64_t)PL.wf_grid * PL.wf_wg * mult;
+    const uint64_t need = ((uint64_t)P.n_paths + 255) / 256 * 256;
+    uint32_t ns = (uint32_t)std::max<uint64_t>(256, std::min(want, need));
+    if (const char* e = getenv("MRT_SPLIT_NSLOTS"))  // test hook: this many slots (a multiple of 256)
+        if (*e) ns = std::max(256u, (uint32_t)atoi(e) & ~255u);
+    const size_t cnt_bytes = (size_t)MRT_NPART * MRT_COUNTER_STRIDE * 8 + 128 + MRT_NPART * 128;  // counters, exhaustion mask, group claims
+    const size_t acc_bytes = (size_t)(ns / 64) * 8;
+    const size_t bytes = (size_t)ns * (7 * 16 + 8 + 4) + cnt_bytes + acc_bytes;
+    mrt_status st = grow(s, &s->d_wf, &s->wf_cap, bytes);
+    if (st) return st;
+    if (!s->h_wf) {
+        HIPCHK(hipHostMalloc((void**)&s->h_wf, 64, hipHostMallocPortable | hipHostMallocCoherent));
+        memset(s->h_wf, 0, 64);
+    }
+    char* b = (char*)s->d_wf;
+    WfParams A{};
+    auto take = [&](size_t n) { char* p = b; b += n; return (void*)p; };
+    A.W.ray0 = (float4*)take((size_t)ns * 16);
+    A.W.ray1 = (float4*)take((size_t)ns * 16);
+    A.W.ray2 = (float4*)take((size_t)ns * 16);
+    A.W.rng = (uint4*)take((size_t)ns * 16);
+    A.W.thr = (float4*)take((size_t)ns * 16);
+    A.W.hit0 = (float4*)take((size_t)ns * 16);
+    A.W.hit1 = (float4*)take((size_t)ns * 16);
+    A.W.hit2 = (float2*)take((size_t)ns * 8);
+    A.W.idx = (uint32_t*)take((size_t)ns * 4);
+    A.cnt = (unsigned long long*)take((size_t)MRT_NPART * MRT_COUNTER_STRIDE * 8);
+    A.exh = (uint32_t*)take(128);
+    A.gcnt = (uint32_t*)take(MRT_NPART * 128);
+    A.ray_acc = (unsigned long long*)take(acc_bytes);
+    HIPCHK(hipMemsetAsync(A.W.idx, 0xFF, (size_t)ns * 4, q));  // every slot idle
+    HIPCHK(hipMemsetAsync(A.cnt, 0, cnt_bytes + acc_bytes, q));
+    A.P = P;
+    A.nslots = ns;
+    s->wf_epoch = (s->wf_epoch + 1) & 0xFFFFFFFFull;
+    if (s->wf_epoch == 0) s->wf_epoch = 1;
+    A.epoch = s->wf_epoch;
+    A.h_state = s->h_wf;
+    uint64_t stop_at = ~0ull;
+    uint64_t seen = 0;
+    bool seen_any = false;
+    for (uint64_t it = 0; it < stop_at; it++) {
+        A.iter = (uint32_t)it;
+        hipLaunchKernelGGL(PL.wf_shade, dim3(ns / 256u), dim3(256), 0, q, A);
+        hipLaunchKernelGGL(PL.wf_ext, dim3(PL.wf_grid), dim3(PL.wf_wg), PL.wf_lds, q, A);
+        HIPCHK(hipGetLastError());
+        for (;;) {
+            const uint64_t h = __atomic_load_n(s->h_wf, __ATOMIC_ACQUIRE);
+            if ((h >> 32) == A.epoch) {
+                seen = h & 0x7FFFFFFFull;
+                seen_any = true;
+                if ((h & 0x80000000ull) && stop_at == ~0ull) stop_at = seen + P.max_bounces + 2;
+            }
+            if (stop_at != ~0ull || it + 1 < (seen_any ? seen : 0) + kAhead) break;
+            const hipError_t e = hipStreamQuery(q);
+            if (e != hipSuccess && e != hipErrorNotReady) return mrt_internal_fail(MRT_ERR_HIP, "split render: stream error");
+            if (e == hipSuccess) {  // the stream drained: the last word must be there now
+                const uint64_t h2 = __atomic_load_n(s->h_wf, __ATOMIC_ACQUIRE);
+                if ((h2 >> 32) != A.epoch || (h2 & 0x7FFFFFFFull) < it)
+                    return mrt_internal_fail(MRT_ERR_HIP, "split render: the hit kernel's state word did not arrive");
+                continue;
+            }
+            std::this_thread::yield();
+        }
+    }
+    hipLaunchKernelGGL(mrt_wf_rays_kernel, dim3(1), dim3(1024), 0, q, A.ray_acc, ns / 64u, P.rays);
+    HIPCHK(hipGetLastError());
     return MRT_OK;
 }
 
@@ -1285,6 +1418,8 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
     }
     s->n_launch = 0;
     s->last_numerics = (d->flags & MRT_RF_FAST) ? 1u : 0u;
+    const bool split = want_split(PL, d->flags);
+    s->last_split = split;
     const bool preview = (d->flags & MRT_RF_PREVIEW) != 0;
     uint32_t seq = 0;
     if (preview) {  // a new render: no snapshot yet (sequence 0), in stream order
@@ -1340,8 +1475,12 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.lev = s->d_lev;
         P.lev_rows = s->lev_rows;
         HIPCHK(hipEventRecord(s->ev[2 * s->n_launch], q));
-        hipLaunchKernelGGL(PL.fn, dim3(PL.grid), dim3(PL.wg), PL.lds_bytes, q, P);
-        HIPCHK(hipGetLastError());
+        if (split) {
+            if ((st = wf_run(s, PL, P, q))) return st;
+        } else {
+            hipLaunchKernelGGL(PL.fn, dim3(PL.grid), dim3(PL.wg), PL.lds_bytes, q, P);
+            HIPCHK(hipGetLastError());
+        }
         HIPCHK(hipEventRecord(s->ev[2 * s->n_launch + 1], q));
         s->n_launch++;
         // the last chunk's full fold finishes the render (no preview: no snapshot of acc needed;
@@ -1531,6 +1670,11 @@ extern "C" mrt_status mrt_scene_kernel_info(const mrt_scene* s, mrt_kernel_info*
                : L.fn == kernel_table_fast_pex().kernel[s->variant] ? MRT_BUILD_PATH_EXACT
                : L.fn == kernel_table_fast_ftz().kernel[s->variant] ? MRT_BUILD_FAST_FTZ
                                                                      : MRT_BUILD_FAST;
+    out->split = s->last_split ? 1u : 0u;
+    out->split_vgprs = L.wf_vgprs;
+    out->split_grid = (uint32_t)L.wf_grid;
+    out->split_wg = L.wf_wg;
+    out->split_tree_nodes = L.wf_tree_n;
     return MRT_OK;
 }
 

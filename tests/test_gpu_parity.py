@@ -193,6 +193,35 @@ def test_tolerance_contract_builds(gpu):
         assert gpu._lib.BUILDS[r.kernel_info()["build"]] == "exact", sid
 
 
+@pytest.mark.parametrize("sid,w,h,spp,mode", [(7, 64, 64, 16, 0), (6, 48, 48, 9, 0), (7, 40, 40, 4, 1)])
+def test_split_kernels_equal_path_kernel(gpu, sid, w, h, spp, mode, monkeypatch):
+    """The split form (MRT_RF_SPLIT: alternating hit / shade kernels, path state in HBM slots,
+    mrt_wavefront.h) of the volume scenes' path-exact kernels: the same radiance and ray count per
+    path, the same image, as the persistent path kernel (few slots per path here, so slots are
+    reused many times and the pool runs dry mid-render)."""
+    sc = gpu.select_scene(sid, w / h)
+    r = gpu.Renderer(sc, 0)
+    n = w * h * (int(spp ** 0.5) ** 2)
+    d = gpu.render_desc(w, h, spp, mode=mode, numerics="fast", flags=gpu._lib.RF_PATH_DEBUG)
+    a, ra = r.render(d)
+    pa = r.paths(n)
+    assert r.kernel_info()["split"] == 0
+    monkeypatch.setenv("MRT_SPLIT_NSLOTS", "2048")
+    ds = gpu.render_desc(w, h, spp, mode=mode, numerics="fast", flags=gpu._lib.RF_PATH_DEBUG, split=True)
+    b, rb = r.render(ds)
+    pb = r.paths(n)
+    info = r.kernel_info()
+    assert info["split"] == 1 and info["split_grid"] > 0, info
+    assert ra == rb
+    assert np.array_equal(pa[1], pb[1])
+    assert np.array_equal(pa[0].view(np.uint32), pb[0].view(np.uint32))
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    # scenes without the split form ignore the flag
+    c = gpu.Renderer(gpu.select_scene(5, 1.0), 0)
+    c.render(gpu.render_desc(16, 16, 1, numerics="fast", split=True))
+    assert c.kernel_info()["split"] == 0
+
+
 @pytest.mark.parametrize("sid,w,h,spp", [(5, 64, 64, 16), (9, 40, 40, 9), (8, 40, 40, 9)])
 def test_shape_specialised_walk_equals_interpreter(gpu, sid, w, h, spp, monkeypatch):
     """Reference scenes whose linear program has a known shape (mrt_sig.h) run a walk unrolled at
