@@ -12,8 +12,9 @@ for r in $(seq 1 "${ROUNDS:-2}"); do
     for cfg in $CFGS; do
       IFS=, read sid W H S <<< "$cfg"
       lib=""; sp=1
-      case "$tag" in base) sp=0 ;; intree) ;; *) lib="exp/libmrt_$tag.so" ;; esac
-      log=gpurun_out/split_${tag}${SFX:-}_${sid}_$r.log
+      # (<lib>:0 -- that library's persistent path kernel, MRT_SPLIT=0)
+      case "$tag" in base) sp=0 ;; intree) ;; *:0) lib="exp/libmrt_${tag%:0}.so"; sp=0 ;; *) lib="exp/libmrt_$tag.so" ;; esac
+      log=gpurun_out/split_${tag/:/-}${SFX:-}_${sid}_$r.log
       MRT_SPLIT=$sp MRT_EXPERIMENT_LIB=$lib timeout -k 10 300 python bench.py --no-cpu-baseline --no-compare-numerics --no-other-walk \
           --no-parity --steps "$STEPS" --warmup 1 --scene "$sid" --width "$W" --height "$H" --samples "$S" ${BENCH_ARGS:-} > "$log" 2>&1 || exit 3
       python tools/show_bench.py "$log" "$tag${SFX:-} split=$sp scene $sid round $r"
