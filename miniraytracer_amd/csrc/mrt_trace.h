@@ -238,6 +238,12 @@ struct LStack {
 #ifndef MRT_TREE_WG
 #define MRT_TREE_WG (MRT_FAST ? 768 : 1024)  // the exact contract's kernels keep 1 x 16 waves (no A/B there)
 #endif
+// the tolerance contract's sky-lit bvh_node kernels (scenes 0-4): six 4-wave groups per CU, each
+// with its own smaller treelet (random spheres +10% per step against 2 x 12 waves; book2, the
+// volume variant, keeps 2 x 12: 3 x 8 -25%, 6 x 4 -12%; profiles/r04_ab.txt section 10)
+#ifndef MRT_TREE_WG_SKY
+#define MRT_TREE_WG_SKY (MRT_FAST ? 256 : MRT_TREE_WG)
+#endif
 template <uint32_t F>
 struct TreeOf {
     // the kernels of bvh_node scenes (wide-node walks); the same test as PathOcc::kWide
@@ -245,7 +251,7 @@ struct TreeOf {
                                ((F & (FT_BVHW | FT_TEX | FT_VOLUME)) != 0 || !(F & FT_LIN));
     // threads per path-kernel workgroup (the generic machine, no linear program, keeps 1 x 16
     // waves: at 6 waves per SIMD it spills)
-    static constexpr uint32_t wg = !on ? 64u : (F & FT_LIN) ? (uint32_t)(MRT_TREE_WG) : 1024u;
+    static constexpr uint32_t wg = !on ? 64u : !(F & FT_LIN) ? 1024u : (F & FT_VOLUME) ? (uint32_t)(MRT_TREE_WG) : (uint32_t)(MRT_TREE_WG_SKY);
 };
 // A treelet node through LDS instructions (ds_read_b128: LDS latency, lgkmcnt only), instead of
 // the flat load that can reach LDS or memory per lane (a flat access waits on both counters)
