@@ -372,6 +372,9 @@ struct mrt_scene {
     unsigned long long* h_wf = nullptr;  // host-coherent: the hit kernel's iteration / exhaustion word
     uint64_t wf_epoch = 0;
     bool last_split = false;  // the last render ran the split form
+    // mrt_render's cancel flag while its split render enqueues (wf_run forwards it to the device flag)
+    const volatile int* host_cancel = nullptr;
+    bool wf_cancelled = false;
 };
 
 static mrt_status dev_alloc(mrt_scene* s, void** p, size_t bytes) {
@@ -1260,6 +1263,11 @@ static mrt_status wf_run(mrt_scene* s, const PathLaunch& PL, PathParams P, hipSt
                 seen_any = true;
                 if ((h & 0x80000000ull) && stop_at == ~0ull) stop_at = seen + P.max_bounces + 2;
             }
+            if (s->host_cancel && *s->host_cancel && !s->wf_cancelled) {  // G_isRunning: stop handing out paths
+                HIPCHK(hipMemcpyAsync(s->d_counter + 4, s->h_one, sizeof(int), hipMemcpyHostToDevice, s->pstream));
+                HIPCHK(hipStreamSynchronize(s->pstream));
+                s->wf_cancelled = true;
+            }
             if (stop_at != ~0ull || it + 1 < (seen_any ? seen : 0) + kAhead) break;
             const hipError_t e = hipStreamQuery(q);
             if (e != hipSuccess && e != hipErrorNotReady) return mrt_internal_fail(MRT_ERR_HIP, "split render: stream error");
@@ -1477,12 +1485,18 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         HIPCHK(hipEventRecord(s->ev[2 * s->n_launch], q));
         if (split) {
             if ((st = wf_run(s, PL, P, q))) return st;
+            // progress (mrt_progress) counts this chunk once its events are enqueued: publish now, the
+            // next chunk's loop only starts when this one's work is handed out
+            std::lock_guard<std::mutex> lk(s->prog_mu);
+            HIPCHK(hipEventRecord(s->ev[2 * s->n_launch + 1], q));
+            s->n_launch++;
+            s->n_chunks.store(s->n_launch, std::memory_order_release);
         } else {
             hipLaunchKernelGGL(PL.fn, dim3(PL.grid), dim3(PL.wg), PL.lds_bytes, q, P);
             HIPCHK(hipGetLastError());
+            HIPCHK(hipEventRecord(s->ev[2 * s->n_launch + 1], q));
+            s->n_launch++;
         }
-        HIPCHK(hipEventRecord(s->ev[2 * s->n_launch + 1], q));
-        s->n_launch++;
         // the last chunk's full fold finishes the render (no preview: no snapshot of acc needed;
         // the 8-VGPR lean fold cannot take the division as well: a final kernel follows it)
         const bool lean = (d->flags & MRT_RF_FOLD_BEHIND) && d->mode == 0;
@@ -1537,9 +1551,13 @@ extern "C" mrt_status mrt_render(mrt_scene* s, const mrt_render_desc* d, float* 
     mrt_status st = mrt_prepare(s, d);
     if (st) return st;
     HIPCHK(hipMemset(s->d_rays, 0, 8));
-    if ((st = mrt_render_device(s, d, (float*)s->d_out, (uint64_t*)s->d_rays, nullptr))) return st;
+    s->host_cancel = cancel;  // (a split render polls it while it enqueues)
+    s->wf_cancelled = false;
+    st = mrt_render_device(s, d, (float*)s->d_out, (uint64_t*)s->d_rays, nullptr);
+    s->host_cancel = nullptr;
+    if (st) return st;
     // wait, forwarding the caller's cancel flag to the device flag the path kernel polls
-    bool cancelled = false;
+    bool cancelled = s->wf_cancelled;
     if (!cancel) {
         HIPCHK(hipEventSynchronize(s->ev_done));
     } else {

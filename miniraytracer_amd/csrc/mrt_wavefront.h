@@ -124,7 +124,8 @@ __global__ void __launch_bounds__(MRT_WF_EXT_WG) __attribute__((amdgpu_waves_per
         // the shade kernel of this iteration has finished (stream order): publish whether every
         // partition is handed out, and the progress snapshots (mrt_progress)
         const uint32_t e = __hip_atomic_load(A.exh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const bool all = e == (1u << MRT_NPART) - 1u;
+        // (a cancelled render hands out nothing more: its loop ends as if the partitions were done)
+        const bool all = e == (1u << MRT_NPART) - 1u || __hip_atomic_load(P.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
         if (P.hprog)
             for (uint32_t k = 0; k < MRT_NPART; k++) {
                 const uint64_t len = P.part_base[k + 1] - P.part_base[k];

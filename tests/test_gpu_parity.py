@@ -222,6 +222,37 @@ def test_split_kernels_equal_path_kernel(gpu, sid, w, h, spp, mode, monkeypatch)
     assert c.kernel_info()["split"] == 0
 
 
+def test_split_render_cancel_and_progress(gpu):
+    """A split render (MRT_RF_SPLIT) honours the cancel flag while its host loop enqueues (the flag
+    reaches the device, no path is handed out after it, the loop ends) and reports progress as its
+    chunks are handed out; the next split render is unaffected (bit-identical)."""
+    import ctypes
+    import threading
+    sc = gpu.select_scene(7, 1.0)
+    r = gpu.Renderer(sc, 0)
+    d = gpu.render_desc(32, 32, 16, numerics="fast", split=True)
+    a, ra = r.render(d)
+    flag = ctypes.c_int(0)
+    err = []
+
+    def run():
+        try:
+            r.render(gpu.render_desc(128, 128, 256 * 256, numerics="fast", split=True), cancel=flag)
+        except gpu.MrtError as e:
+            err.append(e)
+
+    t = threading.Thread(target=run)
+    t.start()
+    while t.is_alive() and r.progress() <= 0.0:
+        pass
+    flag.value = 1
+    t.join()
+    assert err and "cancel" in str(err[0]).lower()
+    b, rb = r.render(d)
+    assert r.kernel_info()["split"] == 1
+    assert ra == rb and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
 @pytest.mark.parametrize("sid,w,h,spp", [(5, 64, 64, 16), (9, 40, 40, 9), (8, 40, 40, 9)])
 def test_shape_specialised_walk_equals_interpreter(gpu, sid, w, h, spp, monkeypatch):
     """Reference scenes whose linear program has a known shape (mrt_sig.h) run a walk unrolled at
