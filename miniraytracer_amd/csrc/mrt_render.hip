@@ -264,6 +264,7 @@ struct PathLaunch {
     uint32_t lds_save = 0;  // LDS words per lane slot for the query ray parked during instances
     uint32_t lds_mesh = 0;  // LDS words per lane of the mesh walk's stack (binary or two-level walk)
     bool rewrite = false;   // the kernel runs the tolerance-contract program rewrite (s->prog_fast)
+    uint32_t walk_min = 32;  // resumable mesh walk threshold of this build (PathParams::walk_min)
     // the split form (mrt_wavefront.h), where the build has it: hit kernel grid / LDS / treelet
     wf_kernel_t wf_ext = nullptr, wf_shade = nullptr;
     int wf_grid = 0;
@@ -1041,8 +1042,12 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     s->lds_save = (lin_kernel && (kVariants[s->variant] & FT_INST)) ? 15u : 0u;
     // resumable mesh walk: deeper pod_bvh trees keep the wave walking longer
     s->walk_min = T.wide.size() >= 2048 ? 40u : 32u;  // inner nodes: bunny 2937, teapot ~1045
+    bool walk_min_env = false;
     if (const char* e = getenv("MRT_WALK_MIN"))  // sweep hook (tools/ab_walk.sh)
-        if (*e) s->walk_min = (uint32_t)atoi(e);
+        if (*e) {
+            s->walk_min = (uint32_t)atoi(e);
+            walk_min_env = true;
+        }
     const std::vector<BvhWide>& bwide = T.bwide;
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
@@ -1060,6 +1065,9 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
         L.lds_save = tabs[k]->box6_walk[s->variant] ? 0u : s->lds_save;
         L.lds_mesh = tabs[k]->mesh4[s->variant] ? std::max(s->lds_mesh, (uint32_t)T.max_mesh4) : s->lds_mesh;
         L.rewrite = tabs[k]->rewrite[s->variant] != 0;
+        // the path-exact build (the metal bunny under the tolerance contract) yields at 32 walking
+        // lanes: 40 -1.2%, 28 -1.7%, 48 -10% (bunny 1024x1024x64, profiles/r04_ab.txt section 13)
+        L.walk_min = (!walk_min_env && L.fn == kernel_table_fast_pex().kernel[s->variant]) ? 32u : s->walk_min;
         L.lds_bytes = (size_t)waves_per_wg * 64 * 4 *
                       (s->lds_frames * 2 + s->lds_rays * 11 + L.lds_mesh + L.lds_save + tabs[k]->lev_k[s->variant] * 4 +
                        tabs[k]->pq[s->variant]);
@@ -1447,7 +1455,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.lds_rays = s->lds_rays;
         P.lds_mesh = PL.lds_mesh;
         P.lds_save = PL.lds_save;
-        P.walk_min = s->walk_min;
+        P.walk_min = PL.walk_min;
         P.tree_src = reinterpret_cast<const float4*>(s->S.bwide);
         P.tree_n = PL.tree_n;
         P.pixels = s->d_pixels;
