@@ -1212,26 +1212,39 @@ static bool want_split(const PathLaunch& PL, uint32_t flags) {
 // path of the chunk has ended.  The host enqueues pairs ahead of the GPU (at most kAhead beyond the
 // iteration the hit kernel last published) until the partitions are handed out; every path then
 // ends within max_bounces + 1 more segments (shade_hit's depth limit), so that many pairs follow.
-static mrt_status wf_run(mrt_scene* s, const PathLaunch& PL, PathParams P, hipStream_t q) {
-    constexpr uint32_t kAhead = 64;
-    P.tree_n = PL.wf_tree_n;
+// slots of a split launch of n_paths paths and the workspace bytes they take
+static uint32_t wf_slots(const PathLaunch& PL, uint64_t n_paths) {
     uint64_t mult = 16;  // slots per resident hit-kernel lane
     if (const char* e = getenv("MRT_SPLIT_SLOTS"))  // sweep hook
         if (*e) mult = std::max(1, atoi(e));
     const uint64_t want = (uint64_t)PL.wf_grid * PL.wf_wg * mult;
-    const uint64_t need = ((uint64_t)P.n_paths + 255) / 256 * 256;
+    const uint64_t need = (n_paths + 255) / 256 * 256;
     uint32_t ns = (uint32_t)std::max<uint64_t>(256, std::min(want, need));
     if (const char* e = getenv("MRT_SPLIT_NSLOTS"))  // test hook: this many slots (a multiple of 256)
         if (*e) ns = std::max(256u, (uint32_t)atoi(e) & ~255u);
-    const size_t cnt_bytes = (size_t)MRT_NPART * MRT_COUNTER_STRIDE * 8 + 128 + MRT_NPART * 128;  // counters, exhaustion mask, group claims
-    const size_t acc_bytes = (size_t)(ns / 64) * 8;
-    const size_t bytes = (size_t)ns * (7 * 16 + 8 + 4) + cnt_bytes + acc_bytes;
-    mrt_status st = grow(s, &s->d_wf, &s->wf_cap, bytes);
+    return ns;
+}
+static constexpr size_t kWfCntBytes = (size_t)MRT_NPART * MRT_COUNTER_STRIDE * 8 + 128 + MRT_NPART * 128;  // counters, exhaustion mask, group claims
+static size_t wf_bytes(uint32_t ns) { return (size_t)ns * (7 * 16 + 8 + 4) + kWfCntBytes + (size_t)(ns / 64) * 8; }
+// the split workspace for a launch of n_paths (mrt_prepare sizes it, so a render allocates nothing)
+static mrt_status wf_reserve(mrt_scene* s, const PathLaunch& PL, uint64_t n_paths) {
+    mrt_status st = grow(s, &s->d_wf, &s->wf_cap, wf_bytes(wf_slots(PL, n_paths)));
     if (st) return st;
     if (!s->h_wf) {
         HIPCHK(hipHostMalloc((void**)&s->h_wf, 64, hipHostMallocPortable | hipHostMallocCoherent));
         memset(s->h_wf, 0, 64);
     }
+    return MRT_OK;
+}
+
+static mrt_status wf_run(mrt_scene* s, const PathLaunch& PL, PathParams P, hipStream_t q) {
+    constexpr uint32_t kAhead = 64;
+    P.tree_n = PL.wf_tree_n;
+    const uint32_t ns = wf_slots(PL, P.n_paths);
+    const size_t cnt_bytes = kWfCntBytes;
+    const size_t acc_bytes = (size_t)(ns / 64) * 8;
+    mrt_status st = wf_reserve(s, PL, P.n_paths);
+    if (st) return st;
     char* b = (char*)s->d_wf;
     WfParams A{};
     auto take = [&](size_t n) { char* p = b; b += n; return (void*)p; };
@@ -1366,6 +1379,10 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
     }
     if (d->flags & MRT_RF_PATH_DEBUG)
         if ((st = grow(s, (void**)&s->d_path_rays, &s->pr_cap, paths * 4))) return st;
+    {  // the split form's slot arrays (MRT_RF_SPLIT on a scene whose build has it)
+        const PathLaunch& PL = s->pl[(d->flags & MRT_RF_FAST) ? 1 : 0];
+        if (want_split(PL, d->flags) && (st = wf_reserve(s, PL, paths))) return st;
+    }
     s->lev_rows = std::max<uint32_t>(d->max_bounces, 1);
     if ((st = grow(s, (void**)&s->d_lev, &s->lev_cap, (size_t)s->lev_rows * s->max_threads * 16))) return st;
     uint32_t launches = (ns + s->chunk - 1) / s->chunk;
