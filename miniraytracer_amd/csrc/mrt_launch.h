@@ -102,8 +102,8 @@ typedef void (*wf_kernel_t)(WfParams);
 // the hit kernel's shape: waves per SIMD it is compiled for, and its workgroup (two groups per CU
 // sharing a treelet each, a multiple of 4 waves so both groups' waves spread evenly over the 4 SIMDs).
 // Measured on book2 (profiles/r04_split_ab.txt): 6 waves (80 VGPRs) best; at 5 the walk is
-// spill-free (96 VGPRs) but slower in 2 x 8 or 5 x 4 groups, and 2 x 10 waves do not fit a CU
-// together (3+3+2+2 waves per group).
+// spill-free (96 VGPRs) but slower in 2 x 8 or 5 x 4 groups, and slower still in 2 x 10 (3+3+2+2
+// waves per group: most likely the two groups are not resident together).
 #ifndef MRT_WF_EXT_W
 #define MRT_WF_EXT_W 6
 #endif
