@@ -89,7 +89,9 @@ static uint32_t pick_variant(uint32_t features) {
 // The sum is sequential per pixel (bit-exact order), so the kernel is load-latency bound when
 // few pixels are local (multi-GPU shards): samples are fetched FOLD_DEPTH at a time (coalesced
 // across the wave's pixels) before the dependent adds.
+#ifndef FOLD_DEPTH
 #define FOLD_DEPTH 16
+#endif
 // The render's last chunk (out != null) also finishes the pixels -- final_pixel into the caller's
 // output -- and resets the counters (FoldEnd), so no separate final kernel follows it.
 struct FoldEnd {
