@@ -475,6 +475,21 @@ def test_own_spp_within_tolerance_of_shipped_reference(gpu, sid, numerics):
     assert abs(c["ray_ratio"] - 1) < FULL_RAYS[numerics], c
 
 
+def test_own_spp_split_form_c5(gpu):
+    """C5 (book2 2048x2048 at 8192 spp) in the split form (MRT_RF_SPLIT) on the shipped reference's
+    own-spp pixel list: the same image as the persistent kernel, bit for bit, at the same bar."""
+    from fixture_cmp import compare_pixels
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "shipped_ownspp_7.npz"))
+    _, w, h, spp, depth = (int(x) for x in g["meta"])
+    _, r = renderer(gpu, 7, w, h)
+    a, ra = r.render(gpu.render_desc(w, h, spp, depth=depth, numerics="fast", pixels=g["pixels"]))
+    b, rb = r.render(gpu.render_desc(w, h, spp, depth=depth, numerics="fast", pixels=g["pixels"], split=True))
+    assert r.kernel_info()["split"] == 1
+    assert ra == rb and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    c = compare_pixels(b, rb, g)
+    assert c["rmse"] < 1e-3 and abs(c["ray_ratio"] - 1) < FULL_RAYS["fast"], c
+
+
 def test_concurrent_contexts_on_two_streams(gpu):
     """bench.py --pipeline: render contexts of the same scene on two HIP streams, launched back to
     back without ordering, share one device ray counter (atomics) and overlap on the CUs; each
