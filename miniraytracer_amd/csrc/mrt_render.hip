@@ -1279,7 +1279,7 @@ static mrt_status wf_run(mrt_scene* s, const PathLaunch& PL, PathParams P, hipSt
         hipLaunchKernelGGL(PL.wf_shade, dim3(ns / 256u), dim3(256), 0, q, A);
         hipLaunchKernelGGL(PL.wf_ext, dim3(PL.wf_grid), dim3(PL.wf_wg), PL.wf_lds, q, A);
         HIPCHK(hipGetLastError());
-        for (;;) {
+        for (uint32_t polls = 0;; polls++) {
             const uint64_t h = __atomic_load_n(s->h_wf, __ATOMIC_ACQUIRE);
             if ((h >> 32) == A.epoch) {
                 seen = h & 0x7FFFFFFFull;
@@ -1300,7 +1300,10 @@ static mrt_status wf_run(mrt_scene* s, const PathLaunch& PL, PathParams P, hipSt
                     return mrt_internal_fail(MRT_ERR_HIP, "split render: the hit kernel's state word did not arrive");
                 continue;
             }
-            std::this_thread::yield();
+            // the GPU is kAhead launch pairs behind: yield at first, then sleep (a long render's host
+            // thread does not spin a core for its whole duration)
+            if (polls < 64) std::this_thread::yield();
+            else usleep(50);
         }
     }
     hipLaunchKernelGGL(mrt_wf_rays_kernel, dim3(1), dim3(1024), 0, q, A.ray_acc, ns / 64u, P.rays);
