@@ -178,9 +178,12 @@ const KernelTable& kernel_table_fast();
 #ifndef MRT_PATH_EXACT
 #define MRT_PATH_EXACT 1
 #endif
+#ifndef MRT_PEX_ALL_MESH
+#define MRT_PEX_ALL_MESH 0  // A/B hook: every room + mesh variant path-exact (the teapot, C3, too)
+#endif
 template <uint32_t F>
 static constexpr bool kPathExact =
-    MRT_PATH_EXACT && ((F & FT_VOLUME) != 0 || (MRT_SIG_OF(F) == SIG_ROOM_MESH && (F & FT_METAL) != 0));
+    MRT_PATH_EXACT && ((F & FT_VOLUME) != 0 || (MRT_SIG_OF(F) == SIG_ROOM_MESH && ((F & FT_METAL) != 0 || MRT_PEX_ALL_MESH)));
 template <uint32_t F>
 static constexpr bool kFtzVariant = MRT_FAST_FTZ && (F & FT_VOLUME) == 0 && !kPathExact<F>;
 // the FTZ build's table: a kernel for the kFtzVariant variants, null for the others
