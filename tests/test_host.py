@@ -87,6 +87,17 @@ def test_render_flags_match_header(mrt):
         assert getattr(mrt._lib, "RF_" + name) == v, name
 
 
+def test_kernel_info_layout_matches_header(mrt):
+    """The ctypes mirror of mrt_kernel_info has the header's fields, in order (all uint32_t): a
+    field added on one side only would shift every later one."""
+    hdr = open(os.path.join(os.path.dirname(__file__), "..", "include", "mrt.h")).read()
+    body = re.search(r"typedef struct mrt_kernel_info \{(.*?)\} mrt_kernel_info;", hdr, re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    names = [n.strip() for decl in body.split(";") if decl.strip() for n in decl.replace("uint32_t", "").split(",")]
+    assert [f for f, _ in mrt._lib.KernelInfo._fields_] == names
+    assert all(t is __import__("ctypes").c_uint32 for _, t in mrt._lib.KernelInfo._fields_)
+
+
 def reference_tiles(W, H, ts):
     """work_queue::work_queue (work_queue.cpp:64-128), restated in numpy-free Python."""
     xc, yc = (W + ts - 1) // ts, (H + ts - 1) // ts
