@@ -87,6 +87,33 @@ def test_render_flags_match_header(mrt):
         assert getattr(mrt._lib, "RF_" + name) == v, name
 
 
+def header_struct(name):
+    """(field, C type) of `typedef struct <name> {...} <name>;` in include/mrt.h, comments dropped."""
+    hdr = open(os.path.join(os.path.dirname(__file__), "..", "include", "mrt.h")).read()
+    body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (name, name), hdr, re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    out = []
+    for decl in body.split(";"):
+        decl = " ".join(decl.split())
+        if not decl:
+            continue
+        m = re.match(r"(const )?(uint32_t|uint64_t|float)(\s*\*)?\s+(.*)", decl)
+        ctype = "ptr" if m.group(3) else m.group(2)
+        out += [(n.strip(), ctype) for n in m.group(4).split(",")]
+    return out
+
+
+@pytest.mark.parametrize("cname,pyname", [("mrt_render_desc", "MrtRenderDesc"), ("mrt_params", "MrtParams")])
+def test_abi_structs_match_header(mrt, cname, pyname):
+    """The ctypes mirrors of the C-ABI's argument structs have the header's fields, in order, with
+    the same types (a field added on one side only would shift every later one)."""
+    want = {"uint32_t": ctypes.c_uint32, "uint64_t": ctypes.c_uint64, "float": ctypes.c_float, "ptr": ctypes.c_void_p}
+    fields = getattr(mrt._lib, pyname)._fields_
+    assert [f for f, _ in fields] == [n for n, _ in header_struct(cname)]
+    for (f, t), (_, ct) in zip(fields, header_struct(cname)):
+        assert t is want[ct], f
+
+
 def test_kernel_info_layout_matches_header(mrt):
     """The ctypes mirror of mrt_kernel_info has the header's fields, in order (all uint32_t): a
     field added on one side only would shift every later one."""
