@@ -140,12 +140,6 @@ typedef struct mrt_render_desc {
                                    work_queue.cpp:133-166).  One thread reproduces the reference's
                                    -threads 1 run bit for bit (its deterministic mode,
                                    cmdline_parser.h:15); world must be 1 */
-#define MRT_RF_SPLIT 0x20u      /* GPU: run the path loop as alternating hit / shade kernels with the
-                                   path state in HBM ("Split kernels"), where the
-                                   scene's kernel build has that form (the path-exact volume scenes,
-                                   C5); the same radiance bit for bit.  mrt_render_device then waits
-                                   on the host for the render's last launches to be enqueued (not
-                                   capturable).  Ignored elsewhere. */
 
 void mrt_default_render_desc(const mrt_params* p, mrt_render_desc* d);
 
@@ -190,9 +184,6 @@ mrt_status mrt_kernel_ms(mrt_scene* s, float* path_ms, uint32_t* launches);
 #define MRT_BUILD_PATH_EXACT 3u
 typedef struct mrt_kernel_info {
     uint32_t features, kernel_features, lds_bytes, grid, prog_ops, vgprs, wg, tree_nodes, build;
-    /* split: 1 when the last render ran the split form (MRT_RF_SPLIT); split_vgprs / split_grid /
-       split_wg / split_tree_nodes: its hit kernel (0 when the scene's build has no split form) */
-    uint32_t split, split_vgprs, split_grid, split_wg, split_tree_nodes;
 } mrt_kernel_info;
 mrt_status mrt_scene_kernel_info(const mrt_scene* s, mrt_kernel_info* out);
 

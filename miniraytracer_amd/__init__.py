@@ -91,14 +91,13 @@ NUMERICS = ("exact", "fast")
 
 def render_desc(width, height, samples, depth=32, max_luminance=1000.0, mode=0, seed=MAIN_SEED, tile_size=32,
                 rank=0, world=1, chunk_samples=0, flags=0, numerics="exact", threads=0, preview=False, ref_order=False,
-                pixels=None, split=False):
+                pixels=None):
     """Render description; `samples` is floored to a perfect square like main.cpp:319-320.
     numerics: "exact" (bit-for-bit the reference built exact) or "fast" (tolerance contract:
     per-pixel RMSE < 1e-3 vs the reference as shipped; MRT_RF_FAST).  ref_order (CPU backend): the
     reference's own RNG order, one stream per worker thread (Renderer.set_worker_seeds).
     pixels: optional row-major pixel indices to render instead of the rank's tiles (the desc keeps
-    a reference to the array; mrt_render_desc.pixels).  split (GPU): the path loop as alternating hit /
-    shade kernels where the scene's kernel build has that form (MRT_RF_SPLIT; same radiance)."""
+    a reference to the array; mrt_render_desc.pixels)."""
     if numerics not in NUMERICS:
         raise ValueError(f"numerics must be one of {NUMERICS}")
     if numerics == "fast":
@@ -107,8 +106,6 @@ def render_desc(width, height, samples, depth=32, max_luminance=1000.0, mode=0, 
         flags |= _lib.RF_PREVIEW
     if ref_order:
         flags |= _lib.RF_REF_ORDER
-    if split:
-        flags |= _lib.RF_SPLIT
     sq = int(np.sqrt(np.float32(samples)))
     d = MrtRenderDesc(width, height, sq, depth, max_luminance, mode, seed, tile_size, rank, world,
                       chunk_samples, flags, threads)

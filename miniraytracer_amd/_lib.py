@@ -19,7 +19,6 @@ RF_FAST = 0x2  # tolerance numerics contract (include/mrt.h MRT_RF_FAST)
 RF_PREVIEW = 0x4  # keep a progressive preview for mrt_preview (include/mrt.h MRT_RF_PREVIEW)
 RF_FOLD_BEHIND = 0x8  # mode-0 fold that runs beside another context's path kernel (include/mrt.h)
 RF_REF_ORDER = 0x10  # CPU backend: the reference's own RNG order (worker streams, work_queue order)
-RF_SPLIT = 0x20  # GPU: alternating hit / shade kernels (path state in HBM) where the scene's build has them
 DEVICE_CPU = -1  # mrt_scene_upload device of the CPU backend (include/mrt.h MRT_DEVICE_CPU)
 
 
@@ -63,8 +62,7 @@ class MrtSceneView(C.Structure):
 class KernelInfo(C.Structure):
     _fields_ = [("features", C.c_uint32), ("kernel_features", C.c_uint32), ("lds_bytes", C.c_uint32),
                 ("grid", C.c_uint32), ("prog_ops", C.c_uint32), ("vgprs", C.c_uint32), ("wg", C.c_uint32),
-                ("tree_nodes", C.c_uint32), ("build", C.c_uint32), ("split", C.c_uint32), ("split_vgprs", C.c_uint32),
-                ("split_grid", C.c_uint32), ("split_wg", C.c_uint32), ("split_tree_nodes", C.c_uint32)]
+                ("tree_nodes", C.c_uint32), ("build", C.c_uint32)]
 BUILDS = ("exact", "fast", "fastz", "pex")  # MRT_BUILD_*: the kernel build (mrt_path_kernel[_fast|_fastz|_pex])
 
 

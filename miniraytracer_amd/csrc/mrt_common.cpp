@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -308,12 +309,17 @@ mrt_status mrt_internal_check_pixels(const mrt_render_desc* d) {
     if (!d->pixels) return MRT_OK;
     if (d->n_pixels == 0) return mrt_internal_fail(MRT_ERR_INVALID, "render desc: empty pixel list");
     const uint64_t wh = (uint64_t)d->width * d->height;
-    std::vector<bool> seen(wh, false);
-    for (uint32_t i = 0; i < d->n_pixels; i++) {
-        const uint32_t p = d->pixels[i];
-        if (p >= wh) return mrt_internal_fail(MRT_ERR_INVALID, "render desc: pixel index outside the image");
-        if (seen[p]) return mrt_internal_fail(MRT_ERR_INVALID, "render desc: pixel listed twice");
-        seen[p] = true;
+    // pixel indices are 32-bit: a pixel-list render of a larger image cannot address its pixels
+    if (wh > (1ull << 32)) return mrt_internal_fail(MRT_ERR_INVALID, "render desc: pixel list on an image above 2^32 pixels");
+    for (uint32_t i = 0; i < d->n_pixels; i++)
+        if (d->pixels[i] >= wh) return mrt_internal_fail(MRT_ERR_INVALID, "render desc: pixel index outside the image");
+    // duplicates: sorted copy of the list (O(n log n) in the list, not the image), no throw across the ABI
+    try {
+        std::vector<uint32_t> v(d->pixels, d->pixels + d->n_pixels);
+        std::sort(v.begin(), v.end());
+        if (std::adjacent_find(v.begin(), v.end()) != v.end()) return mrt_internal_fail(MRT_ERR_INVALID, "render desc: pixel listed twice");
+    } catch (const std::bad_alloc&) {
+        return mrt_internal_fail(MRT_ERR_OOM, "render desc: pixel list check out of memory");
     }
     return MRT_OK;
 }

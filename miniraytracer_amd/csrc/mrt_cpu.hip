@@ -105,9 +105,6 @@ mrt_status mrt_cpu_scene_create(const mrt_scene_view* v, mrt_cpu_scene** out) {
     S.mnodes = c->mnodes.data();
     S.mwide = T.wide.data();
     S.mwide_n = (uint32_t)T.wide.size();
-    S.mesh4 = T.mesh4.data();
-    S.mesh4p = T.mesh4p.data();
-    S.mesh4_all = T.mesh4_all;
     S.bwide = T.bwide.data();
     S.bprims = T.bprims.data();
     S.tri_geo = c->tri_geo.data();
@@ -396,77 +393,6 @@ mrt_status mrt_cpu_preview(mrt_cpu_scene* c, float* rgb_out, uint32_t* samples_d
         *samples_done = c->tiles_done.load(std::memory_order_acquire) == c->n_tiles ? c->fb_ns : 0u;
     }
     return MRT_OK;
-}
-
-// Test hook (tests/test_mesh4.py): the resumable mesh walk's two steps -- binary (MeshWide) and
-// two-level (Mesh4, MRT_MESH4 kernels) -- run to completion on the host for n_rays random rays per
-// mesh of the scene (origins in 1.5x the mesh's box, directions uniform; one ray in four with a
-// zero direction component, which makes it not nice).  out[0..4]: rays that entered a root box,
-// hits, walks whose (result, t, triangle, u, v) differ, deepest two-level stack reached, its
-// bound (SceneTables::max_mesh4).
-extern "C" int mrt_debug_mesh4_walks(const mrt_scene_view* v, uint32_t n_rays, uint64_t seed, uint64_t* out) {
-    mrt_cpu_scene* c = nullptr;
-    if (mrt_cpu_scene_create(v, &c) != MRT_OK) return 1;
-    const SceneTables& T = c->T;
-    const DScene& S = c->S;
-    std::vector<uint32_t> stack((size_t)(std::max(T.max_mesh, T.max_mesh4) + 64) * 64);  // (headroom: an overrun is reported, not a crash)
-    LStack L{};
-    L.mesh = stack.data();
-    L.lane = 0;
-    uint64_t x = seed;
-    auto rnd = [&]() {  // splitmix64 -> [0, 1)
-        uint64_t z = (x += 0x9E3779B97F4A7C15ull);
-        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-        return (float)((z ^ (z >> 31)) >> 40) * 0x1p-24f;
-    };
-    uint64_t entered = 0, hits = 0, bad = 0, deep = 0;
-    for (const mrt_node& n : T.nodes) {
-        if ((n.kind & 0xFF) != MRT_K_MESH) continue;
-        const mrt_mesh_node& rt = c->mnodes[n.a];
-        uint32_t root4;
-        std::memcpy(&root4, &n.f[11], 4);
-        for (uint32_t i = 0; i < n_rays; i++) {
-            f3 o, d;
-            float* po = &o.x;
-            float* pd = &d.x;
-            for (int k = 0; k < 3; k++) {
-                const float mid = 0.5f * (rt.bmin[k] + rt.bmax[k]), ext = rt.bmax[k] - rt.bmin[k];
-                po[k] = mid + (rnd() - 0.5f) * 1.5f * ext;
-            }
-            float len;
-            do {
-                for (int k = 0; k < 3; k++) pd[k] = 2.0f * rnd() - 1.0f;
-                len = dot(d, d);
-            } while (len > 1.0f || len < 1e-4f);
-            if ((i & 3) == 3) pd[i % 3] = 0.0f;  // axis-parallel in one axis: not a nice ray
-            const Ray r = make_ray(o, d, 0.0f, 0);
-            if (!aabb_hit(rt.bmin, rt.bmax, r, 0.001f, FLT_MAX_)) continue;
-            entered++;
-            float t2 = FLT_MAX_, t4 = FLT_MAX_;
-            HitRec h2{}, h4{};
-            bool in2 = false, in4 = false;
-            uint32_t ref = n.b, msp = 0, s2, s4;
-            while ((s2 = mesh_step<false, true, false>(S, n, r, 0.001f, t2, h2, L, ref, msp, in2)) == 0u) {}
-            ref = root4;
-            msp = 0;
-            while ((s4 = mesh_step<false, true, true>(S, n, r, 0.001f, t4, h4, L, ref, msp, in4)) == 0u)
-                deep = std::max<uint64_t>(deep, msp);
-            hits += s2 == 1u;
-            bool same = s2 == s4;
-            if (same && s2 == 1u)
-                same = std::memcmp(&t2, &t4, 4) == 0 && h2.mat == h4.mat && std::memcmp(&h2.u, &h4.u, 4) == 0 &&
-                       std::memcmp(&h2.v, &h4.v, 4) == 0;
-            bad += !same;
-        }
-    }
-    out[0] = entered;
-    out[1] = hits;
-    out[2] = bad;
-    out[3] = deep;
-    out[4] = (uint64_t)T.max_mesh4;
-    mrt_cpu_scene_free(c);
-    return 0;
 }
 
 // Test hook (tests/test_host.py): the scene's linear hit program as compiled, or its

@@ -4,7 +4,7 @@
 // FMA contraction, hardware reciprocal/sqrt, f32 transcendentals).  DESIGN.md "Numerics contracts".
 #pragma once
 #include <hip/hip_runtime.h>
-#include "mrt_shade.h"
+#include "mrt_psum.h"
 
 namespace mrtd {
 
@@ -43,19 +43,36 @@ struct PathParams {
     uint32_t walk_min;                    // resumable mesh walk: yield once at most this many lanes walk
     const float4* tree_src;               // TreeOf<F>::on kernels: BvhWide nodes copied to LDS at start
     uint32_t tree_n;                      // how many (the first tree_n of the breadth-first array)
+    // pixel sums (mrt_psum.h; tolerance contract, mode 0): psum.acc non-null -> paths are ordered
+    // pixel-major (i = lp * cs + sl) and each path's radiance is added to its pixel's sum instead of
+    // written to rad
+    PsumOut psum;
+    uint32_t cs;                          // samples of this chunk (pixel-major order)
+    double inv_cs;                        // 1.0 / cs
+    uint32_t lds_psum;                    // LDS words per lane slot of the wave's pixel slots (PSUM_WORDS or 0)
+    uint32_t retrace_phase;               // mrt_retrace_kernel: 0 the handed-over paths, 1 the non-finite samples' prefixes
 };
+
+// path index -> (local pixel, sample row of the chunk): sample-major i = sl * npix + lp, or
+// pixel-major i = lp * cs + sl under pixel sums
+MRT_DFN void path_coords(const PathParams& P, uint32_t i, uint32_t* lp_out, uint32_t* sl_out) {
+    const bool pm = MRT_FWD_FOLD && P.psum.acc != nullptr;  // (the exact build folds deepest-first, per path)
+    const uint32_t n = pm ? P.cs : P.npix;
+    // the double estimate of i / n is off by at most one either way
+    uint32_t q = (uint32_t)((double)i * (pm ? P.inv_cs : P.inv_npix));
+    uint32_t r = i - q * n;
+    if ((int32_t)r < 0) { q--; r += n; }
+    if (r >= n) { q++; r -= n; }
+    *lp_out = pm ? q : r;
+    *sl_out = pm ? r : q;
+}
 
 typedef void (*path_kernel_t)(PathParams);
 
 // path index -> its camera coordinates (u, v) and its PCG stream seeded from the path key
 // (main.cpp:138-149 per (pixel, sample); the stream key of DESIGN.md section 2)
-MRT_DFN void path_key_of(const PathParams& P, uint32_t i, Pcg& rng, float* uo, float* vo) {
-    // i = sl * npix + lp; the double estimate is off by at most one either way
-    uint32_t sl = (uint32_t)((double)i * P.inv_npix);
-    uint32_t lp = i - sl * P.npix;
-    if ((int32_t)lp < 0) { sl--; lp += P.npix; }
-    if (lp >= P.npix) { sl++; lp -= P.npix; }
-    const uint32_t s = P.s0 + sl;
+// (local pixel lp, sample s) -> the same
+MRT_DFN void path_key_at(const PathParams& P, uint32_t lp, uint32_t s, Pcg& rng, float* uo, float* vo) {
     const uint2 xy = P.pixels[lp];
     const uint32_t x = xy.x, y = xy.y;
     const uint32_t pix = x + y * P.width;
@@ -68,51 +85,11 @@ MRT_DFN void path_key_of(const PathParams& P, uint32_t i, Pcg& rng, float* uo, f
     const uint64_t path_id = (uint64_t)pix * P.ns + s;
     pcg_seed(rng, splitmix64(P.seed ^ path_id), path_id);
 }
-
-// The split ("wavefront") form of the path loop for the bvh_node scenes with volumes (DESIGN.md
-// section 4, "Split kernels"): each path lives in a slot of state arrays in HBM between two
-// kernels that alternate -- mrt_wf_ext<F> runs scene_object::hit for every slot's ray (the walk
-// alone, at the occupancy its registers allow) and mrt_wf_shade<F> runs the rest of trace()'s
-// segment (emission, material::scatter, pdfs), ends paths and starts new ones in the freed slots.
-// Same per-path operations in the same order as the path kernel: the same radiance bit for bit.
-struct WfState {
-    float4* __restrict__ ray0;    // o.xyz, time
-    float4* __restrict__ ray1;    // d.xyz, mask | nice << 8 | inside << 16
-    float4* __restrict__ ray2;    // inv.xyz, depth
-    uint4* __restrict__ rng;      // PCG state, inc
-    float4* __restrict__ thr;     // throughput T.xyz (forward fold)
-    uint32_t* __restrict__ idx;   // path index, MRT_NONE: idle slot
-    float4* __restrict__ hit0;    // t, p.xyz
-    float4* __restrict__ hit1;    // n.xyz, material (MRT_NONE: no hit)
-    float2* __restrict__ hit2;    // u, v
-};
-struct WfParams {
-    PathParams P;
-    WfState W;
-    uint32_t nslots;              // a multiple of 256
-    uint32_t iter;                // iteration of this launch pair
-    uint64_t epoch;               // render-loop serial (the host ignores older h_state words)
-    unsigned long long* __restrict__ cnt;   // MRT_NPART claim counters (paths handed out, relative), MRT_COUNTER_STRIDE apart
-    uint32_t* __restrict__ exh;   // bit k: partition k handed out
-    unsigned long long* __restrict__ ray_acc;  // per 64-slot group: rays of its ended paths
-    uint32_t* __restrict__ gcnt;  // the hit kernel's group claims: MRT_NPART counters, 128 B apart
-    unsigned long long* h_state;  // host-coherent: epoch << 32 | iter | exhausted << 31 (ext kernel, block 0)
-};
-typedef void (*wf_kernel_t)(WfParams);
-// the hit kernel's shape: waves per SIMD it is compiled for, and its workgroup (two groups per CU
-// sharing a treelet each, a multiple of 4 waves so both groups' waves spread evenly over the 4 SIMDs).
-// Measured on book2 (profiles/r04_split_ab.txt): 6 waves (80 VGPRs) best; at 5 the walk is
-// spill-free (96 VGPRs) but slower in 2 x 8 or 5 x 4 groups, and slower still in 2 x 10 (3+3+2+2
-// waves per group: most likely the two groups are not resident together).
-#ifndef MRT_WF_EXT_W
-#define MRT_WF_EXT_W 6
-#endif
-#ifndef MRT_WF_EXT_WG
-#define MRT_WF_EXT_WG (MRT_WF_EXT_W * 128)
-#endif
-#ifndef MRT_WF_CLAIM
-#define MRT_WF_CLAIM 2u  // 64-slot groups a hit-kernel wave claims per atomic
-#endif
+MRT_DFN void path_key_of(const PathParams& P, uint32_t i, Pcg& rng, float* uo, float* vo) {
+    uint32_t lp, sl;
+    path_coords(P, i, &lp, &sl);
+    path_key_at(P, lp, P.s0 + sl, rng, uo, vo);
+}
 
 // threads per path-kernel workgroup: TreeOf<F>::wg (mrt_trace.h).  One-wave groups by default
 // (each wave owns its own LDS slice; a small group frees its CU slot as soon as its wave finishes,
@@ -151,11 +128,11 @@ struct KernelTable {
     uint32_t tree[kNumVariants];  // 1: the kernel reads the top BvhWide nodes from an LDS treelet
     uint32_t pq[kNumVariants];    // LDS words per lane slot of the kernel's queue of path starts
     uint32_t box6_walk[kNumVariants];  // 1: Cornell shape walked by cornell_fast_hit when op 8 is MRT_F_BOX6
-    uint32_t mesh4[kNumVariants];      // 1: the resumable mesh walk two levels at a time (Mesh4, MRT_MESH4)
     uint32_t rewrite[kNumVariants];    // 1: the interpreter runs the rewritten program (mrt_sig.h lin_rewrite_fast)
-    wf_kernel_t wf_ext[kNumVariants];  // split form (WfParams): the hit kernel, or null
-    wf_kernel_t wf_shade[kNumVariants];  // its shade kernel
-    uint32_t wf_ext_wg[kNumVariants];  // threads per hit-kernel workgroup
+    uint32_t psum[kNumVariants];       // 1: the kernel can add its paths to pixel sums (mrt_psum.h; LDS reserved)
+    // the path-exact build's retrace kernel for the tolerance variants that hand rounding-critical
+    // paths over (mrt_shade.h light_critical): launched over PsumOut::rt after the path kernels
+    path_kernel_t retrace[kNumVariants];
 };
 const KernelTable& kernel_table_exact();
 const KernelTable& kernel_table_fast();

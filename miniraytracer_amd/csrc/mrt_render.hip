@@ -50,11 +50,8 @@ static void take_variant(KernelTable& m, const KernelTable& s, uint32_t i) {
     m.tree[i] = s.tree[i];
     m.pq[i] = s.pq[i];
     m.box6_walk[i] = s.box6_walk[i];
-    m.mesh4[i] = s.mesh4[i];
     m.rewrite[i] = s.rewrite[i];
-    m.wf_ext[i] = s.wf_ext[i];
-    m.wf_shade[i] = s.wf_shade[i];
-    m.wf_ext_wg[i] = s.wf_ext_wg[i];
+    m.psum[i] = s.psum[i];
 }
 static const KernelTable& fast_table() {
     static const KernelTable t = [] {
@@ -68,6 +65,8 @@ static const KernelTable& fast_table() {
         for (uint32_t i = 0; i < kNumVariants; i++) {
             if (x.kernel[i] && !off("MRT_PATH_EXACT")) take_variant(m, x, i);
             else if (z.kernel[i] && !off("MRT_FTZ")) take_variant(m, z, i);
+            // the exact arithmetic for the pixel-sum renders' small jobs (mrt_kernels.hip mrt_retrace_kernel)
+            m.retrace[i] = x.retrace[i];
         }
         return m;
     }();
@@ -209,6 +208,47 @@ mrt_final_kernel(const float4* __restrict__ acc, float4* __restrict__ out, uint3
     __builtin_amdgcn_raw_buffer_store_b128(o, ro, lp * 16u, 0, 0);
 }
 
+// Pixel sums (mrt_psum.h): the render's colours from the 64-bit sums -- draw()'s `/= numSamples`
+// and luminance clamp (final_pixel, main.cpp:168-173) -- into the caller's output; unless `keep`
+// (a preview), the sums cleared for the next render, the counters reset (FoldEnd) and, by the last
+// group to finish, the non-finite list emptied (every group has read its length by then).
+__global__ void __launch_bounds__(256) mrt_psum_final_kernel(unsigned long long* __restrict__ acc, float4* __restrict__ out, uint32_t npix,
+                                                            uint32_t ns, float max_lum, const uint2* __restrict__ nf,
+                                                            const unsigned long long* __restrict__ nfp, uint32_t* nf_n,
+                                                            uint32_t* done, uint32_t* rt_n, uint32_t nf_cap, uint32_t keep, FoldEnd fe) {
+    const uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
+    if (!keep) reset_counters(fe, lp);
+    const uint32_t n_nf = __hip_atomic_load(nf_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lp < npix) {
+        ulonglong2* a2 = reinterpret_cast<ulonglong2*>(acc + (size_t)lp * 4u);
+        const ulonglong2 p = a2[0], q = a2[1];
+        const unsigned long long a[4] = {p.x, p.y, q.x, q.y};
+        f3 c = psum_color(a, lp, ns, nf, nfp, n_nf, nf_cap);
+        c = final_pixel(c, ns, 0u, max_lum);
+        out[lp] = make_float4(c.x, c.y, c.z, 0.0f);
+        if (!keep) {
+            a2[0] = make_ulonglong2(0ull, 0ull);
+            a2[1] = make_ulonglong2(0ull, 0ull);
+        }
+    }
+    if (!keep) {
+        __shared__ uint32_t last;
+        __syncthreads();
+        if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1u;
+        __syncthreads();
+        if (last) {  // every other group has read the lists: clear them (and the prefixes) for the next render
+            const uint32_t nl = n_nf < nf_cap ? n_nf : nf_cap;
+            if (nfp)
+                for (uint32_t i = threadIdx.x; i < nl * 4u; i += blockDim.x) const_cast<unsigned long long*>(nfp)[i] = 0ull;
+            if (threadIdx.x == 0) {
+                atomicExch(nf_n, 0u);
+                atomicExch(rt_n, 0u);
+                atomicExch(done, 0u);
+            }
+        }
+    }
+}
+
 // Image output on the device (main.cpp:416-444): global max luminance, then per-pixel Drago +
 // ARGB32 -- the functions of include/mrt_tonemap.h, the same bits as the host mrt_tonemap_argb.
 __global__ void __launch_bounds__(256) mrt_lum_max_kernel(const float4* __restrict__ rgb, uint32_t n, unsigned int* __restrict__ lwmax_bits) {
@@ -264,14 +304,13 @@ struct PathLaunch {
     uint32_t wg = 64;     // threads per workgroup
     uint32_t tree_n = 0;  // BvhWide nodes kept in each workgroup's LDS (treelet kernels)
     uint32_t lds_save = 0;  // LDS words per lane slot for the query ray parked during instances
-    uint32_t lds_mesh = 0;  // LDS words per lane of the mesh walk's stack (binary or two-level walk)
+    uint32_t lds_mesh = 0;  // LDS words per lane of the mesh walk's stack
     bool rewrite = false;   // the kernel runs the tolerance-contract program rewrite (s->prog_fast)
+    bool psum = false;      // the kernel can add paths to pixel sums (mrt_psum.h; its LDS slots reserved)
+    path_kernel_t retrace = nullptr;  // the exact arithmetic for pixel-sum renders (mrt_retrace_kernel)
+    size_t retrace_lds = 0;
+    bool handover = false;  // the kernel hands its rounding-critical paths to it (fast arithmetic)
     uint32_t walk_min = 32;  // resumable mesh walk threshold of this build (PathParams::walk_min)
-    // the split form (mrt_wavefront.h), where the build has it: hit kernel grid / LDS / treelet
-    wf_kernel_t wf_ext = nullptr, wf_shade = nullptr;
-    int wf_grid = 0;
-    size_t wf_lds = 0;
-    uint32_t wf_wg = 0, wf_tree_n = 0, wf_vgprs = 0;
 };
 
 // Wide nodes renumbered breadth-first over all roots together (level 0 of every tree, then level
@@ -337,7 +376,20 @@ struct mrt_scene {
     std::vector<uint32_t> prev_px;   // local pixel -> row-major pixel of the previewed render
     uint32_t prev_w = 0, prev_h = 0;
     uint32_t lev_rows = 0;
-    uint64_t* d_counter = nullptr;   // 64 B scratch: [0] unused, [2] ray total of mrt_render, [4] cancel flag
+    uint64_t* d_counter = nullptr;   // 64 B scratch: [0] unused, [2] ray total of mrt_render, [4] cancel flag,
+                                     // [6] non-finite samples listed (u32), [7] pixel-sum final groups done (u32),
+                                     // [1] rounding-critical paths listed (u32), [3] retrace groups done (u32)
+    // pixel sums (mrt_psum.h): 4 x u64 per local pixel, zero between renders (the final kernel
+    // clears what it read); the non-finite samples' list
+    unsigned long long* d_acc64 = nullptr;
+    size_t acc64_cap = 0;
+    uint2* d_nf = nullptr;
+    size_t nf_cap = 0;
+    unsigned long long* d_nfp = nullptr;  // per non-finite entry: the finite samples ahead of it
+    size_t nfp_cap = 0;
+    uint2* d_rt = nullptr;           // rounding-critical paths handed to the retrace kernel
+    size_t rt_cap = 0;
+    bool psum = false;               // the workspace's render (wdesc) runs with pixel sums
     uint64_t* d_counters = nullptr;  // one work counter per chunk launch (progress reads them)
     size_t cnt_cap = 0;
     std::vector<uint64_t> chunk_paths;
@@ -369,15 +421,6 @@ struct mrt_scene {
     uint64_t last_paths = 0;
     uint32_t last_numerics = 0;
     uint32_t prog_ops = 0;  // linear hit program length (0: generic machine)
-    // split-form workspace (mrt_wavefront.h): slot arrays, claim counters, per-group ray words
-    void* d_wf = nullptr;
-    size_t wf_cap = 0;
-    unsigned long long* h_wf = nullptr;  // host-coherent: the hit kernel's iteration / exhaustion word
-    uint64_t wf_epoch = 0;
-    bool last_split = false;  // the last render ran the split form
-    // mrt_render's cancel flag while its split render enqueues (wf_run forwards it to the device flag)
-    const volatile int* host_cancel = nullptr;
-    bool wf_cancelled = false;
 };
 
 static mrt_status dev_alloc(mrt_scene* s, void** p, size_t bytes) {
@@ -692,102 +735,6 @@ mrt_status mrt_internal_scene_tables(const mrt_scene_view* v, SceneTables* T) {
             if ((n.kind & 0xFF) == MRT_K_MESH) mroots.push_back(&n.b);
         bfs_order(wide, mroots, MESH_LEAF, 63u);
     }
-    // pod_bvh two levels per node (Mesh4, mrt_trace.h), breadth-first from each mesh's root; the
-    // root ref in the MESH node's f[11]
-    {
-        const mrt_mesh_node* mn = v->mesh_nodes;
-        auto inner = [&](uint32_t i) { return (mn[i].count_order & 0xFFFFFFu) == 0; };
-        auto leaf_ref = [&](uint32_t i) { return MESH_LEAF | ((mn[i].count_order & 0xFFFFFFu) << 24) | mn[i].left_or_first; };
-        auto inside = [&](uint32_t c, uint32_t p) {
-            for (int k = 0; k < 3; k++)
-                if (!(mn[c].bmin[k] >= mn[p].bmin[k] && mn[c].bmax[k] <= mn[p].bmax[k])) return false;
-            return true;
-        };
-        std::vector<uint32_t> idx4(v->n_mesh_nodes, MRT_NONE);
-        std::vector<uint32_t> queue;
-        auto alloc = [&](uint32_t i) {
-            if (idx4[i] == MRT_NONE) {
-                idx4[i] = (uint32_t)T->mesh4.size();
-                T->mesh4.push_back(Mesh4{});
-                T->mesh4p.push_back(Mesh4Pair{});
-                queue.push_back(i);
-            }
-            return idx4[i];
-        };
-        for (mrt_node& n : nodes) {
-            if ((n.kind & 0xFF) != MRT_K_MESH) continue;
-            // (the wide build above has checked the mesh's node indices and leaf encodings)
-            const uint32_t root = inner(n.a) ? alloc(n.a) : leaf_ref(n.a);
-            uint32_t bits = root;
-            std::memcpy(&n.f[11], &bits, 4);
-            for (size_t qi = 0; qi < queue.size(); qi++) {
-                const uint32_t i = queue[qi];
-                Mesh4 q{};
-                Mesh4Pair pr{};
-                uint32_t sl[4] = {MRT_NONE, MRT_NONE, MRT_NONE, MRT_NONE};  // binary node of each slot
-                uint32_t meta = mn[i].count_order >> 24;
-                for (uint32_t p = 0; p < 2; p++) {
-                    const uint32_t c = mn[i].left_or_first + p;
-                    float* pmin = p ? pr.bmin : pr.amin;
-                    float* pmax = p ? pr.bmax : pr.amax;
-                    for (int k = 0; k < 3; k++) { pmin[k] = mn[c].bmin[k]; pmax[k] = mn[c].bmax[k]; }
-                    if (!inside(c, i)) T->mesh4_all = 1;
-                    if (inner(c)) {
-                        meta |= (mn[c].count_order >> 24) << (8 + 8 * p);
-                        sl[2 * p] = mn[c].left_or_first;
-                        sl[2 * p + 1] = mn[c].left_or_first + 1;
-                    } else {
-                        meta |= 0xFFu << (8 + 8 * p);  // (one slot: its order is moot)
-                        sl[2 * p] = c;
-                    }
-                }
-                for (uint32_t k = 0; k < 4; k++) {
-                    const uint32_t b = sl[k];
-                    if (b == MRT_NONE) continue;
-                    meta |= 1u << (24 + k);
-                    Mesh4::Slot& S4 = q.s[k];
-                    for (int j = 0; j < 3; j++) { S4.lo[j] = mn[b].bmin[j]; S4.hi[j] = mn[b].bmax[j]; }
-                    S4.ref = inner(b) ? alloc(b) : leaf_ref(b);
-                    const uint32_t par = mn[i].left_or_first + (k >> 1);
-                    if (b != par && !inside(b, par)) T->mesh4_all = 1;
-                }
-                q.s[0].meta = meta;
-                T->mesh4[idx4[i]] = q;
-                T->mesh4p[idx4[i]] = pr;
-            }
-            queue.clear();
-        }
-        // deepest stack of the two-level walk: per ray octant, every box hit; children are
-        // numbered after their parents, so one pass from the back
-        const size_t n4 = T->mesh4.size();
-        std::vector<int> need(n4 * 8, 0);
-        for (size_t j = n4; j-- > 0;) {
-            const uint32_t meta = T->mesh4[j].s[0].meta;
-            for (uint32_t o = 0; o < 8; o++) {
-                const uint32_t mask = 1u << o;
-                const bool nl = (meta & mask) != 0, al = ((meta >> 8) & mask) != 0, bl = ((meta >> 16) & mask) != 0;
-                const uint32_t pa[2] = {al ? 0u : 1u, al ? 1u : 0u}, pb[2] = {bl ? 2u : 3u, bl ? 3u : 2u};
-                const uint32_t seq[4] = {nl ? pa[0] : pb[0], nl ? pa[1] : pb[1], nl ? pb[0] : pa[0], nl ? pb[1] : pa[1]};
-                uint32_t vis[4], nv = 0;
-                for (uint32_t k = 0; k < 4; k++)
-                    if (meta & (1u << (24 + seq[k]))) vis[nv++] = seq[k];
-                int best = 0;
-                for (uint32_t p = 0; p < nv; p++) {
-                    const Mesh4::Slot& S4 = T->mesh4[j].s[vis[p]];
-                    const int below = (S4.ref & MESH_LEAF) ? 0 : need[(size_t)S4.ref * 8 + o];
-                    best = std::max(best, (int)(nv - 1 - p) + below);
-                }
-                need[j * 8 + o] = best;
-            }
-        }
-        for (const mrt_node& n : nodes) {
-            if ((n.kind & 0xFF) != MRT_K_MESH) continue;
-            uint32_t r;
-            std::memcpy(&r, &n.f[11], 4);
-            if (!(r & MESH_LEAF))
-                for (uint32_t o = 0; o < 8; o++) T->max_mesh4 = std::max(T->max_mesh4, need[(size_t)r * 8 + o]);
-        }
-    }
     // bvh_node subtrees whose leaves are primitives / object_lists of primitives (and of boxes of
     // primitives) -> wide nodes; the subtree root becomes an MRT_K_BVHW node (a = root ref)
     std::vector<BvhWide> bwide;
@@ -996,9 +943,6 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     UP(v->mesh_nodes, v->n_mesh_nodes, &S.mnodes);
     UP(T.wide.data(), T.wide.size(), &S.mwide);
     S.mwide_n = (uint32_t)T.wide.size();
-    UP(T.mesh4.data(), T.mesh4.size(), &S.mesh4);
-    UP(T.mesh4p.data(), T.mesh4p.size(), &S.mesh4p);
-    S.mesh4_all = T.mesh4_all;
     UP(T.bwide.data(), T.bwide.size(), &S.bwide);
     UP(T.bprims.data(), T.bprims.size(), &S.bprims);
     UP((const float4*)v->tri_geo, (size_t)v->n_tris * 3, &S.tri_geo);
@@ -1065,25 +1009,39 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
         const uint32_t waves_per_wg = L.wg / 64u;
         // the Cornell walk of the tolerance contract (mrt_sig.h cornell_fast_hit) parks no ray
         L.lds_save = tabs[k]->box6_walk[s->variant] ? 0u : s->lds_save;
-        L.lds_mesh = tabs[k]->mesh4[s->variant] ? std::max(s->lds_mesh, (uint32_t)T.max_mesh4) : s->lds_mesh;
+        L.lds_mesh = s->lds_mesh;
         L.rewrite = tabs[k]->rewrite[s->variant] != 0;
+        L.psum = tabs[k]->psum[s->variant] != 0;
+        L.retrace = tabs[k]->retrace[s->variant];
+        // a fast-arithmetic kernel hands its rounding-critical paths to the exact arithmetic
+        // (mrt_shade.h light_critical); MRT_RETRACE=0 at upload keeps them (A/B)
+        {
+            const char* e = getenv("MRT_RETRACE");
+            L.handover = k == 1 && L.retrace && L.fn != kernel_table_fast_pex().kernel[s->variant] && !(e && *e && atoi(e) == 0);
+        }
+        L.retrace_lds = (size_t)64 * 4 * (s->lds_frames * 2 + s->lds_rays * 11 + s->lds_mesh + s->lds_save);
         // the path-exact build (the metal bunny under the tolerance contract) yields at 32 walking
         // lanes: 40 -1.2%, 28 -1.7%, 48 -10% (bunny 1024x1024x64, profiles/r04_ab.txt section 13)
         L.walk_min = (!walk_min_env && L.fn == kernel_table_fast_pex().kernel[s->variant]) ? 32u : s->walk_min;
-        L.lds_bytes = (size_t)waves_per_wg * 64 * 4 *
-                      (s->lds_frames * 2 + s->lds_rays * 11 + L.lds_mesh + L.lds_save + tabs[k]->lev_k[s->variant] * 4 +
-                       tabs[k]->pq[s->variant]);
+        hipFuncAttributes fa{};
+        HIPCHK(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(L.fn)));
+        const int vg = std::max(8, (fa.numRegs + 7) & ~7);
+        const int nb_vgpr = std::max(1, std::min(8, 512 / vg) * 4 / (int)waves_per_wg);  // waves per CU / waves per group
+        auto groups = [&](size_t lds) { return std::max(1, lds ? std::min<int>(nb_vgpr, (int)((160u * 1024u) / lds)) : nb_vgpr); };
+        const size_t lds_core = (size_t)waves_per_wg * 64 * 4 *
+                                (s->lds_frames * 2 + s->lds_rays * 11 + L.lds_mesh + L.lds_save + tabs[k]->lev_k[s->variant] * 4 +
+                                 tabs[k]->pq[s->variant]);
+        // pixel sums only where their LDS slots (PSUM_WORDS per lane slot) cost no resident group:
+        // the mesh kernels' stacks leave no room for them at 7 waves per SIMD (measured with them:
+        // teapot -11%, bunny -24% at 6), and those kernels keep the per-path radiance buffer
+        if (L.psum && !tabs[k]->tree[s->variant] && groups(lds_core + (size_t)waves_per_wg * 64 * 4 * PSUM_WORDS) < groups(lds_core))
+            L.psum = false;
+        L.lds_bytes = lds_core + (L.psum ? (size_t)waves_per_wg * 64 * 4 * PSUM_WORDS : 0u);
         if (L.lds_bytes > (size_t)prop.sharedMemPerBlock) {
             mrt_scene_free(s);
             return mrt_internal_fail(MRT_ERR_INVALID, "scene graph too deep for the LDS stacks");
         }
-        hipFuncAttributes fa{};
-        HIPCHK(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(L.fn)));
-        const int vg = std::max(8, (fa.numRegs + 7) & ~7);
-        int nb = std::min(8, 512 / vg) * 4 / (int)waves_per_wg;  // waves per CU / waves per group
-        if (nb < 1) nb = 1;
-        if (L.lds_bytes) nb = std::min<int>(nb, (int)((160u * 1024u) / L.lds_bytes));
-        if (nb < 1) nb = 1;
+        int nb = groups(L.lds_bytes);
         if (tabs[k]->tree[s->variant]) {
             // the LDS the resident groups leave free, split among them: the treelet of each group
             const size_t per = std::min<size_t>((160u * 1024u) / nb, (size_t)prop.sharedMemPerBlock);
@@ -1103,26 +1061,6 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
             if (*e) nb = std::max(1, atoi(e));
 #endif
         L.grid = prop.multiProcessorCount * nb;
-        if (tabs[k]->wf_ext[s->variant]) {  // the split form: the hit kernel's own occupancy and treelet
-            L.wf_ext = tabs[k]->wf_ext[s->variant];
-            L.wf_shade = tabs[k]->wf_shade[s->variant];
-            L.wf_wg = tabs[k]->wf_ext_wg[s->variant];
-            const uint32_t wwg = L.wf_wg / 64u;
-            L.wf_lds = (size_t)wwg * 64 * 4 * (s->lds_frames * 2 + s->lds_rays * 11 + L.lds_mesh + L.lds_save);
-            hipFuncAttributes wa{};
-            HIPCHK(hipFuncGetAttributes(&wa, reinterpret_cast<const void*>(L.wf_ext)));
-            const int wv = std::max(8, (wa.numRegs + 7) & ~7);
-            int wn = std::max(1, std::min(8, 512 / wv) * 4 / (int)wwg);
-            if (L.wf_lds) wn = std::max(1, std::min<int>(wn, (int)((160u * 1024u) / L.wf_lds)));
-            if (tabs[k]->tree[s->variant]) {
-                const size_t per = std::min<size_t>((160u * 1024u) / wn, (size_t)prop.sharedMemPerBlock);
-                const uint32_t cap = per > L.wf_lds ? (uint32_t)((per - L.wf_lds) / 64u) : 0u;
-                L.wf_tree_n = std::min(cap, (uint32_t)bwide.size());
-                L.wf_lds += (size_t)L.wf_tree_n * 64u;
-            }
-            L.wf_vgprs = (uint32_t)wa.numRegs;
-            L.wf_grid = prop.multiProcessorCount * wn;
-        }
         // every work partition needs waves of its own: a wave leaves its partition only once it is
         // handed out, and visits at most MRT_STEAL_TRIES partitions (mrt_kernels.hip)
         if (L.grid < (int)MRT_NPART) return mrt_internal_fail(MRT_ERR_HIP, "path kernel grid smaller than the work partitions");
@@ -1148,10 +1086,9 @@ extern "C" void mrt_scene_free(mrt_scene* s) {
     if (s->h_one) (void)hipHostFree(s->h_one);
     if (s->h_prev) (void)hipHostFree(s->h_prev);
     if (s->h_seq) (void)hipHostFree(s->h_seq);
-    if (s->h_wf) (void)hipHostFree(s->h_wf);
     if (s->ev_done) (void)hipEventDestroy(s->ev_done);
     for (void* p : {(void*)s->d_counters, (void*)s->d_pixels, (void*)s->d_sdist, (void*)s->d_rad, (void*)s->d_path_rays, (void*)s->d_acc,
-                    (void*)s->d_lev, (void*)s->d_out, (void*)s->d_prev, s->d_wf})
+                    (void*)s->d_lev, (void*)s->d_out, (void*)s->d_prev, (void*)s->d_acc64, (void*)s->d_nf, (void*)s->d_nfp, (void*)s->d_rt})
         if (p) (void)hipFree(p);
     delete s;
 }
@@ -1193,122 +1130,18 @@ static mrt_status grow(mrt_scene* s, void** p, size_t* cap, size_t bytes) {
     return MRT_OK;
 }
 
-// the render's ray total from the split form's per-group words
-__global__ void __launch_bounds__(1024) mrt_wf_rays_kernel(unsigned long long* __restrict__ acc, uint32_t n, unsigned long long* __restrict__ rays) {
-    unsigned long long t = 0;
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) t += acc[i];
-    for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
-    if ((threadIdx.x & 63u) == 0 && t) atomicAdd(rays, t);
-}
-
-// Whether a render runs the split form (mrt_wavefront.h): where the scene's kernel build has it,
-// on MRT_RF_SPLIT; MRT_SPLIT=1 / 0 in the environment turns it on / off for every render (A/B).
-static bool want_split(const PathLaunch& PL, uint32_t flags) {
-    if (!PL.wf_ext) return false;
-    const char* e = getenv("MRT_SPLIT");
-    if (e && *e) return atoi(e) != 0;
-    return (flags & MRT_RF_SPLIT) != 0;
-}
-
-// One launch chunk in the split form: shade / hit kernel pairs over the slot arrays until every
-// path of the chunk has ended.  The host enqueues pairs ahead of the GPU (at most kAhead beyond the
-// iteration the hit kernel last published) until the partitions are handed out; every path then
-// ends within max_bounces + 1 more segments (shade_hit's depth limit), so that many pairs follow.
-// slots of a split launch of n_paths paths and the workspace bytes they take
-static uint32_t wf_slots(const PathLaunch& PL, uint64_t n_paths) {
-    uint64_t mult = 16;  // slots per resident hit-kernel lane
-    if (const char* e = getenv("MRT_SPLIT_SLOTS"))  // sweep hook
-        if (*e) mult = std::max(1, atoi(e));
-    const uint64_t want = (uint64_t)PL.wf_grid * PL.wf_wg * mult;
-    const uint64_t need = (n_paths + 255) / 256 * 256;
-    uint32_t ns = (uint32_t)std::max<uint64_t>(256, std::min(want, need));
-    if (const char* e = getenv("MRT_SPLIT_NSLOTS"))  // test hook: this many slots (a multiple of 256)
-        if (*e) ns = std::max(256u, (uint32_t)atoi(e) & ~255u);
-    return ns;
-}
-static constexpr size_t kWfCntBytes = (size_t)MRT_NPART * MRT_COUNTER_STRIDE * 8 + 128 + MRT_NPART * 128;  // counters, exhaustion mask, group claims
-static size_t wf_bytes(uint32_t ns) { return (size_t)ns * (7 * 16 + 8 + 4) + kWfCntBytes + (size_t)(ns / 64) * 8; }
-// the split workspace for a launch of n_paths (mrt_prepare sizes it, so a render allocates nothing)
-static mrt_status wf_reserve(mrt_scene* s, const PathLaunch& PL, uint64_t n_paths) {
-    mrt_status st = grow(s, &s->d_wf, &s->wf_cap, wf_bytes(wf_slots(PL, n_paths)));
-    if (st) return st;
-    if (!s->h_wf) {
-        HIPCHK(hipHostMalloc((void**)&s->h_wf, 64, hipHostMallocPortable | hipHostMallocCoherent));
-        memset(s->h_wf, 0, 64);
-    }
-    return MRT_OK;
-}
-
-static mrt_status wf_run(mrt_scene* s, const PathLaunch& PL, PathParams P, hipStream_t q) {
-    constexpr uint32_t kAhead = 64;
-    P.tree_n = PL.wf_tree_n;
-    const uint32_t ns = wf_slots(PL, P.n_paths);
-    const size_t cnt_bytes = kWfCntBytes;
-    const size_t acc_bytes = (size_t)(ns / 64) * 8;
-    mrt_status st = wf_reserve(s, PL, P.n_paths);
-    if (st) return st;
-    char* b = (char*)s->d_wf;
-    WfParams A{};
-    auto take = [&](size_t n) { char* p = b; b += n; return (void*)p; };
-    A.W.ray0 = (float4*)take((size_t)ns * 16);
-    A.W.ray1 = (float4*)take((size_t)ns * 16);
-    A.W.ray2 = (float4*)take((size_t)ns * 16);
-    A.W.rng = (uint4*)take((size_t)ns * 16);
-    A.W.thr = (float4*)take((size_t)ns * 16);
-    A.W.hit0 = (float4*)take((size_t)ns * 16);
-    A.W.hit1 = (float4*)take((size_t)ns * 16);
-    A.W.hit2 = (float2*)take((size_t)ns * 8);
-    A.W.idx = (uint32_t*)take((size_t)ns * 4);
-    A.cnt = (unsigned long long*)take((size_t)MRT_NPART * MRT_COUNTER_STRIDE * 8);
-    A.exh = (uint32_t*)take(128);
-    A.gcnt = (uint32_t*)take(MRT_NPART * 128);
-    A.ray_acc = (unsigned long long*)take(acc_bytes);
-    HIPCHK(hipMemsetAsync(A.W.idx, 0xFF, (size_t)ns * 4, q));  // every slot idle
-    HIPCHK(hipMemsetAsync(A.cnt, 0, cnt_bytes + acc_bytes, q));
-    A.P = P;
-    A.nslots = ns;
-    s->wf_epoch = (s->wf_epoch + 1) & 0xFFFFFFFFull;
-    if (s->wf_epoch == 0) s->wf_epoch = 1;
-    A.epoch = s->wf_epoch;
-    A.h_state = s->h_wf;
-    uint64_t stop_at = ~0ull;
-    uint64_t seen = 0;
-    bool seen_any = false;
-    for (uint64_t it = 0; it < stop_at; it++) {
-        A.iter = (uint32_t)it;
-        hipLaunchKernelGGL(PL.wf_shade, dim3(ns / 256u), dim3(256), 0, q, A);
-        hipLaunchKernelGGL(PL.wf_ext, dim3(PL.wf_grid), dim3(PL.wf_wg), PL.wf_lds, q, A);
-        HIPCHK(hipGetLastError());
-        for (uint32_t polls = 0;; polls++) {
-            const uint64_t h = __atomic_load_n(s->h_wf, __ATOMIC_ACQUIRE);
-            if ((h >> 32) == A.epoch) {
-                seen = h & 0x7FFFFFFFull;
-                seen_any = true;
-                if ((h & 0x80000000ull) && stop_at == ~0ull) stop_at = seen + P.max_bounces + 2;
-            }
-            if (s->host_cancel && *s->host_cancel && !s->wf_cancelled) {  // G_isRunning: stop handing out paths
-                HIPCHK(hipMemcpyAsync(s->d_counter + 4, s->h_one, sizeof(int), hipMemcpyHostToDevice, s->pstream));
-                HIPCHK(hipStreamSynchronize(s->pstream));
-                s->wf_cancelled = true;
-            }
-            if (stop_at != ~0ull || it + 1 < (seen_any ? seen : 0) + kAhead) break;
-            const hipError_t e = hipStreamQuery(q);
-            if (e != hipSuccess && e != hipErrorNotReady) return mrt_internal_fail(MRT_ERR_HIP, "split render: stream error");
-            if (e == hipSuccess) {  // the stream drained: the last word must be there now
-                const uint64_t h2 = __atomic_load_n(s->h_wf, __ATOMIC_ACQUIRE);
-                if ((h2 >> 32) != A.epoch || (h2 & 0x7FFFFFFFull) < it)
-                    return mrt_internal_fail(MRT_ERR_HIP, "split render: the hit kernel's state word did not arrive");
-                continue;
-            }
-            // the GPU is kAhead launch pairs behind: yield at first, then sleep (a long render's host
-            // thread does not spin a core for its whole duration)
-            if (polls < 64) std::this_thread::yield();
-            else usleep(50);
-        }
-    }
-    hipLaunchKernelGGL(mrt_wf_rays_kernel, dim3(1), dim3(1024), 0, q, A.ray_acc, ns / 64u, P.rays);
-    HIPCHK(hipGetLastError());
-    return MRT_OK;
+// Pixel sums (mrt_psum.h) for a render: the tolerance contract, mode 0 (draw(); draw2()'s per-pass
+// clamp needs the samples in order), no per-path debug output, on a kernel that has them.
+// MRT_PSUM=0 in the environment keeps the per-path radiance buffer and the fold (A/B).
+static constexpr uint32_t kNfCap = 1u << 16;  // non-finite samples listed per render
+// rounding-critical paths listed per render (a kernel stops handing over at half of it): ~1.5e-5 per
+// path in the Cornell scenes, so room for ~3.5e10 paths
+static constexpr uint32_t kRtCap = 1u << 20;
+static constexpr uint32_t kRetraceGroups = 512;  // one-wave groups of the retrace kernel
+static bool want_psum(const mrt_scene* s, const mrt_render_desc* d) {
+    if (!(d->flags & MRT_RF_FAST) || d->mode != 0 || (d->flags & (MRT_RF_PATH_DEBUG | MRT_RF_FOLD_BEHIND)) || !s->pl[1].psum) return false;
+    const char* e = getenv("MRT_PSUM");
+    return !(e && *e && atoi(e) == 0);
 }
 
 #define MRT_GPU_ONLY(s, what) \
@@ -1349,16 +1182,36 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
         HIPCHK(hipMemcpy(s->d_sdist, sd.data(), sd.size() * 8, hipMemcpyHostToDevice));
         s->sdist_sq = sq;
     }
-    uint32_t chunk = d->chunk_samples ? std::min(d->chunk_samples, ns) : auto_chunk(s->npix, ns);
+    // pixel sums (mrt_psum.h): the tolerance contract's mode 0 on a kernel that has them; no
+    // per-path radiance buffer, so a launch is bounded by the 32-bit path index only
+    const bool psum = want_psum(s, d);
+    uint32_t chunk = d->chunk_samples ? std::min(d->chunk_samples, ns) : psum ? ns : auto_chunk(s->npix, ns);
     chunk = (uint32_t)std::min<uint64_t>(chunk, 0xFFFFFFFFull / std::max<uint32_t>(s->npix, 1));  // 32-bit path index
     // 32-bit byte offsets of the chunk's radiance (the path kernel's held store, mrt_kernels.hip)
-    chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(chunk, 0xFFFFFFFFull / (12ull * std::max<uint32_t>(s->npix, 1))));
+    if (!psum) chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(chunk, 0xFFFFFFFFull / (12ull * std::max<uint32_t>(s->npix, 1))));
     if (chunk == 0) return mrt_internal_fail(MRT_ERR_INVALID, "image too large for one launch");
     if (d->flags & MRT_RF_PATH_DEBUG) chunk = ns;  // debug keeps every path
     if (chunk != s->chunk && (st = quiesce(s))) return st;  // the fold of a running render reads `chunk` rows
     s->chunk = chunk;
     size_t paths = (size_t)s->npix * s->chunk;
-    if ((st = grow(s, (void**)&s->d_rad, &s->rad_cap, paths * 12))) return st;
+    if (psum) {
+        void* const before = s->d_acc64;
+        if ((st = grow(s, (void**)&s->d_acc64, &s->acc64_cap, (size_t)s->npix * 32))) return st;
+        // zeroed once at allocation; afterwards every render's final kernel leaves it zero
+        if (s->d_acc64 != before) HIPCHK(hipMemset(s->d_acc64, 0, s->acc64_cap));
+        if ((st = grow(s, (void**)&s->d_nf, &s->nf_cap, (size_t)kNfCap * sizeof(uint2)))) return st;
+        if (s->pl[1].retrace) {
+            void* const b2 = s->d_nfp;
+            if ((st = grow(s, (void**)&s->d_nfp, &s->nfp_cap, (size_t)kNfCap * 32))) return st;
+            if (s->d_nfp != b2) HIPCHK(hipMemset(s->d_nfp, 0, s->nfp_cap));  // later: cleared by each render's final kernel
+        }
+    } else if ((st = grow(s, (void**)&s->d_rad, &s->rad_cap, paths * 12))) {
+        return st;
+    }
+    if ((d->flags & MRT_RF_FAST) && !(d->flags & MRT_RF_PATH_DEBUG) && s->pl[1].handover &&
+        (st = grow(s, (void**)&s->d_rt, &s->rt_cap, (size_t)kRtCap * sizeof(uint2))))
+        return st;
+    s->psum = psum;
     if ((st = grow(s, (void**)&s->d_acc, &s->acc_cap, (size_t)s->npix * 16))) return st;
     if ((st = grow(s, (void**)&s->d_out, &s->out_cap, (size_t)s->npix * 16 + 16))) return st;
     if (d->flags & MRT_RF_PREVIEW) {
@@ -1384,10 +1237,6 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
     }
     if (d->flags & MRT_RF_PATH_DEBUG)
         if ((st = grow(s, (void**)&s->d_path_rays, &s->pr_cap, paths * 4))) return st;
-    {  // the split form's slot arrays (MRT_RF_SPLIT on a scene whose build has it)
-        const PathLaunch& PL = s->pl[(d->flags & MRT_RF_FAST) ? 1 : 0];
-        if (want_split(PL, d->flags) && (st = wf_reserve(s, PL, paths))) return st;
-    }
     s->lev_rows = std::max<uint32_t>(d->max_bounces, 1);
     if ((st = grow(s, (void**)&s->d_lev, &s->lev_cap, (size_t)s->lev_rows * s->max_threads * 16))) return st;
     uint32_t launches = (ns + s->chunk - 1) / s->chunk;
@@ -1456,8 +1305,6 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
     }
     s->n_launch = 0;
     s->last_numerics = (d->flags & MRT_RF_FAST) ? 1u : 0u;
-    const bool split = want_split(PL, d->flags);
-    s->last_split = split;
     const bool preview = (d->flags & MRT_RF_PREVIEW) != 0;
     uint32_t seq = 0;
     if (preview) {  // a new render: no snapshot yet (sequence 0), in stream order
@@ -1466,6 +1313,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         HIPCHK(hipStreamWriteValue32(q, s->h_seq, 0u, 0));
         s->prev_epoch++;
     }
+    PathParams Plast{};
     for (uint32_t s0 = 0; s0 < ns; s0 += s->chunk) {
         uint32_t s1 = std::min(ns, s0 + s->chunk);
         PathParams P{};
@@ -1512,20 +1360,42 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.rays = d_rays ? (unsigned long long*)d_rays : s->d_rays;
         P.lev = s->d_lev;
         P.lev_rows = s->lev_rows;
+        P.lds_psum = PL.psum ? PSUM_WORDS : 0u;  // (reserved in the kernel's LDS layout either way)
+        P.cs = s1 - s0;
+        P.inv_cs = 1.0 / (double)P.cs;
+        // the rounding-critical paths' hand-over: tolerance contract, not the per-path debug output
+        const bool handover = PL.handover && !(d->flags & MRT_RF_PATH_DEBUG);
+        if (s->psum)
+            P.psum = PsumOut{s->d_acc64, s->d_nf, (uint32_t*)(s->d_counter + 6), kNfCap, s->d_nfp, handover ? s->d_rt : nullptr,
+                             (uint32_t*)(s->d_counter + 1), kRtCap, (uint32_t*)(s->d_counter + 3)};
+        else if (handover)
+            P.psum.rt = s->d_rt, P.psum.rt_n = (uint32_t*)(s->d_counter + 1), P.psum.rt_cap = kRtCap,
+            P.psum.rt_done = (uint32_t*)(s->d_counter + 3);
         HIPCHK(hipEventRecord(s->ev[2 * s->n_launch], q));
-        if (split) {
-            if ((st = wf_run(s, PL, P, q))) return st;
-            // progress (mrt_progress) counts this chunk once its events are enqueued: publish now, the
-            // next chunk's loop only starts when this one's work is handed out
-            std::lock_guard<std::mutex> lk(s->prog_mu);
-            HIPCHK(hipEventRecord(s->ev[2 * s->n_launch + 1], q));
-            s->n_launch++;
-            s->n_chunks.store(s->n_launch, std::memory_order_release);
-        } else {
-            hipLaunchKernelGGL(PL.fn, dim3(PL.grid), dim3(PL.wg), PL.lds_bytes, q, P);
+        hipLaunchKernelGGL(PL.fn, dim3(PL.grid), dim3(PL.wg), PL.lds_bytes, q, P);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(s->ev[2 * s->n_launch + 1], q));
+        s->n_launch++;
+        if (s->psum) {  // pixel sums: no fold; a preview reads the sums as they stand
+            if (preview) {
+                hipLaunchKernelGGL(mrt_psum_final_kernel, dim3((s->npix + 255) / 256), dim3(256), 0, q, s->d_acc64, s->d_prev, s->npix, s1,
+                                   d->max_luminance, (const uint2*)s->d_nf, (const unsigned long long*)nullptr, (uint32_t*)(s->d_counter + 6), (uint32_t*)(s->d_counter + 7),
+                                   (uint32_t*)(s->d_counter + 1), kNfCap, 1u, FoldEnd{});
+                HIPCHK(hipGetLastError());
+                HIPCHK(hipStreamWriteValue32(q, s->h_seq, 2 * seq + 1, 0));
+                HIPCHK(hipMemcpyAsync(s->h_prev, s->d_prev, (size_t)s->npix * 16, hipMemcpyDeviceToHost, q));
+                HIPCHK(hipStreamWriteValue32(q, s->h_seq + 1, s1, 0));
+                HIPCHK(hipStreamWriteValue32(q, s->h_seq, 2 * seq + 2, 0));
+                seq++;
+            }
+            s->last_paths = P.n_paths;
+            Plast = P;
+            continue;
+        }
+        if (handover) {  // the handed-over paths of this launch, exact, into the radiance buffer (fold next)
+            P.retrace_phase = 2;
+            hipLaunchKernelGGL(PL.retrace, dim3(kRetraceGroups), dim3(64), PL.retrace_lds, q, P);
             HIPCHK(hipGetLastError());
-            HIPCHK(hipEventRecord(s->ev[2 * s->n_launch + 1], q));
-            s->n_launch++;
         }
         // the last chunk's full fold finishes the render (no preview: no snapshot of acc needed;
         // the 8-VGPR lean fold cannot take the division as well: a final kernel follows it)
@@ -1554,7 +1424,24 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         }
         s->last_paths = P.n_paths;
     }
-    if (preview || ((d->flags & MRT_RF_FOLD_BEHIND) && d->mode == 0)) {  // (otherwise the last fold wrote the output and reset the counters)
+    if (s->psum) {  // the colours from the sums, the counters reset, the sums cleared
+        if (PL.retrace) {  // the exact arithmetic's jobs (their counts are on the device: fixed small grids)
+            if (PL.handover && !(d->flags & MRT_RF_PATH_DEBUG)) {  // phase 0: the handed-over paths
+                Plast.retrace_phase = 0;
+                hipLaunchKernelGGL(PL.retrace, dim3(kRetraceGroups), dim3(64), PL.retrace_lds, q, Plast);
+                HIPCHK(hipGetLastError());
+            }
+            Plast.retrace_phase = 1;  // phase 1: the prefixes of the non-finite samples
+            hipLaunchKernelGGL(PL.retrace, dim3(kRetraceGroups), dim3(64), PL.retrace_lds, q, Plast);
+            HIPCHK(hipGetLastError());
+        }
+        const uint32_t nreset = launches * MRT_CNT_SLOTS;
+        const FoldEnd fe{(float4*)d_local, ns, (unsigned long long*)s->d_counters, (unsigned long long*)s->h_prog, nreset, launches * MRT_NPART};
+        hipLaunchKernelGGL(mrt_psum_final_kernel, dim3((std::max(s->npix, nreset) + 255) / 256), dim3(256), 0, q, s->d_acc64, (float4*)d_local,
+                           s->npix, ns, d->max_luminance, (const uint2*)s->d_nf, (const unsigned long long*)(PL.retrace ? s->d_nfp : nullptr), (uint32_t*)(s->d_counter + 6), (uint32_t*)(s->d_counter + 7),
+                           (uint32_t*)(s->d_counter + 1), kNfCap, 0u, fe);
+        HIPCHK(hipGetLastError());
+    } else if (preview || ((d->flags & MRT_RF_FOLD_BEHIND) && d->mode == 0)) {  // (otherwise the last fold wrote the output and reset the counters)
         const uint32_t nreset = launches * MRT_CNT_SLOTS;
         const uint32_t blocks = (std::max(s->npix, nreset) + MRT_FINAL_WG - 1) / MRT_FINAL_WG;
         hipLaunchKernelGGL(mrt_final_kernel, dim3(blocks), dim3(MRT_FINAL_WG), 0, q, s->d_acc, (float4*)d_local, s->npix, ns, d->mode,
@@ -1581,13 +1468,10 @@ extern "C" mrt_status mrt_render(mrt_scene* s, const mrt_render_desc* d, float* 
     mrt_status st = mrt_prepare(s, d);
     if (st) return st;
     HIPCHK(hipMemset(s->d_rays, 0, 8));
-    s->host_cancel = cancel;  // (a split render polls it while it enqueues)
-    s->wf_cancelled = false;
     st = mrt_render_device(s, d, (float*)s->d_out, (uint64_t*)s->d_rays, nullptr);
-    s->host_cancel = nullptr;
     if (st) return st;
     // wait, forwarding the caller's cancel flag to the device flag the path kernel polls
-    bool cancelled = s->wf_cancelled;
+    bool cancelled = false;
     if (!cancel) {
         HIPCHK(hipEventSynchronize(s->ev_done));
     } else {
@@ -1718,11 +1602,6 @@ extern "C" mrt_status mrt_scene_kernel_info(const mrt_scene* s, mrt_kernel_info*
                : L.fn == kernel_table_fast_pex().kernel[s->variant] ? MRT_BUILD_PATH_EXACT
                : L.fn == kernel_table_fast_ftz().kernel[s->variant] ? MRT_BUILD_FAST_FTZ
                                                                      : MRT_BUILD_FAST;
-    out->split = s->last_split ? 1u : 0u;
-    out->split_vgprs = L.wf_vgprs;
-    out->split_grid = (uint32_t)L.wf_grid;
-    out->split_wg = L.wf_wg;
-    out->split_tree_nodes = L.wf_tree_n;
     return MRT_OK;
 }
 

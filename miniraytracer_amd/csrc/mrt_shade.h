@@ -185,6 +185,18 @@ MRT_DFN f3 biased_pdf_generate(const DScene& S, f3 origin, float time, Pcg& rng,
     return leaf_pdf_generate<F>(S, S.bleaf[i], origin, time, rng, dr);
 }
 
+// A light sample is rounding-critical (tolerance contract, DESIGN.md section 2 "Non-finite
+// samples") when its direction is (nearly) parallel to the plane of an xz_rect light through the
+// origin.  xz_rect::pdf_value (rect.cpp:92-102) of a ray from a point ON the light's plane with a
+// direction parallel to it (dir.y == 0: the sampled point's y minus the origin's) computes
+// t = 0 / 0 and reports a hit with a NaN pdf; main.cpp:162-164 then doubles the pixel's running
+// colour.  Whether a wall hit lands on y == 554 exactly depends on the last bit of its
+// arithmetic, so under the fast arithmetic these events fall on other paths than the reference's
+// (C3 at 4096 spp: 98% of the tolerance contract's squared error in 100 such pixels).  Such paths
+// are handed to the exact arithmetic instead (mrt_retrace_kernel): a sample direction whose y is
+// within 2^-16 of the origin's height (~140 ulps: the fast and the exact path differ by a few).
+MRT_DFN bool light_critical(f3 origin, f3 gen) { return fabsf(gen.y) <= fmaxf(fabsf(origin.y), 1.0f) * 0x1p-16f; }
+
 // ------------------------------------------------------------------------------------------
 // trace() (main.cpp:66-118) as a per-lane state machine advanced one segment (= one ray, one
 // scene_object::hit query) per call, so a lane whose path ends can start a new one at once.
@@ -310,7 +322,7 @@ MRT_DFN void camera_ray_args(const DScene& S, Pcg& rng, float s, float t, f3* o,
 // is then in *L.
 template <uint32_t F, uint32_t LK>
 MRT_DFN bool shade_hit(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev, bool hit,
-                                          const HitRec& rec, f3* L, PhaseClock& ph) {
+                                          const HitRec& rec, f3* L, PhaseClock& ph, bool* crit = nullptr) {
     Ray& r = ps.r;
     if (!hit) {
         if ((F & FT_SKY) && S.sky) {  // main.cpp:113-115
@@ -393,6 +405,11 @@ MRT_DFN bool shade_hit(const DScene& S, PathState& ps, uint32_t max_bounces, con
     }
     if (light) gen = biased_pdf_generate<F>(S, rec.p, r.time, ps.rng, dr);
     else gen = lamb ? onb_apply(rec.n, random_cosine_direction_pre(dr.v0, dr.v1)) : random_in_sphere(ps.rng);
+    if (crit && light && light_critical(rec.p, gen)) {  // ends here: retraced with the exact arithmetic
+        *crit = true;
+        *L = f3{0, 0, 0};
+        return true;
+    }
     PH_MARK(ph, 6);
     const Ray sc = make_ray(rec.p, gen, r.time, 0);
     float sval, spdf;
@@ -418,14 +435,14 @@ MRT_DFN bool shade_hit(const DScene& S, PathState& ps, uint32_t max_bounces, con
 // One segment.  Returns true when the path has ended; its radiance is then in *L.
 template <uint32_t F, uint32_t LK>
 MRT_DFN bool trace_segment(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev,
-                                              const LStack& Ls, f3* L, PhaseClock& ph) {
+                                              const LStack& Ls, f3* L, PhaseClock& ph, bool* crit = nullptr) {
     HitRec rec;
     bool hit;
     if constexpr (MRT_SIG_OF(F) != SIG_NONE) hit = scene_hit_sig<F>(S, ps.r, 0.001f, rec, Ls);
     else if constexpr ((F & FT_LIN) != 0) hit = scene_hit_lin<F>(S, ps.r, 0.001f, rec, Ls, ps.rng, ph);
     else hit = scene_hit<F>(S, ps.r, 0.001f, rec, ps.rng, Ls);
     PH_MARK(ph, 1);
-    return shade_hit<F, LK>(S, ps, max_bounces, lev, hit, rec, L, ph);
+    return shade_hit<F, LK>(S, ps, max_bounces, lev, hit, rec, L, ph, crit);
 }
 
 // The next ray of a lane, built by make_ray once per iteration for all lanes at once (camera
@@ -478,22 +495,13 @@ MRT_DFN void dielectric_scatter(const DMat& M, const Ray& r, f3 n, Pcg& rng, Pen
     pr->inside = inside;
 }
 
-// Dielectric deferral (experiment, MRT_DEFER_DIEL): a lane whose hit needs the
-// dielectric branch parks its hit (point, normal) and sits out the next iterations' walks until
-// enough lanes need the branch, which then runs once for all of them.  Same operations, same RNG
-// draws per path: results unchanged.
-#ifndef MRT_DEFER_DIEL
-#define MRT_DEFER_DIEL 0
-#endif
-
 // trace_segment up to the next ray's constructor arguments.  Returns true when the path has
 // ended (radiance in *L); otherwise *pr holds the next ray's arguments.
 // `flush` runs once the hit is known, before the material is read (the path loop issues the
 // previous path's radiance store there).
-template <uint32_t F, uint32_t LK, typename FLUSH, typename DEFER = std::nullptr_t>
+template <uint32_t F, uint32_t LK, typename FLUSH>
 MRT_DFN bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev,
-                                            const LStack& Ls, f3* L, PendRay* pr, PhaseClock& ph, FLUSH&& flush,
-                                            DEFER defer = nullptr) {
+                                            const LStack& Ls, f3* L, PendRay* pr, PhaseClock& ph, FLUSH&& flush, bool* crit = nullptr) {
     HitRec rec;
     Ray& r = ps.r;
     bool hit;
@@ -549,13 +557,6 @@ MRT_DFN bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, c
     }
     if (M.kind == MRT_M_DIELECTRIC) {  // dielectric::scatter (material.h:121-175)
         BSTAT(5);
-#if MRT_DEFER_DIEL
-        if constexpr (!std::is_same<DEFER, std::nullptr_t>::value) {  // shaded later, with other lanes'
-            defer(rec);
-            pr->kind = 3u;
-            return false;
-        }
-#endif
         dielectric_scatter(M, r, rec.n, ps.rng, pr);
         return false;
     }
@@ -577,6 +578,11 @@ MRT_DFN bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, c
     BSTATC(7, light);
     if (light) pr->dir = biased_pdf_generate<F>(S, rec.p, r.time, ps.rng, dr);
     else pr->dir = lamb ? onb_apply(rec.n, random_cosine_direction_pre(dr.v0, dr.v1)) : random_in_sphere(ps.rng);
+    if (crit && light && light_critical(rec.p, pr->dir)) {  // ends here: retraced with the exact arithmetic
+        *crit = true;
+        *L = f3{0, 0, 0};
+        return true;
+    }
     PH_MARK(ph, 6);
     return false;
 }

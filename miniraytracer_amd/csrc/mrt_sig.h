@@ -674,9 +674,6 @@ MRT_DFN bool cornell_fast_hit(const MRT_CONST_AS LinOp* prog, const Ray& r, floa
 // the kernels that walk the Cornell shape by cornell_fast_hit (the host sizes LDS by it)
 template <uint32_t F>
 static constexpr uint32_t kBox6Walk = (MRT_FAST_BOX && MRT_SIG_OF(F) == SIG_CORNELL && !(F & (FT_UV | FT_MOVING))) ? 1u : 0u;
-// the kernels whose resumable mesh walk runs the two-level nodes (Mesh4; the host sizes LDS by it)
-template <uint32_t F>
-static constexpr uint32_t kMesh4 = (MRT_MESH4 && MRT_SIG_OF(F) == SIG_ROOM_MESH) ? 1u : 0u;
 
 // scene_object::hit for a program of shape SIG (same contract as scene_hit_lin)
 template <uint32_t F>

@@ -9,10 +9,6 @@
 struct SceneTables {
     std::vector<mrt_node> nodes;        // the view's nodes (+ NEEDUV / SLOWDIV flags, fused TRROTY, BVHW roots)
     std::vector<mrtd::MeshWide> wide;   // pod_bvh inner nodes, both child boxes inline
-    std::vector<mrtd::Mesh4> mesh4;     // pod_bvh two levels per node (MRT_MESH4 walks), breadth-first
-    std::vector<mrtd::Mesh4Pair> mesh4p;
-    int max_mesh4 = 0;                  // deepest stack of their walk (per ray octant, every box hit)
-    uint32_t mesh4_all = 0;             // 1: some child box is not inside its parent's (test the parents always)
     std::vector<mrtd::BvhWide> bwide;   // bvh_node subtrees as wide nodes, breadth-first
     std::vector<mrt_node> bprims;       // their leaves' primitive runs
     std::vector<mrtd::DMat> dmats;      // materials (+ inline constant colour, dielectric quotients)

@@ -22,33 +22,6 @@ struct MeshWide {
 };
 #define MESH_LEAF 0x80000000u
 
-// pod_bvh two levels at a time (the resumable room + mesh walk, MRT_MESH4): an inner node N with
-// children A, B holds the four grandchild slots [A.left, A.right, B.left, B.right] -- a leaf child
-// is its own slot 0 / 2 with slot 1 / 3 empty -- with their boxes and refs (leaf -> MESH_LEAF |
-// count << 24 | first, inner -> index into the Mesh4 array), and in meta N's, A's and B's
-// node_order bytes (bits 0-7, 8-15, 16-23) and the slots' valid bits (24-27).  128 B, one cache
-// line, issued as eight 16-B loads together.  Every pod_bvh child box lies inside its parent's
-// (checked on upload, else the walk stays binary), and the slab test is monotone in the box
-// planes, so for a nice ray (mrt_device.h) a slot's box hit implies its parent's: the parents'
-// boxes (Mesh4Pair) are read and tested only when a lane's ray is not nice.
-struct Mesh4 {
-    struct Slot {
-        float lo[3];
-        uint32_t ref;
-        float hi[3];
-        uint32_t meta;  // slot 0: the node's meta word; others 0
-    } s[4];
-};
-struct Mesh4Pair {
-    float amin[3], pad0, amax[3], pad1, bmin[3], pad2, bmax[3], pad3;
-};
-#ifndef MRT_MESH4
-#define MRT_MESH4 0
-#endif
-#ifndef MRT_MESH4_BAR
-#define MRT_MESH4_BAR 1
-#endif
-
 // device material: mrt_material plus, when its texture is a constant colour, that colour inline
 // (one load per shading instead of material -> texture)
 struct DMat {
@@ -160,9 +133,6 @@ struct DScene {
     const mrt_mesh_node* __restrict__ mnodes;
     const MeshWide* __restrict__ mwide;
     uint32_t mwide_n;
-    const Mesh4* __restrict__ mesh4;       // two-level nodes (MRT_MESH4 kernels); MESH node f[11] = root ref
-    const Mesh4Pair* __restrict__ mesh4p;  // their children's boxes (rays that are not nice)
-    uint32_t mesh4_all;                    // 1: test the children's boxes for every ray (a box outside its parent)
     const BvhWide* __restrict__ bwide;
     const mrt_node* __restrict__ bprims;  // leaf primitive runs of the wide subtrees
     const float4* __restrict__ tri_geo;
@@ -551,75 +521,10 @@ MRT_DFN bool mesh_hit(const DScene& S, const mrt_node& n, const Ray& r, float tm
 // tt only -- mesh_hit_rec completes it once the walk is over.  Completed inside the step, the point
 // and normal were carried round every walk step of the wave (the compiler copied all six registers
 // in and out of each step's branches).
-// W4 (with DEFER): ref walks the Mesh4 array instead -- an inner step tests a node's four
-// grandchild slots and goes to the first hit one in the reference's visit order (N's closer child
-// first, inside it that child's closer child first), pushing the other hit slots farthest first:
-// the leaves are visited in mesh_hit's order and every box test has mesh_hit's (tmin, tmax), so
-// the results are the same bits in half the inner steps.
-template <bool TREE = false, bool DEFER = false, bool W4 = false>
+template <bool TREE = false, bool DEFER = false>
 MRT_DFN uint32_t mesh_step(const DScene& S, const mrt_node& n, const Ray& r, float tmin, float& tt, HitRec& rec,
                                               const LStack& L, uint32_t& ref, uint32_t& msp, bool& in_hit) {
-    static_assert(!W4 || (DEFER && !TREE), "two-level walk: the deferred, treelet-free step");
-    if constexpr (W4) {
-        uint32_t res = 0u;
-        bool pop;
-        if (ref & MESH_LEAF) {
-            const uint32_t first = ref & 0xFFFFFFu, cnt = (ref >> 24) & 0x7Fu;
-            float t = 0.0f, uu = 0.0f, vv = 0.0f;
-            const bool h = cnt > 0 && tri_hit(S, first, r, tmin, tt, &t, &uu, &vv);
-            in_hit = in_hit || h;
-            tt = h ? t : tt;
-            rec.mat = h ? first : rec.mat;
-            rec.u = h ? uu : rec.u;
-            rec.v = h ? vv : rec.v;
-            const bool more = cnt > 1;
-            ref = more ? (MESH_LEAF | ((cnt - 1) << 24) | (first + 1)) : ref;
-            res = (!more && in_hit) ? 1u : 0u;
-            pop = !more && !in_hit;
-        } else {
-            const float4* q = reinterpret_cast<const float4*>(S.mesh4 + ref);
-            float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4], q5 = q[5], q6 = q[6], q7 = q[7];
-#if defined(__HIP_DEVICE_COMPILE__) && MRT_MESH4_BAR
-            asm volatile("" : "+v"(q0.x), "+v"(q0.y), "+v"(q0.z), "+v"(q0.w), "+v"(q1.x), "+v"(q1.y), "+v"(q1.z), "+v"(q1.w));
-            asm volatile("" : "+v"(q2.x), "+v"(q2.y), "+v"(q2.z), "+v"(q2.w), "+v"(q3.x), "+v"(q3.y), "+v"(q3.z), "+v"(q3.w));
-            asm volatile("" : "+v"(q4.x), "+v"(q4.y), "+v"(q4.z), "+v"(q4.w), "+v"(q5.x), "+v"(q5.y), "+v"(q5.z), "+v"(q5.w));
-            asm volatile("" : "+v"(q6.x), "+v"(q6.y), "+v"(q6.z), "+v"(q6.w), "+v"(q7.x), "+v"(q7.y), "+v"(q7.z), "+v"(q7.w));
-#endif
-            const uint32_t meta = __float_as_uint(q1.w);
-            bool h0 = (meta & (1u << 24)) && aabb_hit(ld3(q0), ld3(q1), r, tmin, tt);
-            bool h1 = (meta & (1u << 25)) && aabb_hit(ld3(q2), ld3(q3), r, tmin, tt);
-            bool h2 = (meta & (1u << 26)) && aabb_hit(ld3(q4), ld3(q5), r, tmin, tt);
-            bool h3 = (meta & (1u << 27)) && aabb_hit(ld3(q6), ld3(q7), r, tmin, tt);
-            if (__builtin_expect(any_lane(!r.nice) || S.mesh4_all, 0)) {  // the children's own box tests (see Mesh4)
-                const Mesh4Pair& P = S.mesh4p[ref];
-                const bool skip = r.nice && !S.mesh4_all;
-                const bool ha = skip || aabb_hit(P.amin, P.amax, r, tmin, tt);
-                const bool hb = skip || aabb_hit(P.bmin, P.bmax, r, tmin, tt);
-                h0 = h0 && ha;
-                h1 = h1 && ha;
-                h2 = h2 && hb;
-                h3 = h3 && hb;
-            }
-            const uint32_t r0 = __float_as_uint(q0.w), r1 = __float_as_uint(q2.w), r2 = __float_as_uint(q4.w);
-            const uint32_t r3 = __float_as_uint(q6.w);
-            const bool nl = (meta & r.mask) != 0, al = ((meta >> 8) & r.mask) != 0, bl = ((meta >> 16) & r.mask) != 0;
-            // the pairs in their own closer-first order, then the closer pair first
-            const bool ha0 = al ? h0 : h1, ha1 = al ? h1 : h0, hb0 = bl ? h2 : h3, hb1 = bl ? h3 : h2;
-            const uint32_t ra0 = al ? r0 : r1, ra1 = al ? r1 : r0, rb0 = bl ? r2 : r3, rb1 = bl ? r3 : r2;
-            const bool v0 = nl ? ha0 : hb0, v1 = nl ? ha1 : hb1, v2 = nl ? hb0 : ha0, v3 = nl ? hb1 : ha1;
-            const uint32_t w0 = nl ? ra0 : rb0, w1 = nl ? ra1 : rb1, w2 = nl ? rb0 : ra0, w3 = nl ? rb1 : ra1;
-            if (v3 && (v0 || v1 || v2)) L.mesh[(msp++) * 64 + L.lane] = w3;
-            if (v2 && (v0 || v1)) L.mesh[(msp++) * 64 + L.lane] = w2;
-            if (v1 && v0) L.mesh[(msp++) * 64 + L.lane] = w1;
-            ref = v0 ? w0 : v1 ? w1 : v2 ? w2 : v3 ? w3 : ref;
-            pop = !(v0 || v1 || v2 || v3);
-        }
-        if (pop) {
-            if (msp == 0) res = 2u;
-            else ref = L.mesh[(--msp) * 64 + L.lane];
-        }
-        return res;
-    } else if constexpr (DEFER) {
+    if constexpr (DEFER) {
         // the same step with the walk state updated by selects where mesh_step branches and
         // returns: each branch's results otherwise merged in copies of every state register
         uint32_t res = 0u;

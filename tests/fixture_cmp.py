@@ -9,6 +9,7 @@ Two fixture shapes:
   shipped_full_<id>.npz  C3 / C4 / C5 at full resolution: a 32x32 grid of block means, channel means,
                          a band of rows and a seeded pixel sample; per-pixel RMSE over band + sample
   shipped_ownspp_<id>.npz  C3 / C4 / C5 at their own spp, a pixel list only (compare_pixels)
+  shipped_ownspp_full_9.npz  C3 at its own spp (4096), the whole 800x800 image
 """
 import os
 
@@ -46,8 +47,14 @@ def compare(img, rays, path):
         out["over"] = f"all {w * h} pixels"
         b = 25
         bm = im.reshape(h // b, b, w // b, b, 3).mean(axis=(1, 3), dtype=np.float64)
-        out["block_rmse"] = _rmse(bm, g["block_mean"])
+        rbm = g["block_mean"] if "block_mean" in g.files else ref.reshape(h // b, b, w // b, b, 3).mean(axis=(1, 3), dtype=np.float64)
+        out["block_rmse"] = _rmse(bm, rbm)
         out["block"] = f"{b}x{b} px"
+        # where the squared error sits: the share of the ten largest pixels
+        e2 = ((im.astype(np.float64) - ref) ** 2).sum(axis=-1).ravel()
+        top = np.argsort(e2)[::-1][:10]
+        out["top10_share"] = float(e2[top].sum() / max(e2.sum(), 1e-300))
+        out["top10"] = [[int(i % w), int(i // w), float(np.sqrt(e2[i] / 3))] for i in top]
     else:  # band + sample
         r0, r1 = (int(x) for x in g["band_rows"])
         flat = im.reshape(-1, 3)
@@ -59,7 +66,8 @@ def compare(img, rays, path):
         bm = im[:bh * gg, :bw * gg].reshape(gg, bh, gg, bw, 3).mean(axis=(1, 3), dtype=np.float64)
         out["block_rmse"] = _rmse(bm, g["block_mean"])
         out["block"] = f"{bh}x{bw} px"
-    out["mean_delta"] = float(np.abs(im.reshape(-1, 3).mean(axis=0, dtype=np.float64) - g["mean"]).max())
+    gmean = g["mean"] if "mean" in g.files else g["image"].reshape(-1, 3).mean(axis=0, dtype=np.float64)
+    out["mean_delta"] = float(np.abs(im.reshape(-1, 3).mean(axis=0, dtype=np.float64) - gmean).max())
     return out
 
 

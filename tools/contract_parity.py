@@ -30,6 +30,18 @@ for num in sys.argv[1:] or ["fast"]:
     print(json.dumps({"tag": tag, "numerics": num, "config": "C2", "kernel_ms": round(float(np.median(ms)), 3),
                       "grays": round(rays / np.median(ms) / 1e6, 2), **c}), flush=True)
     r.close()
+    # C3 over the whole image at its own spp (shipped_ownspp_full_9.npz); images kept for analysis
+    g = os.path.join(G, "shipped_ownspp_full_9.npz")
+    _, w, h, spp, depth = (int(x) for x in np.load(g)["meta"])
+    r = m.Renderer(m.select_scene(9, w / h), 0)
+    img, rays = r.render(m.render_desc(w, h, spp, depth=depth, numerics=num))
+    t, n = r.kernel_ms()
+    c = compare(img, rays, g)
+    if os.environ.get("MRT_PARITY_SAVE"):
+        np.save(os.path.join(os.environ["MRT_PARITY_SAVE"], f"c3full_{tag}_{num}.npy"), img[..., :3])
+    print(json.dumps({"tag": tag, "numerics": num, "config": "C3 whole image", "kernel_ms": round(t, 3),
+                      "grays": round(rays / t / 1e6, 2), **c}), flush=True)
+    r.close()
     for sid in (9, 8, 7):
         g = np.load(os.path.join(G, f"shipped_ownspp_{sid}.npz"))
         _, w, h, spp, depth = (int(x) for x in g["meta"])

@@ -24,6 +24,7 @@ Fixtures (all small; data only -- inputs and expected outputs):
   shipped_ownspp_<id>.npz C3 / C4 / C5 at their OWN spp (4096, 2025, 8100): the reference as shipped
                           on a pixel list (a row band + seeded pixels), values + the list's ray total
                           (`--only-ownspp`; OWNSPP)
+  shipped_ownspp_full_9.npz  C3 at its own spp (4096), the WHOLE 800x800 image (`--only-fullown`)
   refseq_<id>_m<mode>.npz the exact reference build with -threads 1 (its own deterministic mode:
                           one worker PCG stream, work_queue tile order), image + G_rayCounter
                           (`--only-refseq`)
@@ -177,6 +178,25 @@ def ownspp(tmp, only=None, threads=8):
         print("shipped own-spp", sid, w, h, spp, px.size, meta, flush=True)
 
 
+# C3 at its own spp over the WHOLE image (round 5): the pixel list of OWNSPP holds 9.5% of C3's
+# pixels, and its error is carried by a handful of caustic pixels, so a subset does not bound the
+# image.  The full 800x800x4096 render of the reference as shipped, stream-matched (~7.2 G rays,
+# minutes on the container's cores), kept whole: 640 k float3 pixels.
+FULLOWN = [(9, 800, 800, 4096)]
+
+
+def fullown(tmp, only=None, threads=8):
+    img = os.path.join(tmp, "fo.pfm")
+    for sid, w, h, spp in FULLOWN:
+        if only is not None and sid not in only:
+            continue
+        meta = json.loads(run(SHIPPED, ["--h-mode", "stream", "-width", w, "-height", h, "-samples", spp, "-depth", 32,
+                                        "--h-threads", threads, "--h-out", img] + scene_args(sid)))
+        np.savez_compressed(os.path.join(OUT, f"shipped_ownspp_full_{sid}.npz"), image=read_pfm(img, w, h),
+                            rays=np.array([meta["rays"]], dtype=np.int64), meta=np.array([sid, w, h, spp, 32], dtype=np.int64))
+        print("shipped own-spp whole image", sid, w, h, spp, meta, flush=True)
+
+
 # the reference's own deterministic mode: -threads 1, one worker stream, work_queue tile order
 # (scene id, width, height, samples, depth, tile size); both -mode 0 (draw) and -mode 1 (draw2)
 REFSEQ_CASES = [(0, 60, 30, 16, 8, 16), (5, 48, 40, 16, 32, 16), (7, 40, 40, 4, 32, 16), (8, 40, 40, 9, 32, 16)]
@@ -204,6 +224,11 @@ def main():
         only = [int(a) for a in os.environ.get("MRT_FULLRES_SCENES", "").split(",") if a]
         with tempfile.TemporaryDirectory() as tmp:
             ownspp(tmp, only or None, int(os.environ.get("MRT_FULLRES_THREADS", "8")))
+        return
+    if "--only-fullown" in sys.argv:
+        only = [int(a) for a in os.environ.get("MRT_FULLRES_SCENES", "").split(",") if a]
+        with tempfile.TemporaryDirectory() as tmp:
+            fullown(tmp, only or None, int(os.environ.get("MRT_FULLRES_THREADS", "8")))
         return
     if "--only-fullres" in sys.argv:
         only = [int(a) for a in os.environ.get("MRT_FULLRES_SCENES", "").split(",") if a]

@@ -100,15 +100,12 @@ def main():
             grid_waves = None
         res["sq_wave_check"].append({"dispatch": int(did), "kernel": k, "SQ_WAVES": c.get("SQ_WAVES"), "grid_waves": grid_waves})
     for k in fetch:
-        split = "mrt_wf_" in k  # the split form's hit / shade kernels: one launch pair per segment
-        if not (k.startswith("mrt_path_kernel") or split):
+        if not k.startswith("mrt_path_kernel"):
             continue
         e = {"launches": n_f[k], "dispatch": meta[k], "rays_per_launch": rays_per_launch, "FETCH_SIZE_KiB": fetch[k].get("FETCH_SIZE"),
              "WRITE_SIZE_KiB": write.get(k, {}).get("WRITE_SIZE")}
         e["hbm_bytes_per_launch"] = 2 * e["FETCH_SIZE_KiB"] * 1024 + (e["WRITE_SIZE_KiB"] or 0) * 1024
-        if split:  # per-launch means; rays are per step, not per launch: no per-ray figures
-            e["rays_per_launch"] = None
-        elif rays_per_launch:
+        if rays_per_launch:
             e["hbm_bytes_per_ray"] = e["hbm_bytes_per_launch"] / rays_per_launch
             e["write_bytes_per_ray"] = (e["WRITE_SIZE_KiB"] or 0) * 1024 / rays_per_launch
         if k in avg_ns:
@@ -118,7 +115,7 @@ def main():
         s = sq.get(k)
         if s:
             e["sq"] = s
-            if rays_per_launch and not split:
+            if rays_per_launch:
                 e["valu_insts_per_ray"] = s["SQ_INSTS_VALU"] / rays_per_launch
             if s.get("SQ_ACTIVE_INST_VALU"):
                 e["valu_lane_util"] = s["SQ_THREAD_CYCLES_VALU"] / (64.0 * s["SQ_ACTIVE_INST_VALU"])
