@@ -100,6 +100,10 @@ def parse():
                     help="skip timing the general hit walk (MRT_NO_SIG=1: the linear-program interpreter) "
                          "beside a shape-specialised one")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--step-times", action="store_true",
+                    help="record a HIP event after every timed step (on its stream) and report the per-step "
+                         "completion intervals (median / p90 / max and where the max fell): tells a whole-run "
+                         "slowdown (clock) from single-step stalls (rehearsal diagnosis)")
     return ap.parse_args()
 
 
@@ -405,6 +409,7 @@ def main():
             print(f"bench.py: {msg} ({time.strftime('%H:%M:%S')})", file=sys.stderr, flush=True)
 
     live = [None]  # (path-kernel ms per launch, launches per render) of the last measure()
+    step_times = [None]  # --step-times: the timed steps' completion intervals
 
     def measure(d):
         """W untimed warmup steps, then EXACTLY K steps between barrier + synchronize on both
@@ -435,9 +440,14 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
         note("timed steps")
+        evs = []
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step(d)
+            if args.step_times:
+                e = torch.cuda.Event(enable_timing=True)
+                e.record(streams[(it[0] - 1) % npipe])
+                evs.append(e)
         drain()
         torch.cuda.synchronize(dev)
         if world > 1:
@@ -449,6 +459,11 @@ def main():
         # parity check ran on a GPU that had idled for seconds, 8.6-9.0 ms against 8.0 ms)
         kl = [c.kernel_ms() for c in ctx[0][:min(npipe, max(args.steps, 1))]]
         live[0] = (float(np.mean([ms / max(n, 1) for ms, n in kl])), max(kl[0][1], 1))
+        if len(evs) > 1:  # completion intervals of consecutive steps
+            iv = np.array([evs[i - 1].elapsed_time(evs[i]) for i in range(1, len(evs))])
+            step_times[0] = {"median_ms": round(float(np.median(iv)), 4), "p90_ms": round(float(np.percentile(iv, 90)), 4),
+                             "max_ms": round(float(iv.max()), 4), "max_at_step": int(iv.argmax()) + 1,
+                             "mean_ms": round(float(iv.mean()), 4), "intervals": len(iv)}
         elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
         total_rays = rays.clone()
         if world > 1:
@@ -564,6 +579,8 @@ def main():
         }
         if verified is not None:
             res["verify_bit_exact"] = verified
+        if step_times[0] is not None:
+            res["step_times"] = step_times[0]
         if world == 1 and not args.no_cpu_baseline:
             try:
                 res["cpu_baseline"] = cpu_baseline(args)

@@ -184,6 +184,11 @@ mrt_status mrt_kernel_ms(mrt_scene* s, float* path_ms, uint32_t* launches);
 #define MRT_BUILD_PATH_EXACT 3u
 typedef struct mrt_kernel_info {
     uint32_t features, kernel_features, lds_bytes, grid, prog_ops, vgprs, wg, tree_nodes, build;
+    /* handed_over: paths the fast-arithmetic kernels listed for the exact arithmetic since the
+       scene's upload (rounding-critical light samples) -- reading it waits
+       for the scene's renders; pad: 0 */
+    uint32_t pad;
+    uint64_t handed_over;
 } mrt_kernel_info;
 mrt_status mrt_scene_kernel_info(const mrt_scene* s, mrt_kernel_info* out);
 

@@ -62,7 +62,8 @@ class MrtSceneView(C.Structure):
 class KernelInfo(C.Structure):
     _fields_ = [("features", C.c_uint32), ("kernel_features", C.c_uint32), ("lds_bytes", C.c_uint32),
                 ("grid", C.c_uint32), ("prog_ops", C.c_uint32), ("vgprs", C.c_uint32), ("wg", C.c_uint32),
-                ("tree_nodes", C.c_uint32), ("build", C.c_uint32)]
+                ("tree_nodes", C.c_uint32), ("build", C.c_uint32), ("pad", C.c_uint32),
+                ("handed_over", C.c_uint64)]
 BUILDS = ("exact", "fast", "fastz", "pex")  # MRT_BUILD_*: the kernel build (mrt_path_kernel[_fast|_fastz|_pex])
 
 

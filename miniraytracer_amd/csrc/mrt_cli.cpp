@@ -3,8 +3,10 @@
 // MI355X(s) through the C-ABI, prints the reference's "Trace: ... Mrays/s" line (main.cpp:403-406)
 // and writes the image (-o out.pfm: linear; -o out.ppm: Drago tone map, main.cpp:416-444).
 //
-// -gpus N shards the work_queue tiles over N GPUs (one host thread per device, the tiles dealt in
-// permuted rounds of N, mrt_local_pixels); 0 = every visible GPU.  -backend cpu renders on the host instead (the CPU backend: the
+// -gpus N shards the work_queue tiles over N ranks (one host thread per rank, the tiles dealt in
+// permuted rounds of N, mrt_local_pixels); 0 = every visible GPU.  Rank r renders on GPU r % (GPUs
+// visible): with fewer GPUs than ranks several ranks share a device (the multi-rank assembly runs
+// on one GPU as on eight); with -backend cpu each rank is a CPU-backend context of -threads workers.  -backend cpu renders on the host instead (the CPU backend: the
 // same hot-path code compiled for the host, exact contract), with -threads worker threads as the
 // reference's -threads (0 = every core).  -numerics exact|fast picks the GPU's arithmetic contract.
 #include <chrono>
@@ -38,20 +40,18 @@ int main(int argc, char** argv) {
     mrt_scene_blob_view(blob, &view);
 
     const bool cpu = p.backend == 1;
-    int ndev = 0, world = 1;
+    int ndev = 0, world = p.gpus ? (int)p.gpus : 1;
     if (!cpu) {
         if ((st = mrt_init(&ndev))) return fail("mrt_init", st);
-        world = p.gpus ? (int)p.gpus : ndev;
-        if (world > ndev) {
-            fprintf(stderr, "-gpus %u: only %d GPU(s) visible\n", p.gpus, ndev);
-            return 1;
-        }
+        if (ndev < 1) return fail("mrt_init", MRT_ERR_NO_DEVICE);
+        if (!p.gpus) world = ndev;
+        if (world > ndev) fprintf(stderr, "-gpus %d: %d rank(s) on %d visible GPU(s)\n", world, world, ndev);
     }
 
     std::vector<mrt_scene*> scenes(world, nullptr);
     std::vector<mrt_render_desc> descs(world);
     for (int r = 0; r < world; r++) {
-        if ((st = mrt_scene_upload(cpu ? MRT_DEVICE_CPU : r, &view, &scenes[r]))) return fail("scene_upload", st);
+        if ((st = mrt_scene_upload(cpu ? MRT_DEVICE_CPU : r % ndev, &view, &scenes[r]))) return fail("scene_upload", st);
         mrt_default_render_desc(&p, &descs[r]);
         descs[r].rank = (uint32_t)r;
         descs[r].world = (uint32_t)world;
@@ -60,6 +60,10 @@ int main(int argc, char** argv) {
     if (descs[0].flags & MRT_RF_REF_ORDER) {  // main.cpp:338-366: the workers' (initstate, initseq)
         if (!cpu) {
             fprintf(stderr, "-order ref: the reference's per-thread RNG order runs on the CPU backend only (-backend cpu)\n");
+            return 1;
+        }
+        if (world > 1) {
+            fprintf(stderr, "-order ref: the reference's per-thread RNG order is one rank's (use -order path with -gpus)\n");
             return 1;
         }
         const uint32_t n = p.num_threads ? p.num_threads : std::max(1u, std::thread::hardware_concurrency());
@@ -86,9 +90,11 @@ int main(int argc, char** argv) {
     if (cpu) {
         mrt_kernel_info ki{};
         mrt_scene_kernel_info(scenes[0], &ki);
-        snprintf(where, sizeof where, "CPU, %u threads", ki.grid);
-    } else {
+        snprintf(where, sizeof where, "CPU, %d x %u threads", world, ki.grid);
+    } else if (world <= ndev) {
         snprintf(where, sizeof where, "%d x MI355X", world);
+    } else {
+        snprintf(where, sizeof where, "%d ranks on %d x MI355X", world, ndev);
     }
     printf("MiniRayTracer - Scene: %.0fms - Trace: %.2fs - %.3f Mrays/s | %.3f us/ray  [%s, %u spp, %s numerics]\n", gen_ms,
            secs, (total * 0.000001) / secs, (secs * 1000000.0) / (double)total, where, descs[0].sqrt_samples * descs[0].sqrt_samples,

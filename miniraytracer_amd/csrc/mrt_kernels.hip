@@ -162,18 +162,6 @@ template <uint32_t F> struct PathLevLds {
 #ifndef MRT_PATHQ
 #define MRT_PATHQ MRT_FAST
 #endif
-// pixel sums (mrt_psum.h): in the forward-fold builds (tolerance contract); MRT_PSUM=0 builds them out
-#ifndef MRT_PSUM
-#define MRT_PSUM 1
-#endif
-static constexpr bool kPsum = MRT_PSUM && MRT_FWD_FOLD;
-// ... compiled only into the bvh_node (treelet) kernels: measured there book2 (C5) -6% per render;
-// in the Cornell kernel its code spilled 27 VGPRs at 7 waves per SIMD (C2 kernel 8.8 -> 21 ms; a
-// first form with one sum per slot: +10%, 64-bit LDS atomics of most of a wave on one address),
-// and in the mesh kernels its LDS cost a resident wave (teapot -11%, bunny -24%) -- both keep the
-// per-path radiance buffer and the fold ("Pixel sums")
-template <uint32_t F>
-static constexpr bool kPsumF = kPsum && TreeOf<F>::on && (F & FT_LIN) != 0;  // (not the generic machine: 128 -> 140 VGPRs)
 // rounding-critical light samples handed to the exact arithmetic (mrt_shade.h light_critical): the
 // fast-arithmetic builds' light-sampled variants (MRT_CRIT=0 builds it out: A/B)
 #ifndef MRT_CRIT
@@ -193,7 +181,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
     // per wave: its stacks and queues ([slot][word][lane])
-    const uint32_t words = (P.lds_frames * 2 + P.lds_rays * 11 + P.lds_mesh + P.lds_save + LK * 4 + PathQ<F>::words + P.lds_psum) * 64;
+    const uint32_t words = (P.lds_frames * 2 + P.lds_rays * 11 + P.lds_mesh + P.lds_save + LK * 4 + PathQ<F>::words) * 64;
     uint32_t* wb = lds + wave * words;
     uint32_t* const wmesh = wb + P.lds_frames * 128 + P.lds_rays * 704;
     float4* tree = nullptr;
@@ -208,14 +196,8 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                     TreeOf<F>::on ? P.tree_n : 0u};
     // the wave's queue of path starts ([word][entry], PathQ): after the fold levels
     float* const Lq = (float*)(wmesh + (P.lds_mesh + P.lds_save + LK * 4) * 64);
-    // the wave's pixel-sum slots (mrt_psum.h): after the queue
-    uint32_t* const Lsum = wmesh + (P.lds_mesh + P.lds_save + LK * 4 + PathQ<F>::words) * 64;
-    const bool psum = kPsumF<F> && P.psum.acc != nullptr;  // wave-uniform
-    if (psum) psum_init(Lsum, lane);
-    // hand rounding-critical paths over (while the list has room: half of it, read once per wave)
-    const bool flag = kCrit<F> && P.psum.rt != nullptr &&
-                      (uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(P.psum.rt_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) <
-                          P.psum.rt_cap / 2u;
+    // list rounding-critical paths for the exact arithmetic (wave-uniform)
+    const bool flag = kCrit<F> && P.rt.idx != nullptr;
     const DScene& S = P.sc;
     const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const LevStore<LK> lev{(MRT_GLOBAL_AS v4f*)P.lev, P.lev_rows, (uint32_t)slot,
@@ -392,30 +374,16 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
         }
         PH_MARK(ph, 4);
     };
-    // pixel sums: the path's radiance into its pixel's sum (mrt_psum.h)
-    auto psum_path = [&](f3 L) {
-        uint32_t lp, sl;
-        path_coords(P, idx, &lp, &sl);
-        psum_add(Lsum, P.psum, lp, P.s0 + sl, L, lane);
-    };
-    // a rounding-critical path: listed for the retrace kernel, no contribution, no rays counted
-    auto retrace_path = [&]() {
-        uint32_t lp, sl;
-        path_coords(P, idx, &lp, &sl);
-        const uint32_t k = atomicAdd(P.psum.rt_n, 1u);
-        if (k < P.psum.rt_cap) P.psum.rt[k] = make_uint2(lp, P.s0 + sl);
-        active = false;
+    // a rounding-critical path (its light sample this bounce): listed for the retrace kernel, which
+    // replaces its radiance; the path itself goes on here (its rays are counted here)
+    auto list_critical = [&]() {
+        const uint32_t k = atomicAdd(P.rt.n, 1u);
+        if (k < P.rt.cap) P.rt.idx[k] = idx;
     };
     // a finished path: the recursion's fold, radiance out (sample-major, coalesced), rays counted
     auto finish_path = [&](f3 L) {
         L = end_path(ps, lev, L);
         PH_MARK(ph, 5);
-        if (psum) {
-            psum_path(L);
-            done_rays += ps.rays();
-            active = false;
-            return;
-        }
         float* dst = P.rad + (size_t)idx * 3;
 #if defined(MRT_EXPERIMENTS) && defined(MRT_EXP_NOSTORE)  // experiment: what the radiance store costs
         if (__float_as_uint(L.x) == 0x7fc00123u) {
@@ -471,15 +439,13 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                         dst[2] = st_v.z;
                     }
                     st_pend = false;
-                }, flag ? &crit : nullptr);
+                }, &crit, flag);
                 PH_MARK(ph, 2);
-                if (crit) {
-                    retrace_path();
-                } else if (ended) {
+                if (crit) list_critical();
+                if (ended) {
                     st_v = end_path(ps, lev, L);
-                    if (psum) psum_path(st_v);
                     st_off = idx * 12u;
-                    st_pend = !psum;
+                    st_pend = true;
                     if (P.path_rays) P.path_rays[idx] = ps.rays();
                     done_rays += ps.rays();
                     active = false;
@@ -652,13 +618,11 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                 }
                 f3 L{0.0f, 0.0f, 0.0f};
                 bool crit = false;
-                const bool ended = shade_hit<F, LK>(S, ps, P.max_bounces, lev, w.hnode != MRT_NONE, rec, &L, ph, flag ? &crit : nullptr);
+                const bool ended = shade_hit<F, LK>(S, ps, P.max_bounces, lev, w.hnode != MRT_NONE, rec, &L, ph, &crit, flag);
                 PH_MARK(ph, 2);
                 phase = PH_BEGIN;
-                if (crit) {
-                    retrace_path();
-                    phase = 0;
-                } else if (ended) {
+                if (crit) list_critical();
+                if (ended) {
                     finish_path(L);
                     phase = 0;
                 }
@@ -673,10 +637,10 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
             if (active) {
                 f3 L{0.0f, 0.0f, 0.0f};
                 bool crit = false;
-                const bool ended = trace_segment<F, LK>(S, ps, P.max_bounces, lev, Ls, &L, ph, flag ? &crit : nullptr);
+                const bool ended = trace_segment<F, LK>(S, ps, P.max_bounces, lev, Ls, &L, ph, &crit, flag);
                 PH_MARK(ph, 2);
-                if (crit) retrace_path();
-                else if (ended) finish_path(L);
+                if (crit) list_critical();
+                if (ended) finish_path(L);
             }
             PH_MARK(ph, 3);
         }
@@ -700,27 +664,21 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
         }
     }
 #endif
-    if (psum) psum_drain(Lsum, P.psum, lane);
     // one 64-bit add per wave
     uint64_t my = done_rays;
     for (int off = 32; off > 0; off >>= 1) my += __shfl_xor(my, off);
     if (lane == 0 && my) atomicAdd(P.rays, (unsigned long long)my);
 }
 
-// The exact arithmetic (the path-exact build: the reference's, forward fold) for two small jobs of a
-// pixel-sum render (mrt_psum.h), one path per lane from its camera ray to its end:
-//   phase 0: the paths the fast-arithmetic kernels handed over (mrt_shade.h light_critical;
-//            PsumOut::rt): each traced as the reference traces it -- including its non-finite end
-//            -- its radiance added to the pixel's sums, its rays to the ray total;
-//   phase 1: for each listed non-finite sample (PsumOut::nf), the finite samples of its pixel ahead
-//            of it, summed in fixed point (integer sums: no order) -- the running colour
-//            main.cpp:162-164 doubles there (psum_color);
-//   phase 2: the handed-over paths of one launch of a per-path render (no pixel sums): each
-//            path's radiance into its slot of the radiance buffer, where the fold finds it (and
-//            doubles the running colour itself if it is non-finite); the last group clears the list.
-// A few thousand paths per render: one-wave groups over the lists, no regeneration.
+// The exact arithmetic (the path-exact build: the reference's, forward fold) for the paths a
+// fast-arithmetic launch listed as rounding-critical (mrt_shade.h light_critical; PathParams::rt):
+// each traced from its camera ray to its end as the reference traces it -- including its
+// non-finite end, which the fold then turns into main.cpp:162-164's doubling -- and its radiance
+// written over the fast one in the launch's radiance buffer, before the fold.  A few hundred to a
+// few thousand paths per launch: one-wave groups over the list, one path per lane; the last group
+// to finish clears the list for the next launch.  (The launch's ray count stays the fast paths'.)
 template <uint32_t F>
-static constexpr bool kRetrace = MRT_TABLE_PEX && kPsum;
+static constexpr bool kRetrace = MRT_TABLE_PEX && MRT_FWD_FOLD && (F & FT_BIASED) != 0 && !kPathExact<F>;
 #if MRT_TABLE_PEX
 template <uint32_t F>
 __global__ void __launch_bounds__(64) mrt_retrace_kernel(PathParams P) {
@@ -732,11 +690,15 @@ __global__ void __launch_bounds__(64) mrt_retrace_kernel(PathParams P) {
     const LevStore<0> lev{nullptr, 0u, 0u, 0u};
     const DScene& S = P.sc;
     PhaseClock ph{};
-    // (inlined at both call sites: as a real function its scalar scene loads became VGPR values)
-    auto trace_path = [&](uint32_t lp, uint32_t s, uint32_t* rays) __attribute__((always_inline)) -> f3 {
+    const uint32_t n = min(__hip_atomic_load(P.rt.n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), P.rt.cap);
+    if (blockIdx.x == 0 && lane == 0 && n) atomicAdd(P.rt.total, (unsigned long long)n);
+    for (uint32_t i = blockIdx.x * 64u + lane; i < n; i += gridDim.x * 64u) {
+        const uint32_t idx = P.rt.idx[i];
+        uint32_t lp, sl;
+        path_coords(P, idx, &lp, &sl);
         PathState ps;
         float u, v;
-        path_key_at(P, lp, s, ps.rng, &u, &v);
+        path_key_at(P, lp, P.s0 + sl, ps.rng, &u, &v);
         ps.r = camera_ray(S, ps.rng, u, v);
         ps.depth = 0;
         ps.nlev = 0;
@@ -744,51 +706,15 @@ __global__ void __launch_bounds__(64) mrt_retrace_kernel(PathParams P) {
         f3 L{0.0f, 0.0f, 0.0f};
         while (!trace_segment<F, 0>(S, ps, P.max_bounces, lev, Ls, &L, ph)) {
         }
-        *rays = ps.rays();
-        return end_path(ps, lev, L);
-    };
-    if (P.retrace_phase != 1) {
-        const uint32_t n = min(__hip_atomic_load(P.psum.rt_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), P.psum.rt_cap);
-        uint64_t rays = 0;
-        for (uint32_t i = blockIdx.x * 64u + lane; i < n; i += gridDim.x * 64u) {
-            const uint2 e = P.psum.rt[i];
-            uint32_t nr = 0;
-            const f3 L = trace_path(e.x, e.y, &nr);
-            if (P.retrace_phase == 0) {
-                psum_add_global(P.psum, e.x, e.y, L);
-            } else {  // the path's slot of this launch's radiance buffer ([s - s0][local pixel])
-                float* dst = P.rad + ((size_t)(e.y - P.s0) * P.npix + e.x) * 3u;
-                dst[0] = L.x;
-                dst[1] = L.y;
-                dst[2] = L.z;
-            }
-            rays += nr;
-        }
-        for (int off = 32; off > 0; off >>= 1) rays += __shfl_xor(rays, off);
-        if (lane == 0 && rays) atomicAdd(P.rays, (unsigned long long)rays);
-        if (P.retrace_phase == 2 && lane == 0 && atomicAdd(P.psum.rt_done, 1u) == gridDim.x - 1u) {
-            atomicExch(P.psum.rt_n, 0u);  // every group has read the count: the list is empty for the next launch
-            atomicExch(P.psum.rt_done, 0u);
-        }
-    } else {
-        // flat over (entry, sample): lane work f -> entry f / ns, sample f % ns, traced when ahead of
-        // the entry's own sample; its fixed-point sums added to the entry's (integer atomics: no order)
-        const uint32_t m = min(__hip_atomic_load(P.psum.nf_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), P.psum.nf_cap);
-        const uint64_t total = (uint64_t)m * P.ns;
-        for (uint64_t f = (uint64_t)blockIdx.x * 64u + lane; f < total; f += (uint64_t)gridDim.x * 64u) {
-            const uint32_t j = (uint32_t)(f / P.ns), sp = (uint32_t)(f - (uint64_t)j * P.ns);
-            const uint2 e = P.psum.nf[j];
-            if (sp >= e.y) continue;
-            uint32_t nr = 0;
-            const f3 L = trace_path(e.x, sp, &nr);
-            if (finite3(L)) {
-                unsigned long long* q = P.psum.nfp + (size_t)j * 4u;
-                atomicAdd(q + 0, (unsigned long long)psum_fx(L.x));
-                atomicAdd(q + 1, (unsigned long long)psum_fx(L.y));
-                atomicAdd(q + 2, (unsigned long long)psum_fx(L.z));
-                atomicAdd(q + 3, 1ull);
-            }
-        }
+        L = end_path(ps, lev, L);
+        float* dst = P.rad + (size_t)idx * 3u;
+        dst[0] = L.x;
+        dst[1] = L.y;
+        dst[2] = L.z;
+    }
+    if (lane == 0 && atomicAdd(P.rt.done, 1u) == gridDim.x - 1u) {
+        atomicExch(P.rt.n, 0u);  // every group has read the count: the list is empty for the next launch
+        atomicExch(P.rt.done, 0u);
     }
 }
 #endif
@@ -823,7 +749,6 @@ static KernelTable make_table(const char* numerics, std::index_sequence<I...>) {
                        {PathQ<kVariants[I]>::words...},
                        {kBox6Walk<kVariants[I]>...},
                        {(uint32_t)(kLinSlabOps<kVariants[I]> && MRT_SIG_OF(kVariants[I]) == SIG_NONE)...},
-                       {(uint32_t)kPsumF<kVariants[I]>...},
                        {kfn_retrace<kVariants[I]>()...}};
 }
 #if MRT_TABLE_PEX

@@ -4,7 +4,7 @@
 // FMA contraction, hardware reciprocal/sqrt, f32 transcendentals).  DESIGN.md "Numerics contracts".
 #pragma once
 #include <hip/hip_runtime.h>
-#include "mrt_psum.h"
+#include "mrt_shade.h"
 
 namespace mrtd {
 
@@ -43,31 +43,23 @@ struct PathParams {
     uint32_t walk_min;                    // resumable mesh walk: yield once at most this many lanes walk
     const float4* tree_src;               // TreeOf<F>::on kernels: BvhWide nodes copied to LDS at start
     uint32_t tree_n;                      // how many (the first tree_n of the breadth-first array)
-    // pixel sums (mrt_psum.h; tolerance contract, mode 0): psum.acc non-null -> paths are ordered
-    // pixel-major (i = lp * cs + sl) and each path's radiance is added to its pixel's sum instead of
-    // written to rad
-    PsumOut psum;
-    uint32_t cs;                          // samples of this chunk (pixel-major order)
-    double inv_cs;                        // 1.0 / cs
-    uint32_t lds_psum;                    // LDS words per lane slot of the wave's pixel slots (PSUM_WORDS or 0)
-    uint32_t retrace_phase;               // mrt_retrace_kernel: 0 the handed-over paths, 1 the non-finite samples' prefixes
+    // rounding-critical paths (mrt_shade.h light_critical) listed for the exact-arithmetic retrace
+    // kernel: null rt, no hand-over
+    RetraceList rt;
 };
 
-// path index -> (local pixel, sample row of the chunk): sample-major i = sl * npix + lp, or
-// pixel-major i = lp * cs + sl under pixel sums
-MRT_DFN void path_coords(const PathParams& P, uint32_t i, uint32_t* lp_out, uint32_t* sl_out) {
-    const bool pm = MRT_FWD_FOLD && P.psum.acc != nullptr;  // (the exact build folds deepest-first, per path)
-    const uint32_t n = pm ? P.cs : P.npix;
-    // the double estimate of i / n is off by at most one either way
-    uint32_t q = (uint32_t)((double)i * (pm ? P.inv_cs : P.inv_npix));
-    uint32_t r = i - q * n;
-    if ((int32_t)r < 0) { q--; r += n; }
-    if (r >= n) { q++; r -= n; }
-    *lp_out = pm ? q : r;
-    *sl_out = pm ? r : q;
-}
-
 typedef void (*path_kernel_t)(PathParams);
+
+// path index -> (local pixel, sample row of the chunk): i = sl * npix + lp
+MRT_DFN void path_coords(const PathParams& P, uint32_t i, uint32_t* lp_out, uint32_t* sl_out) {
+    // the double estimate of i / npix is off by at most one either way
+    uint32_t sl = (uint32_t)((double)i * P.inv_npix);
+    uint32_t lp = i - sl * P.npix;
+    if ((int32_t)lp < 0) { sl--; lp += P.npix; }
+    if (lp >= P.npix) { sl++; lp -= P.npix; }
+    *lp_out = lp;
+    *sl_out = sl;
+}
 
 // path index -> its camera coordinates (u, v) and its PCG stream seeded from the path key
 // (main.cpp:138-149 per (pixel, sample); the stream key of DESIGN.md section 2)
@@ -129,9 +121,8 @@ struct KernelTable {
     uint32_t pq[kNumVariants];    // LDS words per lane slot of the kernel's queue of path starts
     uint32_t box6_walk[kNumVariants];  // 1: Cornell shape walked by cornell_fast_hit when op 8 is MRT_F_BOX6
     uint32_t rewrite[kNumVariants];    // 1: the interpreter runs the rewritten program (mrt_sig.h lin_rewrite_fast)
-    uint32_t psum[kNumVariants];       // 1: the kernel can add its paths to pixel sums (mrt_psum.h; LDS reserved)
     // the path-exact build's retrace kernel for the tolerance variants that hand rounding-critical
-    // paths over (mrt_shade.h light_critical): launched over PsumOut::rt after the path kernels
+    // paths over (mrt_shade.h light_critical): launched over PathParams::rt after each path kernel
     path_kernel_t retrace[kNumVariants];
 };
 const KernelTable& kernel_table_exact();

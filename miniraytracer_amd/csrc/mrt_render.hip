@@ -51,7 +51,6 @@ static void take_variant(KernelTable& m, const KernelTable& s, uint32_t i) {
     m.pq[i] = s.pq[i];
     m.box6_walk[i] = s.box6_walk[i];
     m.rewrite[i] = s.rewrite[i];
-    m.psum[i] = s.psum[i];
 }
 static const KernelTable& fast_table() {
     static const KernelTable t = [] {
@@ -65,7 +64,7 @@ static const KernelTable& fast_table() {
         for (uint32_t i = 0; i < kNumVariants; i++) {
             if (x.kernel[i] && !off("MRT_PATH_EXACT")) take_variant(m, x, i);
             else if (z.kernel[i] && !off("MRT_FTZ")) take_variant(m, z, i);
-            // the exact arithmetic for the pixel-sum renders' small jobs (mrt_kernels.hip mrt_retrace_kernel)
+            // the exact arithmetic for the rounding-critical paths of the fast variants (mrt_retrace_kernel)
             m.retrace[i] = x.retrace[i];
         }
         return m;
@@ -208,47 +207,6 @@ mrt_final_kernel(const float4* __restrict__ acc, float4* __restrict__ out, uint3
     __builtin_amdgcn_raw_buffer_store_b128(o, ro, lp * 16u, 0, 0);
 }
 
-// Pixel sums (mrt_psum.h): the render's colours from the 64-bit sums -- draw()'s `/= numSamples`
-// and luminance clamp (final_pixel, main.cpp:168-173) -- into the caller's output; unless `keep`
-// (a preview), the sums cleared for the next render, the counters reset (FoldEnd) and, by the last
-// group to finish, the non-finite list emptied (every group has read its length by then).
-__global__ void __launch_bounds__(256) mrt_psum_final_kernel(unsigned long long* __restrict__ acc, float4* __restrict__ out, uint32_t npix,
-                                                            uint32_t ns, float max_lum, const uint2* __restrict__ nf,
-                                                            const unsigned long long* __restrict__ nfp, uint32_t* nf_n,
-                                                            uint32_t* done, uint32_t* rt_n, uint32_t nf_cap, uint32_t keep, FoldEnd fe) {
-    const uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
-    if (!keep) reset_counters(fe, lp);
-    const uint32_t n_nf = __hip_atomic_load(nf_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (lp < npix) {
-        ulonglong2* a2 = reinterpret_cast<ulonglong2*>(acc + (size_t)lp * 4u);
-        const ulonglong2 p = a2[0], q = a2[1];
-        const unsigned long long a[4] = {p.x, p.y, q.x, q.y};
-        f3 c = psum_color(a, lp, ns, nf, nfp, n_nf, nf_cap);
-        c = final_pixel(c, ns, 0u, max_lum);
-        out[lp] = make_float4(c.x, c.y, c.z, 0.0f);
-        if (!keep) {
-            a2[0] = make_ulonglong2(0ull, 0ull);
-            a2[1] = make_ulonglong2(0ull, 0ull);
-        }
-    }
-    if (!keep) {
-        __shared__ uint32_t last;
-        __syncthreads();
-        if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1u;
-        __syncthreads();
-        if (last) {  // every other group has read the lists: clear them (and the prefixes) for the next render
-            const uint32_t nl = n_nf < nf_cap ? n_nf : nf_cap;
-            if (nfp)
-                for (uint32_t i = threadIdx.x; i < nl * 4u; i += blockDim.x) const_cast<unsigned long long*>(nfp)[i] = 0ull;
-            if (threadIdx.x == 0) {
-                atomicExch(nf_n, 0u);
-                atomicExch(rt_n, 0u);
-                atomicExch(done, 0u);
-            }
-        }
-    }
-}
-
 // Image output on the device (main.cpp:416-444): global max luminance, then per-pixel Drago +
 // ARGB32 -- the functions of include/mrt_tonemap.h, the same bits as the host mrt_tonemap_argb.
 __global__ void __launch_bounds__(256) mrt_lum_max_kernel(const float4* __restrict__ rgb, uint32_t n, unsigned int* __restrict__ lwmax_bits) {
@@ -306,8 +264,7 @@ struct PathLaunch {
     uint32_t lds_save = 0;  // LDS words per lane slot for the query ray parked during instances
     uint32_t lds_mesh = 0;  // LDS words per lane of the mesh walk's stack
     bool rewrite = false;   // the kernel runs the tolerance-contract program rewrite (s->prog_fast)
-    bool psum = false;      // the kernel can add paths to pixel sums (mrt_psum.h; its LDS slots reserved)
-    path_kernel_t retrace = nullptr;  // the exact arithmetic for pixel-sum renders (mrt_retrace_kernel)
+    path_kernel_t retrace = nullptr;  // the exact arithmetic for its rounding-critical paths (mrt_retrace_kernel)
     size_t retrace_lds = 0;
     bool handover = false;  // the kernel hands its rounding-critical paths to it (fast arithmetic)
     uint32_t walk_min = 32;  // resumable mesh walk threshold of this build (PathParams::walk_min)
@@ -376,20 +333,10 @@ struct mrt_scene {
     std::vector<uint32_t> prev_px;   // local pixel -> row-major pixel of the previewed render
     uint32_t prev_w = 0, prev_h = 0;
     uint32_t lev_rows = 0;
-    uint64_t* d_counter = nullptr;   // 64 B scratch: [0] unused, [2] ray total of mrt_render, [4] cancel flag,
-                                     // [6] non-finite samples listed (u32), [7] pixel-sum final groups done (u32),
+    uint64_t* d_counter = nullptr;   // 64 B scratch: [0] paths handed to the exact arithmetic since upload, [2] ray total of mrt_render, [4] cancel flag,
                                      // [1] rounding-critical paths listed (u32), [3] retrace groups done (u32)
-    // pixel sums (mrt_psum.h): 4 x u64 per local pixel, zero between renders (the final kernel
-    // clears what it read); the non-finite samples' list
-    unsigned long long* d_acc64 = nullptr;
-    size_t acc64_cap = 0;
-    uint2* d_nf = nullptr;
-    size_t nf_cap = 0;
-    unsigned long long* d_nfp = nullptr;  // per non-finite entry: the finite samples ahead of it
-    size_t nfp_cap = 0;
-    uint2* d_rt = nullptr;           // rounding-critical paths handed to the retrace kernel
+    uint32_t* d_rt = nullptr;        // rounding-critical paths listed for the retrace kernel (path indices)
     size_t rt_cap = 0;
-    bool psum = false;               // the workspace's render (wdesc) runs with pixel sums
     uint64_t* d_counters = nullptr;  // one work counter per chunk launch (progress reads them)
     size_t cnt_cap = 0;
     std::vector<uint64_t> chunk_paths;
@@ -1011,7 +958,6 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
         L.lds_save = tabs[k]->box6_walk[s->variant] ? 0u : s->lds_save;
         L.lds_mesh = s->lds_mesh;
         L.rewrite = tabs[k]->rewrite[s->variant] != 0;
-        L.psum = tabs[k]->psum[s->variant] != 0;
         L.retrace = tabs[k]->retrace[s->variant];
         // a fast-arithmetic kernel hands its rounding-critical paths to the exact arithmetic
         // (mrt_shade.h light_critical); MRT_RETRACE=0 at upload keeps them (A/B)
@@ -1031,12 +977,7 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
         const size_t lds_core = (size_t)waves_per_wg * 64 * 4 *
                                 (s->lds_frames * 2 + s->lds_rays * 11 + L.lds_mesh + L.lds_save + tabs[k]->lev_k[s->variant] * 4 +
                                  tabs[k]->pq[s->variant]);
-        // pixel sums only where their LDS slots (PSUM_WORDS per lane slot) cost no resident group:
-        // the mesh kernels' stacks leave no room for them at 7 waves per SIMD (measured with them:
-        // teapot -11%, bunny -24% at 6), and those kernels keep the per-path radiance buffer
-        if (L.psum && !tabs[k]->tree[s->variant] && groups(lds_core + (size_t)waves_per_wg * 64 * 4 * PSUM_WORDS) < groups(lds_core))
-            L.psum = false;
-        L.lds_bytes = lds_core + (L.psum ? (size_t)waves_per_wg * 64 * 4 * PSUM_WORDS : 0u);
+        L.lds_bytes = lds_core;
         if (L.lds_bytes > (size_t)prop.sharedMemPerBlock) {
             mrt_scene_free(s);
             return mrt_internal_fail(MRT_ERR_INVALID, "scene graph too deep for the LDS stacks");
@@ -1088,7 +1029,7 @@ extern "C" void mrt_scene_free(mrt_scene* s) {
     if (s->h_seq) (void)hipHostFree(s->h_seq);
     if (s->ev_done) (void)hipEventDestroy(s->ev_done);
     for (void* p : {(void*)s->d_counters, (void*)s->d_pixels, (void*)s->d_sdist, (void*)s->d_rad, (void*)s->d_path_rays, (void*)s->d_acc,
-                    (void*)s->d_lev, (void*)s->d_out, (void*)s->d_prev, (void*)s->d_acc64, (void*)s->d_nf, (void*)s->d_nfp, (void*)s->d_rt})
+                    (void*)s->d_lev, (void*)s->d_out, (void*)s->d_prev, (void*)s->d_rt})
         if (p) (void)hipFree(p);
     delete s;
 }
@@ -1130,19 +1071,10 @@ static mrt_status grow(mrt_scene* s, void** p, size_t* cap, size_t bytes) {
     return MRT_OK;
 }
 
-// Pixel sums (mrt_psum.h) for a render: the tolerance contract, mode 0 (draw(); draw2()'s per-pass
-// clamp needs the samples in order), no per-path debug output, on a kernel that has them.
-// MRT_PSUM=0 in the environment keeps the per-path radiance buffer and the fold (A/B).
-static constexpr uint32_t kNfCap = 1u << 16;  // non-finite samples listed per render
-// rounding-critical paths listed per render (a kernel stops handing over at half of it): ~1.5e-5 per
-// path in the Cornell scenes, so room for ~3.5e10 paths
+// rounding-critical paths listed per launch (mrt_shade.h light_critical; a full list loses the rest,
+// which keep their fast radiance): measured ~1e-5 per path in the Cornell scenes
 static constexpr uint32_t kRtCap = 1u << 20;
 static constexpr uint32_t kRetraceGroups = 512;  // one-wave groups of the retrace kernel
-static bool want_psum(const mrt_scene* s, const mrt_render_desc* d) {
-    if (!(d->flags & MRT_RF_FAST) || d->mode != 0 || (d->flags & (MRT_RF_PATH_DEBUG | MRT_RF_FOLD_BEHIND)) || !s->pl[1].psum) return false;
-    const char* e = getenv("MRT_PSUM");
-    return !(e && *e && atoi(e) == 0);
-}
 
 #define MRT_GPU_ONLY(s, what) \
     if ((s) && (s)->cpu) return mrt_internal_fail(MRT_ERR_INVALID, what " is a GPU-backend entry point (scene on MRT_DEVICE_CPU)")
@@ -1182,36 +1114,19 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
         HIPCHK(hipMemcpy(s->d_sdist, sd.data(), sd.size() * 8, hipMemcpyHostToDevice));
         s->sdist_sq = sq;
     }
-    // pixel sums (mrt_psum.h): the tolerance contract's mode 0 on a kernel that has them; no
-    // per-path radiance buffer, so a launch is bounded by the 32-bit path index only
-    const bool psum = want_psum(s, d);
-    uint32_t chunk = d->chunk_samples ? std::min(d->chunk_samples, ns) : psum ? ns : auto_chunk(s->npix, ns);
+    uint32_t chunk = d->chunk_samples ? std::min(d->chunk_samples, ns) : auto_chunk(s->npix, ns);
     chunk = (uint32_t)std::min<uint64_t>(chunk, 0xFFFFFFFFull / std::max<uint32_t>(s->npix, 1));  // 32-bit path index
     // 32-bit byte offsets of the chunk's radiance (the path kernel's held store, mrt_kernels.hip)
-    if (!psum) chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(chunk, 0xFFFFFFFFull / (12ull * std::max<uint32_t>(s->npix, 1))));
+    chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(chunk, 0xFFFFFFFFull / (12ull * std::max<uint32_t>(s->npix, 1))));
     if (chunk == 0) return mrt_internal_fail(MRT_ERR_INVALID, "image too large for one launch");
     if (d->flags & MRT_RF_PATH_DEBUG) chunk = ns;  // debug keeps every path
     if (chunk != s->chunk && (st = quiesce(s))) return st;  // the fold of a running render reads `chunk` rows
     s->chunk = chunk;
     size_t paths = (size_t)s->npix * s->chunk;
-    if (psum) {
-        void* const before = s->d_acc64;
-        if ((st = grow(s, (void**)&s->d_acc64, &s->acc64_cap, (size_t)s->npix * 32))) return st;
-        // zeroed once at allocation; afterwards every render's final kernel leaves it zero
-        if (s->d_acc64 != before) HIPCHK(hipMemset(s->d_acc64, 0, s->acc64_cap));
-        if ((st = grow(s, (void**)&s->d_nf, &s->nf_cap, (size_t)kNfCap * sizeof(uint2)))) return st;
-        if (s->pl[1].retrace) {
-            void* const b2 = s->d_nfp;
-            if ((st = grow(s, (void**)&s->d_nfp, &s->nfp_cap, (size_t)kNfCap * 32))) return st;
-            if (s->d_nfp != b2) HIPCHK(hipMemset(s->d_nfp, 0, s->nfp_cap));  // later: cleared by each render's final kernel
-        }
-    } else if ((st = grow(s, (void**)&s->d_rad, &s->rad_cap, paths * 12))) {
-        return st;
-    }
+    if ((st = grow(s, (void**)&s->d_rad, &s->rad_cap, paths * 12))) return st;
     if ((d->flags & MRT_RF_FAST) && !(d->flags & MRT_RF_PATH_DEBUG) && s->pl[1].handover &&
-        (st = grow(s, (void**)&s->d_rt, &s->rt_cap, (size_t)kRtCap * sizeof(uint2))))
+        (st = grow(s, (void**)&s->d_rt, &s->rt_cap, (size_t)kRtCap * sizeof(uint32_t))))
         return st;
-    s->psum = psum;
     if ((st = grow(s, (void**)&s->d_acc, &s->acc_cap, (size_t)s->npix * 16))) return st;
     if ((st = grow(s, (void**)&s->d_out, &s->out_cap, (size_t)s->npix * 16 + 16))) return st;
     if (d->flags & MRT_RF_PREVIEW) {
@@ -1313,7 +1228,6 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         HIPCHK(hipStreamWriteValue32(q, s->h_seq, 0u, 0));
         s->prev_epoch++;
     }
-    PathParams Plast{};
     for (uint32_t s0 = 0; s0 < ns; s0 += s->chunk) {
         uint32_t s1 = std::min(ns, s0 + s->chunk);
         PathParams P{};
@@ -1360,40 +1274,17 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.rays = d_rays ? (unsigned long long*)d_rays : s->d_rays;
         P.lev = s->d_lev;
         P.lev_rows = s->lev_rows;
-        P.lds_psum = PL.psum ? PSUM_WORDS : 0u;  // (reserved in the kernel's LDS layout either way)
-        P.cs = s1 - s0;
-        P.inv_cs = 1.0 / (double)P.cs;
         // the rounding-critical paths' hand-over: tolerance contract, not the per-path debug output
+        // (whose radiance is the fast kernel's own)
         const bool handover = PL.handover && !(d->flags & MRT_RF_PATH_DEBUG);
-        if (s->psum)
-            P.psum = PsumOut{s->d_acc64, s->d_nf, (uint32_t*)(s->d_counter + 6), kNfCap, s->d_nfp, handover ? s->d_rt : nullptr,
-                             (uint32_t*)(s->d_counter + 1), kRtCap, (uint32_t*)(s->d_counter + 3)};
-        else if (handover)
-            P.psum.rt = s->d_rt, P.psum.rt_n = (uint32_t*)(s->d_counter + 1), P.psum.rt_cap = kRtCap,
-            P.psum.rt_done = (uint32_t*)(s->d_counter + 3);
+        if (handover)
+            P.rt = RetraceList{s->d_rt, (uint32_t*)(s->d_counter + 1), kRtCap, (uint32_t*)(s->d_counter + 3), (unsigned long long*)s->d_counter};
         HIPCHK(hipEventRecord(s->ev[2 * s->n_launch], q));
         hipLaunchKernelGGL(PL.fn, dim3(PL.grid), dim3(PL.wg), PL.lds_bytes, q, P);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(s->ev[2 * s->n_launch + 1], q));
         s->n_launch++;
-        if (s->psum) {  // pixel sums: no fold; a preview reads the sums as they stand
-            if (preview) {
-                hipLaunchKernelGGL(mrt_psum_final_kernel, dim3((s->npix + 255) / 256), dim3(256), 0, q, s->d_acc64, s->d_prev, s->npix, s1,
-                                   d->max_luminance, (const uint2*)s->d_nf, (const unsigned long long*)nullptr, (uint32_t*)(s->d_counter + 6), (uint32_t*)(s->d_counter + 7),
-                                   (uint32_t*)(s->d_counter + 1), kNfCap, 1u, FoldEnd{});
-                HIPCHK(hipGetLastError());
-                HIPCHK(hipStreamWriteValue32(q, s->h_seq, 2 * seq + 1, 0));
-                HIPCHK(hipMemcpyAsync(s->h_prev, s->d_prev, (size_t)s->npix * 16, hipMemcpyDeviceToHost, q));
-                HIPCHK(hipStreamWriteValue32(q, s->h_seq + 1, s1, 0));
-                HIPCHK(hipStreamWriteValue32(q, s->h_seq, 2 * seq + 2, 0));
-                seq++;
-            }
-            s->last_paths = P.n_paths;
-            Plast = P;
-            continue;
-        }
-        if (handover) {  // the handed-over paths of this launch, exact, into the radiance buffer (fold next)
-            P.retrace_phase = 2;
+        if (handover) {  // this launch's rounding-critical paths, exact, into the radiance buffer (fold next)
             hipLaunchKernelGGL(PL.retrace, dim3(kRetraceGroups), dim3(64), PL.retrace_lds, q, P);
             HIPCHK(hipGetLastError());
         }
@@ -1424,24 +1315,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         }
         s->last_paths = P.n_paths;
     }
-    if (s->psum) {  // the colours from the sums, the counters reset, the sums cleared
-        if (PL.retrace) {  // the exact arithmetic's jobs (their counts are on the device: fixed small grids)
-            if (PL.handover && !(d->flags & MRT_RF_PATH_DEBUG)) {  // phase 0: the handed-over paths
-                Plast.retrace_phase = 0;
-                hipLaunchKernelGGL(PL.retrace, dim3(kRetraceGroups), dim3(64), PL.retrace_lds, q, Plast);
-                HIPCHK(hipGetLastError());
-            }
-            Plast.retrace_phase = 1;  // phase 1: the prefixes of the non-finite samples
-            hipLaunchKernelGGL(PL.retrace, dim3(kRetraceGroups), dim3(64), PL.retrace_lds, q, Plast);
-            HIPCHK(hipGetLastError());
-        }
-        const uint32_t nreset = launches * MRT_CNT_SLOTS;
-        const FoldEnd fe{(float4*)d_local, ns, (unsigned long long*)s->d_counters, (unsigned long long*)s->h_prog, nreset, launches * MRT_NPART};
-        hipLaunchKernelGGL(mrt_psum_final_kernel, dim3((std::max(s->npix, nreset) + 255) / 256), dim3(256), 0, q, s->d_acc64, (float4*)d_local,
-                           s->npix, ns, d->max_luminance, (const uint2*)s->d_nf, (const unsigned long long*)(PL.retrace ? s->d_nfp : nullptr), (uint32_t*)(s->d_counter + 6), (uint32_t*)(s->d_counter + 7),
-                           (uint32_t*)(s->d_counter + 1), kNfCap, 0u, fe);
-        HIPCHK(hipGetLastError());
-    } else if (preview || ((d->flags & MRT_RF_FOLD_BEHIND) && d->mode == 0)) {  // (otherwise the last fold wrote the output and reset the counters)
+    if (preview || ((d->flags & MRT_RF_FOLD_BEHIND) && d->mode == 0)) {  // (otherwise the last fold wrote the output and reset the counters)
         const uint32_t nreset = launches * MRT_CNT_SLOTS;
         const uint32_t blocks = (std::max(s->npix, nreset) + MRT_FINAL_WG - 1) / MRT_FINAL_WG;
         hipLaunchKernelGGL(mrt_final_kernel, dim3(blocks), dim3(MRT_FINAL_WG), 0, q, s->d_acc, (float4*)d_local, s->npix, ns, d->mode,
@@ -1602,6 +1476,14 @@ extern "C" mrt_status mrt_scene_kernel_info(const mrt_scene* s, mrt_kernel_info*
                : L.fn == kernel_table_fast_pex().kernel[s->variant] ? MRT_BUILD_PATH_EXACT
                : L.fn == kernel_table_fast_ftz().kernel[s->variant] ? MRT_BUILD_FAST_FTZ
                                                                      : MRT_BUILD_FAST;
+    out->pad = 0;
+    out->handed_over = 0;
+    if (s->d_counter) {  // (after the scene's last render: the synchronous copy waits for it)
+        uint64_t n = 0;
+        if (hipMemcpy(&n, s->d_counter, 8, hipMemcpyDeviceToHost) != hipSuccess)
+            return mrt_internal_fail(MRT_ERR_HIP, "mrt_scene_kernel_info: counter read");
+        out->handed_over = n;
+    }
     return MRT_OK;
 }
 

@@ -193,9 +193,20 @@ MRT_DFN f3 biased_pdf_generate(const DScene& S, f3 origin, float time, Pcg& rng,
 // colour.  Whether a wall hit lands on y == 554 exactly depends on the last bit of its
 // arithmetic, so under the fast arithmetic these events fall on other paths than the reference's
 // (C3 at 4096 spp: 98% of the tolerance contract's squared error in 100 such pixels).  Such paths
-// are handed to the exact arithmetic instead (mrt_retrace_kernel): a sample direction whose y is
-// within 2^-16 of the origin's height (~140 ulps: the fast and the exact path differ by a few).
+// are traced again with the exact arithmetic (mrt_retrace_kernel), whose radiance replaces the
+// fast one: a sample direction whose y is within 2^-16 of the origin's height (~140 ulps: the
+// fast and the exact path differ by a few).  The fast kernel only marks them (*crit) and goes on.
 MRT_DFN bool light_critical(f3 origin, f3 gen) { return fabsf(gen.y) <= fmaxf(fabsf(origin.y), 1.0f) * 0x1p-16f; }
+// The list the fast-arithmetic path kernel appends such paths to (their path index in the launch);
+// the retrace kernel (mrt_kernels.hip) traces each again with the exact arithmetic and overwrites
+// its radiance before the fold.  A path listed at several bounces is traced once per entry.
+struct RetraceList {
+    uint32_t* __restrict__ idx;              // path indices of the launch (sample-major, as rad)
+    uint32_t* __restrict__ n;                // entries appended (may exceed cap: the rest are lost)
+    uint32_t cap;
+    uint32_t* __restrict__ done;             // retrace groups finished (the last one clears n)
+    unsigned long long* __restrict__ total;  // paths listed since the scene's upload (mrt_kernel_info)
+};
 
 // ------------------------------------------------------------------------------------------
 // trace() (main.cpp:66-118) as a per-lane state machine advanced one segment (= one ray, one
@@ -322,7 +333,7 @@ MRT_DFN void camera_ray_args(const DScene& S, Pcg& rng, float s, float t, f3* o,
 // is then in *L.
 template <uint32_t F, uint32_t LK>
 MRT_DFN bool shade_hit(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev, bool hit,
-                                          const HitRec& rec, f3* L, PhaseClock& ph, bool* crit = nullptr) {
+                                          const HitRec& rec, f3* L, PhaseClock& ph, bool* crit = nullptr, bool allow_crit = false) {
     Ray& r = ps.r;
     if (!hit) {
         if ((F & FT_SKY) && S.sky) {  // main.cpp:113-115
@@ -405,11 +416,7 @@ MRT_DFN bool shade_hit(const DScene& S, PathState& ps, uint32_t max_bounces, con
     }
     if (light) gen = biased_pdf_generate<F>(S, rec.p, r.time, ps.rng, dr);
     else gen = lamb ? onb_apply(rec.n, random_cosine_direction_pre(dr.v0, dr.v1)) : random_in_sphere(ps.rng);
-    if (crit && light && light_critical(rec.p, gen)) {  // ends here: retraced with the exact arithmetic
-        *crit = true;
-        *L = f3{0, 0, 0};
-        return true;
-    }
+    if (allow_crit && light && light_critical(rec.p, gen)) *crit = true;  // retraced with the exact arithmetic
     PH_MARK(ph, 6);
     const Ray sc = make_ray(rec.p, gen, r.time, 0);
     float sval, spdf;
@@ -435,14 +442,14 @@ MRT_DFN bool shade_hit(const DScene& S, PathState& ps, uint32_t max_bounces, con
 // One segment.  Returns true when the path has ended; its radiance is then in *L.
 template <uint32_t F, uint32_t LK>
 MRT_DFN bool trace_segment(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev,
-                                              const LStack& Ls, f3* L, PhaseClock& ph, bool* crit = nullptr) {
+                                              const LStack& Ls, f3* L, PhaseClock& ph, bool* crit = nullptr, bool allow_crit = false) {
     HitRec rec;
     bool hit;
     if constexpr (MRT_SIG_OF(F) != SIG_NONE) hit = scene_hit_sig<F>(S, ps.r, 0.001f, rec, Ls);
     else if constexpr ((F & FT_LIN) != 0) hit = scene_hit_lin<F>(S, ps.r, 0.001f, rec, Ls, ps.rng, ph);
     else hit = scene_hit<F>(S, ps.r, 0.001f, rec, ps.rng, Ls);
     PH_MARK(ph, 1);
-    return shade_hit<F, LK>(S, ps, max_bounces, lev, hit, rec, L, ph, crit);
+    return shade_hit<F, LK>(S, ps, max_bounces, lev, hit, rec, L, ph, crit, allow_crit);
 }
 
 // The next ray of a lane, built by make_ray once per iteration for all lanes at once (camera
@@ -501,7 +508,7 @@ MRT_DFN void dielectric_scatter(const DMat& M, const Ray& r, f3 n, Pcg& rng, Pen
 // previous path's radiance store there).
 template <uint32_t F, uint32_t LK, typename FLUSH>
 MRT_DFN bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev,
-                                            const LStack& Ls, f3* L, PendRay* pr, PhaseClock& ph, FLUSH&& flush, bool* crit = nullptr) {
+                                            const LStack& Ls, f3* L, PendRay* pr, PhaseClock& ph, FLUSH&& flush, bool* crit = nullptr, bool allow_crit = false) {
     HitRec rec;
     Ray& r = ps.r;
     bool hit;
@@ -578,11 +585,7 @@ MRT_DFN bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, c
     BSTATC(7, light);
     if (light) pr->dir = biased_pdf_generate<F>(S, rec.p, r.time, ps.rng, dr);
     else pr->dir = lamb ? onb_apply(rec.n, random_cosine_direction_pre(dr.v0, dr.v1)) : random_in_sphere(ps.rng);
-    if (crit && light && light_critical(rec.p, pr->dir)) {  // ends here: retraced with the exact arithmetic
-        *crit = true;
-        *L = f3{0, 0, 0};
-        return true;
-    }
+    if (allow_crit && light && light_critical(rec.p, pr->dir)) *crit = true;  // retraced with the exact arithmetic
     PH_MARK(ph, 6);
     return false;
 }

@@ -118,10 +118,31 @@ def test_cli_cpu_backend_writes_reference_image(mrt, tmp_path):
     p = subprocess.run([os.path.join(ROOT, "bin", "mrt"), "-backend", "cpu", "-order", "path", "-threads", "3", "-scene", "5", "-width", str(g["w"]),
                         "-height", str(g["h"]), "-samples", str(g["spp"]), "-depth", str(g["depth"]), "-mode", str(g["mode"]),
                         "-tilesize", "8", "-o", str(out)], capture_output=True, text=True, timeout=120, check=True)
-    assert "CPU, 3 threads" in p.stdout
+    assert "CPU, 1 x 3 threads" in p.stdout
     assert int(p.stdout.split("rays ")[-1].split()[0]) == g["rays"]
     img = mrt.read_pfm(str(out))
     assert np.array_equal(img.view(np.uint32), g["image"].view(np.uint32))
+
+
+@pytest.mark.parametrize("ranks", [2, 3, 8])
+def test_cli_cpu_backend_multi_rank_assembly(mrt, tmp_path, ranks):
+    """bin/mrt -backend cpu -gpus N: N rank contexts (one host thread each, -threads workers each)
+    render the work_queue tiles dealt to them (permuted rounds of N, mrt_local_pixels) into one
+    framebuffer -- the drop-in's multi-GPU assembly on the host: the image and ray total equal the
+    one-rank render and the stream-matched fixture bit for bit."""
+    g = golden_stream("stream_5.npz")
+    out = tmp_path / "x.pfm"
+    p = subprocess.run([os.path.join(ROOT, "bin", "mrt"), "-backend", "cpu", "-order", "path", "-threads", "2", "-gpus", str(ranks),
+                        "-scene", "5", "-width", str(g["w"]), "-height", str(g["h"]), "-samples", str(g["spp"]), "-depth", str(g["depth"]),
+                        "-mode", str(g["mode"]), "-tilesize", "8", "-o", str(out)], capture_output=True, text=True, timeout=120, check=True)
+    assert f"CPU, {ranks} x 2 threads" in p.stdout
+    assert int(p.stdout.split("rays ")[-1].split()[0]) == g["rays"]
+    img = mrt.read_pfm(str(out))
+    assert np.array_equal(img.view(np.uint32), g["image"].view(np.uint32))
+    # the reference's per-thread RNG order is one rank's
+    bad = subprocess.run([os.path.join(ROOT, "bin", "mrt"), "-backend", "cpu", "-order", "ref", "-gpus", "2", "-scene", "5", "-width", "8",
+                          "-height", "8"], capture_output=True, text=True, timeout=120)
+    assert bad.returncode != 0
 
 
 def test_cpu_backend_preview_shows_finished_tiles(mrt):

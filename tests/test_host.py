@@ -115,14 +115,13 @@ def test_abi_structs_match_header(mrt, cname, pyname):
 
 
 def test_kernel_info_layout_matches_header(mrt):
-    """The ctypes mirror of mrt_kernel_info has the header's fields, in order (all uint32_t): a
-    field added on one side only would shift every later one."""
-    hdr = open(os.path.join(os.path.dirname(__file__), "..", "include", "mrt.h")).read()
-    body = re.search(r"typedef struct mrt_kernel_info \{(.*?)\} mrt_kernel_info;", hdr, re.S).group(1)
-    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
-    names = [n.strip() for decl in body.split(";") if decl.strip() for n in decl.replace("uint32_t", "").split(",")]
-    assert [f for f, _ in mrt._lib.KernelInfo._fields_] == names
-    assert all(t is __import__("ctypes").c_uint32 for _, t in mrt._lib.KernelInfo._fields_)
+    """The ctypes mirror of mrt_kernel_info has the header's fields, in order, with the same types:
+    a field added on one side only would shift every later one."""
+    want = {"uint32_t": ctypes.c_uint32, "uint64_t": ctypes.c_uint64}
+    hdr = header_struct("mrt_kernel_info")
+    assert [f for f, _ in mrt._lib.KernelInfo._fields_] == [n for n, _ in hdr]
+    for (f, t), (_, ct) in zip(mrt._lib.KernelInfo._fields_, hdr):
+        assert t is want[ct], f
 
 
 def reference_tiles(W, H, ts):

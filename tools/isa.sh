@@ -11,6 +11,6 @@ d=$(mktemp -d)
   && cp mrt_kernels-hip-amdgcn-amd-amdhsa-gfx950.s /tmp/isa_$tag.s )
 rm -rf $d
 awk '/^_Z(N4mrtd)?[0-9]+mrt_(path_kernel|wf_).*:/{k=$1; n=0; sc=0; inb=1} inb && /^[ \t]+[sv]_|^[ \t]+(global|ds|scratch|buffer|flat)_/{n++} inb && /^[ \t]+scratch_/{sc++} /^\.Lfunc_end/{if(inb) {ins[k]=n; scr[k]=sc}; inb=0}
-     /\.amdhsa_kernel _Z(N4mrtd)?[0-9]+mrt_(path|wf_)/{kk=$2":"} /amdhsa_private_segment_fixed_size/{ps[kk]=$2} /amdhsa_next_free_vgpr/{vg[kk]=$2}
-     /^[ \t]+.name:[ \t]+_Z(N4mrtd)?[0-9]+mrt_(path|wf_)/{mk=$2":"} /\.sgpr_spill_count:/{ss[mk]=$2} /\.vgpr_spill_count:/{vs[mk]=$2}
+     /\.amdhsa_kernel /{kk=""} /\.amdhsa_kernel _Z(N4mrtd)?[0-9]+mrt_(path|wf_)/{kk=$2":"} kk!="" && /amdhsa_private_segment_fixed_size/{ps[kk]=$2} kk!="" && /amdhsa_next_free_vgpr/{vg[kk]=$2}
+     /^[ \t]+.name:/{mk=""} /^[ \t]+.name:[ \t]+_Z(N4mrtd)?[0-9]+mrt_(path|wf_)/{mk=$2":"} mk!="" && /\.sgpr_spill_count:/{ss[mk]=$2} mk!="" && /\.vgpr_spill_count:/{vs[mk]=$2}
      END{for (k in ins) printf "%-46s vgpr %4s vspill %4s sspill %4s scratch %4s (scratch insts %3d) insts %6d\n", k, vg[k], vs[k], ss[k], ps[k], scr[k], ins[k]}' /tmp/isa_$tag.s | sort

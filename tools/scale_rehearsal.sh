@@ -10,10 +10,12 @@ CFGS=${CFGS:-1,0 2,0 4,0 8,0 8,7}
 for cfg in $CFGS; do
   IFS=, read n r <<< "$cfg"
   timeout -k 10 300 python bench.py --no-cpu-baseline --no-compare-numerics --no-other-walk --no-parity --steps ${STEPS:-40} --warmup 4 \
-      --emulate-world $n --emulate-rank $r --emulate-gather ${SCALE_ARGS:-} > gpurun_out/scale_${n}_$r.log 2>&1 || exit 3
+      --emulate-world $n --emulate-rank $r --emulate-gather --step-times ${SCALE_ARGS:-} > gpurun_out/scale_${n}_$r.log 2>&1 || exit 3
   python - gpurun_out/scale_${n}_$r.log $n $r <<'PY'
 import json, sys
 j = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
-print(f"N={sys.argv[2]} rank {sys.argv[3]}: {j['ms_per_step']:.3f} ms/step, {j['value']:.0f} Mrays/s, kernel {j['roofline']['kernel_ms']:.3f} ms")
+st = j.get("step_times") or {}
+print(f"N={sys.argv[2]} rank {sys.argv[3]}: {j['ms_per_step']:.3f} ms/step, {j['value']:.0f} Mrays/s, kernel {j['roofline']['kernel_ms']:.3f} ms"
+      f" | step intervals median {st.get('median_ms')} p90 {st.get('p90_ms')} max {st.get('max_ms')} at {st.get('max_at_step')}")
 PY
 done
