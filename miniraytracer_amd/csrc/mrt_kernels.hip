@@ -14,6 +14,7 @@
 // work_queue.cpp:158-166) and run trace() for each lane's path to completion; per-path radiance
 // is written sample-major [s][local pixel] (coalesced).
 #include <hip/hip_runtime.h>
+#include <cstddef>
 #include <utility>
 
 #include "mrt_launch.h"
@@ -162,6 +163,13 @@ template <uint32_t F> struct PathLevLds {
 #ifndef MRT_PATHQ
 #define MRT_PATHQ MRT_FAST
 #endif
+// the plain path loop reads the scene's kernel arguments through an opaque pointer each iteration
+// (round 5: book2 -1.5%, random spheres -1% per step; SGPR spills of book2's kernel 110 -> 35; in
+// the Cornell kernels' shared-constructor loop it removed their 4 SGPR spills but not a step's time:
+// 8.648 vs 8.655 ms, three rounds, not kept)
+#ifndef MRT_OPAQUE_SCENE
+#define MRT_OPAQUE_SCENE 1
+#endif
 // rounding-critical light samples handed to the exact arithmetic (mrt_shade.h light_critical): the
 // fast-arithmetic builds' light-sampled variants (MRT_CRIT=0 builds it out: A/B)
 #ifndef MRT_CRIT
@@ -169,6 +177,10 @@ template <uint32_t F> struct PathLevLds {
 #endif
 template <uint32_t F>
 static constexpr bool kCrit = MRT_CRIT && MRT_FAST && (F & FT_BIASED) != 0;
+// where crit_check finds the launch's list: PathParams (the kernel's only argument) starts the
+// argument segment
+template <uint32_t F>
+static constexpr uint32_t kCritOff = kCrit<F> ? (uint32_t)offsetof(PathParams, rt) : 0u;
 template <uint32_t F> struct PathQ {
     static constexpr bool on = MRT_PATHQ && (F & FT_MESH) == 0 && !TreeOf<F>::on;
     // LDS words per lane slot: o, dir, time, PCG state + inc, index (12); + the wave's claim state
@@ -196,8 +208,6 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                     TreeOf<F>::on ? P.tree_n : 0u};
     // the wave's queue of path starts ([word][entry], PathQ): after the fold levels
     float* const Lq = (float*)(wmesh + (P.lds_mesh + P.lds_save + LK * 4) * 64);
-    // list rounding-critical paths for the exact arithmetic (wave-uniform)
-    const bool flag = kCrit<F> && P.rt.idx != nullptr;
     const DScene& S = P.sc;
     const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const LevStore<LK> lev{(MRT_GLOBAL_AS v4f*)P.lev, P.lev_rows, (uint32_t)slot,
@@ -374,12 +384,6 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
         }
         PH_MARK(ph, 4);
     };
-    // a rounding-critical path (its light sample this bounce): listed for the retrace kernel, which
-    // replaces its radiance; the path itself goes on here (its rays are counted here)
-    auto list_critical = [&]() {
-        const uint32_t k = atomicAdd(P.rt.n, 1u);
-        if (k < P.rt.cap) P.rt.idx[k] = idx;
-    };
     // a finished path: the recursion's fold, radiance out (sample-major, coalesced), rays counted
     auto finish_path = [&](f3 L) {
         L = end_path(ps, lev, L);
@@ -429,7 +433,6 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
             PendRay pr;
             if (active) {
                 f3 L{0.0f, 0.0f, 0.0f};  // (left undefined, it was carried round the loop in copied registers)
-                bool crit = false;
                 // (the held store is issued inside, after the hit, beside the material load)
                 const bool ended = trace_split<F, LK>(S, ps, P.max_bounces, lev, Ls, &L, &pr, ph, [&]() {
                     if (st_pend) {
@@ -439,9 +442,8 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                         dst[2] = st_v.z;
                     }
                     st_pend = false;
-                }, &crit, flag);
+                }, CritSink{idx, kCritOff<F>});
                 PH_MARK(ph, 2);
-                if (crit) list_critical();
                 if (ended) {
                     st_v = end_path(ps, lev, L);
                     st_off = idx * 12u;
@@ -617,11 +619,9 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                     W::template derive<0>(prog, w, ps.r, ps.r, rec);
                 }
                 f3 L{0.0f, 0.0f, 0.0f};
-                bool crit = false;
-                const bool ended = shade_hit<F, LK>(S, ps, P.max_bounces, lev, w.hnode != MRT_NONE, rec, &L, ph, &crit, flag);
+                const bool ended = shade_hit<F, LK>(S, ps, P.max_bounces, lev, w.hnode != MRT_NONE, rec, &L, ph, CritSink{idx, kCritOff<F>});
                 PH_MARK(ph, 2);
                 phase = PH_BEGIN;
-                if (crit) list_critical();
                 if (ended) {
                     finish_path(L);
                     phase = 0;
@@ -634,12 +634,22 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
             take_paths([&](float u, float v) { ps.r = camera_ray(S, ps.rng, u, v); });
             if (!__any(active)) break;
             PH_MARK(ph, 0);
+#if MRT_OPAQUE_SCENE
+            // the scene's kernel arguments re-derived each iteration through an opaque constant
+            // pointer: its fields are scalar-loaded at their uses in the segment instead of held in
+            // SGPRs across the path loop (which spilled them into VGPR lanes)
+            // (P is the kernel's only argument: it starts the kernarg segment)
+            const MRT_CONST_AS DScene* sp = (const MRT_CONST_AS DScene*)((const MRT_CONST_AS char*)__builtin_amdgcn_kernarg_segment_ptr() +
+                                                                         offsetof(PathParams, sc));
+            asm volatile("" : "+s"(sp));
+            const DScene& Sseg = *(const DScene*)sp;
+#else
+            const DScene& Sseg = S;
+#endif
             if (active) {
                 f3 L{0.0f, 0.0f, 0.0f};
-                bool crit = false;
-                const bool ended = trace_segment<F, LK>(S, ps, P.max_bounces, lev, Ls, &L, ph, &crit, flag);
+                const bool ended = trace_segment<F, LK>(Sseg, ps, P.max_bounces, lev, Ls, &L, ph, CritSink{idx, kCritOff<F>});
                 PH_MARK(ph, 2);
-                if (crit) list_critical();
                 if (ended) finish_path(L);
             }
             PH_MARK(ph, 3);

@@ -1074,7 +1074,9 @@ static mrt_status grow(mrt_scene* s, void** p, size_t* cap, size_t bytes) {
 // rounding-critical paths listed per launch (mrt_shade.h light_critical; a full list loses the rest,
 // which keep their fast radiance): measured ~1e-5 per path in the Cornell scenes
 static constexpr uint32_t kRtCap = 1u << 20;
-static constexpr uint32_t kRetraceGroups = 512;  // one-wave groups of the retrace kernel
+// one-wave groups of the retrace kernel: 16384 lanes, a path each (more loop); its time is the longest
+// listed path's, plus the launch
+static constexpr uint32_t kRetraceGroups = 256;
 
 #define MRT_GPU_ONLY(s, what) \
     if ((s) && (s)->cpu) return mrt_internal_fail(MRT_ERR_INVALID, what " is a GPU-backend entry point (scene on MRT_DEVICE_CPU)")

@@ -90,9 +90,14 @@ MRT_DFN f3 onb_apply(f3 w, f3 vec) {
 // The next randf() values of a path's stream, two of them drawn ahead: every direction generator
 // of the lambertian mix starts with two draws, so they are drawn once before the light/surface
 // branch instead of inside both sides (same values, same stream order).
+// (a light sample's draw this close to 0 or 1 puts its point on the rect's edge: crit_check)
+#ifndef MRT_EDGE_TOL
+#define MRT_EDGE_TOL 0x1p-18f
+#endif
 struct Draws {
     float v0, v1;
     uint32_t used;
+    bool edge = false;  // a light sample drawn within MRT_EDGE_TOL of its rect's edge (crit_check)
     MRT_DFN float next(Pcg& rng) {
         if (used == 0) { used = 1; return v0; }
         if (used == 1) { used = 2; return v1; }
@@ -160,6 +165,7 @@ MRT_DFN f3 leaf_pdf_generate(const DScene& S, const mrt_node& n, f3 origin, floa
         float x = ref_fma(a, n.f[1] - n.f[0], n.f[0]);  // rect.cpp:105 (left to right)
         float b = dr.next(rng);
         float z = ref_fma(b, n.f[3] - n.f[2], n.f[2]);
+        dr.edge = fmaxf(fabsf(a - 0.5f), fabsf(b - 0.5f)) >= 0.5f - MRT_EDGE_TOL;
         return sub(f3{x, n.f[4], z}, origin);
     }
     if ((F & FT_BSPHERE) && k == MRT_K_SPHERE) {
@@ -186,17 +192,27 @@ MRT_DFN f3 biased_pdf_generate(const DScene& S, f3 origin, float time, Pcg& rng,
 }
 
 // A light sample is rounding-critical (tolerance contract, DESIGN.md section 2 "Non-finite
-// samples") when its direction is (nearly) parallel to the plane of an xz_rect light through the
-// origin.  xz_rect::pdf_value (rect.cpp:92-102) of a ray from a point ON the light's plane with a
-// direction parallel to it (dir.y == 0: the sampled point's y minus the origin's) computes
-// t = 0 / 0 and reports a hit with a NaN pdf; main.cpp:162-164 then doubles the pixel's running
-// colour.  Whether a wall hit lands on y == 554 exactly depends on the last bit of its
-// arithmetic, so under the fast arithmetic these events fall on other paths than the reference's
-// (C3 at 4096 spp: 98% of the tolerance contract's squared error in 100 such pixels).  Such paths
-// are traced again with the exact arithmetic (mrt_retrace_kernel), whose radiance replaces the
-// fast one: a sample direction whose y is within 2^-16 of the origin's height (~140 ulps: the
-// fast and the exact path differ by a few).  The fast kernel only marks them (*crit) and goes on.
-MRT_DFN bool light_critical(f3 origin, f3 gen) { return fabsf(gen.y) <= fmaxf(fabsf(origin.y), 1.0f) * 0x1p-16f; }
+// samples") where xz_rect::pdf_value (rect.cpp:92-102) can return a non-finite or zero pdf on one
+// side of a last-bit difference, which main.cpp:162-164 turns into a doubling of the pixel's
+// running colour:
+//  (1) its direction is (nearly) parallel to the light's plane: from a point ON the plane the
+//      sampled direction has dir.y == 0 (the sampled point's y minus the origin's), pdf_value
+//      computes t = 0 / 0 and reports a hit with a NaN pdf.  Whether a wall hit lands on y == 554
+//      exactly depends on the last bit of its arithmetic and on the rounding the path gathered on
+//      its earlier bounces: a window of MRT_CRIT_TOL relative to the origin's height (2^-16, ~140
+//      ulps at the Cornell light's 554);
+//  (2) the sampled point lies on the light's edge (a draw within MRT_EDGE_TOL of 0 or 1, 2^-18:
+//      ~0.5 ulp of 555 on the Cornell light's 130-wide side, a few times the rounding of the hit
+//      point pdf_value recomputes from the origin) and below the surface: the recomputed point can
+//      fall outside the rect by rounding, pdf 0, and with the cosine pdf 0 too the sample is 0 / 0.
+// Under the fast arithmetic these events fall on other paths than the reference's (C3 at 4096
+// spp: 98% of the tolerance contract's squared error in 100 such pixels).  Such paths are traced
+// again with the exact arithmetic (mrt_retrace_kernel), whose radiance replaces the fast one; the
+// fast kernel only lists them and goes on.
+#ifndef MRT_CRIT_TOL
+#define MRT_CRIT_TOL 0x1p-16f
+#endif
+MRT_DFN bool light_critical(f3 origin, f3 gen) { return fabsf(gen.y) <= fabsf(origin.y) * MRT_CRIT_TOL + MRT_CRIT_TOL; }
 // The list the fast-arithmetic path kernel appends such paths to (their path index in the launch);
 // the retrace kernel (mrt_kernels.hip) traces each again with the exact arithmetic and overwrites
 // its radiance before the fold.  A path listed at several bounces is traced once per entry.
@@ -207,6 +223,32 @@ struct RetraceList {
     uint32_t* __restrict__ done;             // retrace groups finished (the last one clears n)
     unsigned long long* __restrict__ total;  // paths listed since the scene's upload (mrt_kernel_info)
 };
+// where a shading step lists its path when its light sample is rounding-critical: the path's index
+// and the byte offset of the launch's RetraceList in the kernel's argument segment (a compile-time
+// constant; 0: no hand-over compiled in).  The list is read from the argument segment only where a
+// path is listed (a null list: no hand-over this launch), so nothing of it is held in registers
+// across the path loop (held there, it cost the Cornell kernel 1.3% with the hand-over off).
+struct CritSink {
+    uint32_t idx;
+    uint32_t rt_off;
+};
+MRT_DFN void crit_check(const CritSink& cs, bool light, f3 origin, f3 gen, bool edge, f3 n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (cs.rt_off && light && (edge || light_critical(origin, gen))) {
+        // (an edge sample above the surface has a cosine pdf > 0: finite either way)
+        if (!light_critical(origin, gen) && dot(gen, n) > (fabsf(gen.x) + fabsf(gen.y) + fabsf(gen.z)) * 0x1p-12f) return;
+        const MRT_CONST_AS char* ka = (const MRT_CONST_AS char*)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(ka));  // (the list's fields are loaded here, not hoisted out of the loop)
+        const MRT_CONST_AS RetraceList& rl = *(const MRT_CONST_AS RetraceList*)(ka + cs.rt_off);
+        if (rl.idx) {
+            const uint32_t k = atomicAdd(rl.n, 1u);
+            if (k < rl.cap) rl.idx[k] = cs.idx;
+        }
+    }
+#else
+    (void)cs, (void)light, (void)origin, (void)gen, (void)edge, (void)n;  // (the CPU backend runs the exact contract)
+#endif
+}
 
 // ------------------------------------------------------------------------------------------
 // trace() (main.cpp:66-118) as a per-lane state machine advanced one segment (= one ray, one
@@ -333,7 +375,7 @@ MRT_DFN void camera_ray_args(const DScene& S, Pcg& rng, float s, float t, f3* o,
 // is then in *L.
 template <uint32_t F, uint32_t LK>
 MRT_DFN bool shade_hit(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev, bool hit,
-                                          const HitRec& rec, f3* L, PhaseClock& ph, bool* crit = nullptr, bool allow_crit = false) {
+                                          const HitRec& rec, f3* L, PhaseClock& ph, const CritSink& cs = CritSink{0u, 0u}) {
     Ray& r = ps.r;
     if (!hit) {
         if ((F & FT_SKY) && S.sky) {  // main.cpp:113-115
@@ -416,7 +458,7 @@ MRT_DFN bool shade_hit(const DScene& S, PathState& ps, uint32_t max_bounces, con
     }
     if (light) gen = biased_pdf_generate<F>(S, rec.p, r.time, ps.rng, dr);
     else gen = lamb ? onb_apply(rec.n, random_cosine_direction_pre(dr.v0, dr.v1)) : random_in_sphere(ps.rng);
-    if (allow_crit && light && light_critical(rec.p, gen)) *crit = true;  // retraced with the exact arithmetic
+    crit_check(cs, light, rec.p, gen, dr.edge, rec.n);  // listed: retraced with the exact arithmetic
     PH_MARK(ph, 6);
     const Ray sc = make_ray(rec.p, gen, r.time, 0);
     float sval, spdf;
@@ -442,14 +484,14 @@ MRT_DFN bool shade_hit(const DScene& S, PathState& ps, uint32_t max_bounces, con
 // One segment.  Returns true when the path has ended; its radiance is then in *L.
 template <uint32_t F, uint32_t LK>
 MRT_DFN bool trace_segment(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev,
-                                              const LStack& Ls, f3* L, PhaseClock& ph, bool* crit = nullptr, bool allow_crit = false) {
+                                              const LStack& Ls, f3* L, PhaseClock& ph, const CritSink& cs = CritSink{0u, 0u}) {
     HitRec rec;
     bool hit;
     if constexpr (MRT_SIG_OF(F) != SIG_NONE) hit = scene_hit_sig<F>(S, ps.r, 0.001f, rec, Ls);
     else if constexpr ((F & FT_LIN) != 0) hit = scene_hit_lin<F>(S, ps.r, 0.001f, rec, Ls, ps.rng, ph);
     else hit = scene_hit<F>(S, ps.r, 0.001f, rec, ps.rng, Ls);
     PH_MARK(ph, 1);
-    return shade_hit<F, LK>(S, ps, max_bounces, lev, hit, rec, L, ph, crit, allow_crit);
+    return shade_hit<F, LK>(S, ps, max_bounces, lev, hit, rec, L, ph, cs);
 }
 
 // The next ray of a lane, built by make_ray once per iteration for all lanes at once (camera
@@ -508,7 +550,7 @@ MRT_DFN void dielectric_scatter(const DMat& M, const Ray& r, f3 n, Pcg& rng, Pen
 // previous path's radiance store there).
 template <uint32_t F, uint32_t LK, typename FLUSH>
 MRT_DFN bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev,
-                                            const LStack& Ls, f3* L, PendRay* pr, PhaseClock& ph, FLUSH&& flush, bool* crit = nullptr, bool allow_crit = false) {
+                                            const LStack& Ls, f3* L, PendRay* pr, PhaseClock& ph, FLUSH&& flush, const CritSink& cs = CritSink{0u, 0u}) {
     HitRec rec;
     Ray& r = ps.r;
     bool hit;
@@ -585,7 +627,7 @@ MRT_DFN bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, c
     BSTATC(7, light);
     if (light) pr->dir = biased_pdf_generate<F>(S, rec.p, r.time, ps.rng, dr);
     else pr->dir = lamb ? onb_apply(rec.n, random_cosine_direction_pre(dr.v0, dr.v1)) : random_in_sphere(ps.rng);
-    if (allow_crit && light && light_critical(rec.p, pr->dir)) *crit = true;  // retraced with the exact arithmetic
+    crit_check(cs, light, rec.p, pr->dir, dr.edge, rec.n);  // listed: retraced with the exact arithmetic
     PH_MARK(ph, 6);
     return false;
 }

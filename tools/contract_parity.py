@@ -2,7 +2,8 @@
 """Experiment: one numerics-contract build (MRT_EXPERIMENT_LIB, tools/build_variant.sh; default the
 in-tree library) against the reference as shipped at every BASELINE config's own spp -- C2 whole
 image (shipped_stream_5.npz), C3 / C4 / C5 pixel lists (shipped_ownspp_<id>.npz) -- with the path
-kernel's time (median of 3 renders) of C2 at full size.  One JSON line per (config, numerics).
+kernel's time (median of 3 renders) of C2 at full size and the paths the fast kernel handed over
+to the exact arithmetic per render.  One JSON line per (config, numerics).
   python tools/contract_parity.py [fast|exact ...]"""
 import json
 import os
@@ -28,7 +29,7 @@ for num in sys.argv[1:] or ["fast"]:
         ms.append(t / n)
     c = compare(img, rays, os.path.join(G, "shipped_stream_5.npz"))
     print(json.dumps({"tag": tag, "numerics": num, "config": "C2", "kernel_ms": round(float(np.median(ms)), 3),
-                      "grays": round(rays / np.median(ms) / 1e6, 2), **c}), flush=True)
+                      "grays": round(rays / np.median(ms) / 1e6, 2), "handed_over": r.kernel_info()["handed_over"] // 3, **c}), flush=True)
     r.close()
     # C3 over the whole image at its own spp (shipped_ownspp_full_9.npz); images kept for analysis
     g = os.path.join(G, "shipped_ownspp_full_9.npz")
@@ -40,7 +41,7 @@ for num in sys.argv[1:] or ["fast"]:
     if os.environ.get("MRT_PARITY_SAVE"):
         np.save(os.path.join(os.environ["MRT_PARITY_SAVE"], f"c3full_{tag}_{num}.npy"), img[..., :3])
     print(json.dumps({"tag": tag, "numerics": num, "config": "C3 whole image", "kernel_ms": round(t, 3),
-                      "grays": round(rays / t / 1e6, 2), **c}), flush=True)
+                      "grays": round(rays / t / 1e6, 2), "handed_over": r.kernel_info()["handed_over"], **c}), flush=True)
     r.close()
     for sid in (9, 8, 7):
         g = np.load(os.path.join(G, f"shipped_ownspp_{sid}.npz"))
@@ -50,5 +51,5 @@ for num in sys.argv[1:] or ["fast"]:
         t, n = r.kernel_ms()
         c = compare_pixels(img, rays, g)
         print(json.dumps({"tag": tag, "numerics": num, "config": {9: "C3", 8: "C4", 7: "C5"}[sid], "kernel_ms": round(t, 3),
-                          "grays": round(rays / t / 1e6, 2), **c}), flush=True)
+                          "grays": round(rays / t / 1e6, 2), "handed_over": r.kernel_info()["handed_over"], **c}), flush=True)
         r.close()
