@@ -390,8 +390,7 @@ def test_full_resolution_within_tolerance_of_shipped_reference(gpu, sid, numeric
     img, rays = r.render(gpu.render_desc(w, h, spp, depth=depth, numerics=numerics))
     c = compare(img, rays, path)
     print(c)
-    if sid != 7:
-        assert c["rmse"] < 1e-3, c
+    assert c["rmse"] < 1e-3, c  # (C5 too: path-exact, 8.2e-6 measured; round 3 needed a 3.5e-3 exception)
     assert c["block_rmse"] < 1e-3, c
     assert c["mean_delta"] < 1e-4, c
     assert abs(c["ray_ratio"] - 1) < FULL_RAYS[numerics], c
@@ -665,7 +664,10 @@ def test_c3_whole_image_own_spp_within_tolerance(gpu, numerics):
     """C3 (teapot in the Cornell room, 800x800) at its own 4096 spp over EVERY pixel against the
     reference as shipped, stream-matched (shipped_ownspp_full_9.npz, 7.2 G rays rendered by
     oracle/_ref/mrt_ref): per-pixel RMSE < 1e-3 under both contracts (north-star bar), channel
-    means within 1e-4, ray total within 0.5%."""
+    means within 1e-4, ray total within 0.5%.  Regression bars below the contract's: the exact
+    contract differs from the shipped build by libm alone (1.3e-5 measured), and the tolerance
+    contract holds 1.0e-4 with the rounding-critical paths handed over (9.0e-4 without them: the
+    non-finite samples of main.cpp:162-164 falling on other paths)."""
     from fixture_cmp import compare
     p = os.path.join(os.path.dirname(__file__), "golden", "shipped_ownspp_full_9.npz")
     _, w, h, spp, depth = (int(x) for x in np.load(p)["meta"])
@@ -674,14 +676,16 @@ def test_c3_whole_image_own_spp_within_tolerance(gpu, numerics):
     c = compare(img, rays, p)
     print(c)
     assert c["rmse"] < 1e-3, c
+    assert c["rmse"] < {"exact": 1e-4, "fast": 3e-4}[numerics], c
     assert c["mean_delta"] < 1e-4, c
     assert abs(c["ray_ratio"] - 1) < FULL_RAYS[numerics], c
 
 
 def test_rounding_critical_paths_retraced_exactly(gpu, monkeypatch):
-    """Tolerance contract: the paths whose light sample is rounding-critical (a point on the light's
-    plane, mrt_shade.h light_critical) are listed by the fast kernel and traced again by the exact
-    arithmetic, whose radiance replaces theirs before the fold.  A C2 render large enough to hold a
+    """Tolerance contract: the paths whose light sample is rounding-critical (a direction nearly in
+    the light's plane, or a point on its edge below the surface: mrt_shade.h crit_check) are listed
+    by the fast kernel and traced again by the exact arithmetic, whose radiance replaces theirs
+    before the fold.  A C2 render large enough to hold a
     few hundred of them: (1) the listed count is reported (mrt_kernel_info.handed_over); (2) the
     image differs from the one without the hand-over (MRT_RETRACE=0) only in pixels holding such a
     path, and it moves towards the exact contract's image there."""
