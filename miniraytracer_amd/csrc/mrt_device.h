@@ -419,6 +419,15 @@ MRT_DFN Ray moved_ray(const Ray& r0, f3 o) {
     r.nice = ray_nice(r.o, r.d);
     return r;
 }
+// x, y or z by a per-lane axis index, as selects (a select chain on one index was turned into a
+// per-lane lookup table in scratch memory)
+MRT_DFN float sel3(uint32_t a, float x, float y, float z) {
+    float v = a == 1u ? y : x;
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(v));
+#endif
+    return a == 2u ? z : v;
+}
 MRT_DFN f3 eval(const Ray& r, float t) { return add(r.o, fmul(t, r.d)); }
 
 // aabb::hit, active SSE branch (aabb.h:49-76)

@@ -67,10 +67,12 @@ using namespace mrtd;
 #define MRT_WPE_MESH 7
 #endif
 #ifndef MRT_WPE_LIN_GEN
-// the interpreter's compact variants (no program shape): 5 waves (96 VGPRs, spill-free with the
-// one-step box instances; round 4: 43.3 Grays/s on C2 through the interpreter against 40.3 at 6
-// waves without the step and 33.7 with it and 10 spilled VGPRs, profiles/r04_ab.txt)
-#define MRT_WPE_LIN_GEN 5
+// the interpreter's compact variants (no program shape): 6 waves (80 VGPRs, spill-free).  Round 4
+// held them at 5 (96 VGPRs): the room op's per-lane axis select had become a lookup table in
+// scratch, which kept the query ray in scratch memory; with sel3 it is gone, 81 VGPRs at 5 waves
+// (C2 through the interpreter 43.3 -> 46.4 Grays/s), 80 at 6 (47.7), 72 + 5 spilled at 7 (44.1;
+// profiles/r05_ab.txt section 6)
+#define MRT_WPE_LIN_GEN 6
 #endif
 template <uint32_t F> struct PathOcc {
     static constexpr bool kWide = (F & (FT_BVHW | FT_TEX | FT_VOLUME)) != 0 || !(F & FT_LIN);

@@ -251,7 +251,7 @@ MRT_DFN bool lin_room_hit(const MRT_CONST_AS LinOp& o, const Ray& r, float tmin,
     const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
     const float tf = fminf(fminf(fx, fy), fz);
     const uint32_t a = tf == fz ? 2u : (tf == fy ? 1u : 0u);  // ties to the later axis
-    const float da = a == 2u ? r.d.z : (a == 1u ? r.d.y : r.d.x);
+    const float da = sel3(a, r.d.x, r.d.y, r.d.z);
     const uint32_t k = a * 2u + (da > 0.0f ? 1u : 0u);
     *t = tf;
     *face = k;

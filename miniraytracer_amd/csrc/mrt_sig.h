@@ -423,15 +423,6 @@ struct SigWalk {
 #ifndef MRT_CORNELL_BATCHES
 #define MRT_CORNELL_BATCHES 2
 #endif
-// x, y or z by a per-lane axis index, as selects (a select chain on one index was turned into a
-// per-lane lookup table in scratch memory)
-MRT_DFN float sel3(uint32_t a, float x, float y, float z) {
-    float v = a == 1u ? y : x;
-#if defined(__HIP_DEVICE_COMPILE__)
-    asm volatile("" : "+v"(v));
-#endif
-    return a == 2u ? z : v;
-}
 struct CornellRec {
     float closest, k, ns;
     uint32_t code, mat;  // code: 0 none; 1-3 world rect of axis code-1 (plane k); 4-6 box face of axis code-4; 7 sphere
