@@ -419,6 +419,14 @@ MRT_DFN Ray moved_ray(const Ray& r0, f3 o) {
     r.nice = ray_nice(r.o, r.d);
     return r;
 }
+// a wave-uniform value the compiler cannot prove uniform, as an SGPR (host: itself)
+MRT_DFN uint32_t uniform_u32(uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+#else
+    return v;
+#endif
+}
 // x, y or z by a per-lane axis index, as selects (a select chain on one index was turned into a
 // per-lane lookup table in scratch memory)
 MRT_DFN float sel3(uint32_t a, float x, float y, float z) {

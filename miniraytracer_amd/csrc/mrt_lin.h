@@ -238,12 +238,40 @@ MRT_DFN LinOp lin_fetch_op(const MRT_CONST_AS LinOp& o) {
     }
     return r;
 }
+// The whole 64-B op as ONE batch of scalar loads and one wait (the compact interpreter kernels):
+// the op's fields are then read from SGPRs; read in place, an op cost the loop several load + wait
+// round trips to the scalar cache (the instance op's box, its rotation, its list's planes ...).
+MRT_DFN LinOp lin_fetch_all(const MRT_CONST_AS LinOp& o) {
+    const MRT_CONST_AS uint32_t* q = reinterpret_cast<const MRT_CONST_AS uint32_t*>(&o);
+    uint32_t w[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) w[k] = q[k];
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+s"(w[0]), "+s"(w[1]), "+s"(w[2]), "+s"(w[3]), "+s"(w[4]), "+s"(w[5]), "+s"(w[6]), "+s"(w[7]), "+s"(w[8]),
+                 "+s"(w[9]), "+s"(w[10]), "+s"(w[11]), "+s"(w[12]), "+s"(w[13]), "+s"(w[14]), "+s"(w[15]));
+#endif
+    LinOp r;
+    r.code = w[0];
+    r.node = w[1];
+    r.skip = w[2];
+    r.mat = w[3];
+#pragma unroll
+    for (int k = 0; k < 12; k++) r.f[k] = __uint_as_float(w[4 + k]);
+    return r;
+}
+// (measured slower: C2 through the interpreter 49.5 vs 50.6 Grays/s with the ops read in place,
+// three interleaved rounds, profiles/r05_ab.txt section 7; kept as an A/B switch)
+#ifndef MRT_LIN_FETCH_ALL
+#define MRT_LIN_FETCH_ALL 0
+#endif
+
 // LOP_ROOM (tolerance contract): the room's walls -- one-sided rects facing into the box
 // [f[0..2], f[3..5]], face k = axis * 2 + side present when bit k of o.node is set -- as one slab
 // test: a ray that meets the box leaves it through the face of its smallest far-plane distance,
 // and that face, if the room has it, is the wall hit (a face crossed going in is back-facing and
 // missed, rect.cpp:26-30).  *face = the exit face.
-MRT_DFN bool lin_room_hit(const MRT_CONST_AS LinOp& o, const Ray& r, float tmin, float tmax, float* t, uint32_t* face) {
+template <typename OP>
+MRT_DFN bool lin_room_hit(const OP& o, const Ray& r, float tmin, float tmax, float* t, uint32_t* face) {
     const float t0x = (o.f[0] - r.o.x) * r.inv.x, t1x = (o.f[3] - r.o.x) * r.inv.x;
     const float t0y = (o.f[1] - r.o.y) * r.inv.y, t1y = (o.f[4] - r.o.y) * r.inv.y;
     const float t0z = (o.f[2] - r.o.z) * r.inv.z, t1z = (o.f[5] - r.o.z) * r.inv.z;
@@ -260,7 +288,8 @@ MRT_DFN bool lin_room_hit(const MRT_CONST_AS LinOp& o, const Ray& r, float tmin,
 // an object_list flagged MRT_F_BOX6 (box.h:12-20, planes in f[6..11]) as one slab test
 // (tolerance contract, box6_leaf_hit); *child = the entry face's position among its six rects
 // (box.h order: xy at max z, xy at min z, xz at max y, xz at min y, yz at max x, yz at min x)
-MRT_DFN bool lin_box6_hit(const MRT_CONST_AS LinOp& o, const Ray& r, float tmin, float tmax, float* t, uint32_t* child) {
+template <typename OP>
+MRT_DFN bool lin_box6_hit(const OP& o, const Ray& r, float tmin, float tmax, float* t, uint32_t* child) {
     const float t0x = (o.f[6] - r.o.x) * r.inv.x, t1x = (o.f[9] - r.o.x) * r.inv.x;
     const float t0y = (o.f[7] - r.o.y) * r.inv.y, t1y = (o.f[10] - r.o.y) * r.inv.y;
     const float t0z = (o.f[8] - r.o.z) * r.inv.z, t1z = (o.f[11] - r.o.z) * r.inv.z;
@@ -274,7 +303,8 @@ MRT_DFN bool lin_box6_hit(const MRT_CONST_AS LinOp& o, const Ray& r, float tmin,
 }
 
 // aabb::hit (invDir = 1/dir of the ray, aabb.h:49)
-MRT_DFN bool lin_box(const MRT_CONST_AS LinOp& o, const Ray& r, float tmin, float tmax) {
+template <typename OP>
+MRT_DFN bool lin_box(const OP& o, const Ray& r, float tmin, float tmax) {
     const float b[6] = {o.f[0], o.f[1], o.f[2], o.f[3], o.f[4], o.f[5]};
     return aabb_hit(b, b + 3, r, tmin, tmax);
 }
@@ -320,10 +350,17 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
     uint32_t hinst = MRT_NONE;    // op index of the instance it lies in (MRT_NONE: world frame)
     bool hdone = false;           // rec already holds the closest hit (mesh_hit writes it)
     const MRT_CONST_AS LinOp* prog = const_ptr(S.prog);
-    for (uint32_t pc = 0;; pc++) {
-        const MRT_CONST_AS LinOp& o = prog[pc];
+    // one op: `o` is the op in place (constant memory) or its register copy (MRT_LIN_FETCH_ALL);
+    // false at the program's end
+    constexpr bool kFetch = MRT_LIN_FETCH_ALL && kLinSlabOps<F>;
+    uint32_t pc = 0;
+    auto op_at = [&](uint32_t k) -> decltype(auto) {
+        if constexpr (kFetch) return lin_fetch_all(prog[k]);
+        else return (prog[k]);
+    };
+    auto step = [&](const auto& o) __attribute__((always_inline)) -> bool {
         const uint32_t op = LOP_OP(o);
-        if (op == LOP_END) break;
+        if (op == LOP_END) return false;
         const bool on = (act >> lvl) & 1u;
         if (op == LOP_PRIM) {
             float t;
@@ -440,7 +477,7 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
             } else {
                 ci = moved_ray<kFastUnit<F>>(cur, sub(cur.o, f3{o.f[0], o.f[1], o.f[2]}));
             }
-            const MRT_CONST_AS LinOp& lo = prog[pc + 1];
+            const auto lo = op_at(pc + 1);
             float t;
             uint32_t c;
             const bool h = in & lin_box6_hit(lo, ci, tmin, closest, &t, &c);
@@ -470,7 +507,7 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
             inst = pc;
             if (!any_lane(in)) {
                 pc = o.skip - 1;
-                continue;
+                return true;
             }
             if (kind == MRT_K_TRROTY || kind == MRT_K_ROTY) cur = rotate_ray<kFastUnit<F>>(cur, o.f[6], o.f[7]);
             else cur = moved_ray<kFastUnit<F>>(r0, sub(r0.o, f3{o.f[0], o.f[1], o.f[2]}));
@@ -487,6 +524,15 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
             lvl--;
         }
         PH_MARK(ph, 8);
+        return true;
+    };
+    for (;; pc++) {
+        if constexpr (kFetch) {
+            pc = uniform_u32(pc);  // (wave-uniform: the op's words go to SGPRs)
+            if (!step(lin_fetch_all(prog[pc]))) break;
+        } else {
+            if (!step(prog[pc])) break;
+        }
     }
     if (INST) r = lin_load_ray(L);
     if (hnode == MRT_NONE) return false;
