@@ -6,7 +6,8 @@
 # rehearsal; the default bench line.  The new profiles/ files are copied to gpurun_out/profiles/
 # (the only directory that comes back).  Every step under its own limit; any failure ends the call.
 # PART=a: suite, smoke, profiles, contract A/B; PART=b: parity, configs, rehearsal, bench (after
-# part a's profiles are committed); unset: both.
+# part a's profiles are committed); unset: both.  NO_CAB=1 leaves the contract A/B out of part a
+# (a call of its own: gpurun's 20-minute limit).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/profiles
 export TMPDIR=/tmp
@@ -29,7 +30,7 @@ step pmc_c2 60 python tools/pmc_summary.py $TAG
 step prof_cfgs 900 bash tools/prof_configs.sh
 for c in c3 c4 c5; do step pmc_$c 60 python tools/pmc_summary.py ${TAG}_$c --prof gpurun_out/prof_$c; done
 cp profiles/${TAG}* profiles/pmc_s*.json gpurun_out/profiles/
-step contract_ab 600 python tools/contract_ab.py --measure
+[ "${NO_CAB:-0}" = 1 ] || step contract_ab 600 python tools/contract_ab.py --measure
 fi
 [ "${PART:-ab}" = a ] && exit 0
 step parity 600 python tools/parity_record.py --out gpurun_out/profiles/${TAG}_parity.json
