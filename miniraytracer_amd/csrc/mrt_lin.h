@@ -334,12 +334,17 @@ MRT_DFN void lin_untransform(const OP& io, HitRec& rec) {
 #ifndef MRT_BOXINST
 #define MRT_BOXINST 1  // the one-step box instance (MRT_F_BOXINST)
 #endif
+#ifndef MRT_LIN_PREFETCH_INST
+#define MRT_LIN_PREFETCH_INST 1
+#endif
 template <uint32_t F>
 static constexpr bool kLinSlabOps = MRT_FAST && (F & FT_LIN) != 0 && (F & (FT_BVHW | FT_VOLUME | FT_TEX | FT_MOVING)) == 0;
 
 template <uint32_t F>
 MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, const LStack& L, Pcg& rng, PhaseClock& ph) {
     constexpr bool INST = (F & FT_INST) != 0;
+    // (parked even when every instance is a one-step box instance, which never displaces it: skipping
+    // the park there measured 0.8% slower, C2 through the interpreter, profiles/r05_ab.txt section 10)
     if (INST) lin_save_ray(L, r);
     Ray cur = r;
     float closest = FLT_MAX_;
@@ -537,6 +542,19 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
     if (INST) r = lin_load_ray(L);
     if (hnode == MRT_NONE) return false;
     if (INST && hinst != MRT_NONE) {
+        // the instance op's words (per lane: vector loads) fetched before the record's node, so the
+        // two sets of loads are in flight together instead of one round trip after the other
+        // (only the words lin_untransform reads: its code, the offset f[0..2], rotate_y's f[6..7], the
+        // fused translation f[8..10])
+#if MRT_LIN_PREFETCH_INST
+        const LinOp* ip = S.prog + hinst;
+        LinOp io;
+        io.code = ip->code;
+        for (int k = 0; k < 3; k++) io.f[k] = ip->f[k];
+        for (int k = 6; k < 11; k++) io.f[k] = ip->f[k];
+#else
+        const LinOp& io = S.prog[hinst];
+#endif
         if (!hdone) {
             const float* b = L.save + L.lane + 9 * 64;
             Ray ir = r;
@@ -544,7 +562,7 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
             ir.d = f3{b[192], b[256], b[320]};
             lin_prim_rec<F>(S, hnode, ir, closest, rec);
         }
-        lin_untransform(S.prog[hinst], rec);  // per-lane instance: vector loads
+        lin_untransform(io, rec);
     } else if (!hdone) {
         lin_prim_rec<F>(S, hnode, r, closest, rec);
     }
