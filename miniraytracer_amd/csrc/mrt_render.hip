@@ -1287,7 +1287,11 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         HIPCHK(hipEventRecord(s->ev[2 * s->n_launch + 1], q));
         s->n_launch++;
         if (handover) {  // this launch's rounding-critical paths, exact, into the radiance buffer (fold next)
-            hipLaunchKernelGGL(PL.retrace, dim3(kRetraceGroups), dim3(64), PL.retrace_lds, q, P);
+            // (the exact arithmetic walks the program as compiled: the tolerance contract's rewrite has
+            // ops -- a room's slab test, one-step box instances -- only the fast builds compile)
+            PathParams PR = P;
+            PR.sc.prog = s->S.prog;
+            hipLaunchKernelGGL(PL.retrace, dim3(kRetraceGroups), dim3(64), PL.retrace_lds, q, PR);
             HIPCHK(hipGetLastError());
         }
         // the last chunk's full fold finishes the render (no preview: no snapshot of acc needed;

@@ -681,14 +681,20 @@ def test_c3_whole_image_own_spp_within_tolerance(gpu, numerics):
     assert abs(c["ray_ratio"] - 1) < FULL_RAYS[numerics], c
 
 
-def test_rounding_critical_paths_retraced_exactly(gpu, monkeypatch):
+@pytest.mark.parametrize("walk", ["specialised", "interpreter"])
+def test_rounding_critical_paths_retraced_exactly(gpu, monkeypatch, walk):
     """Tolerance contract: the paths whose light sample is rounding-critical (a direction nearly in
     the light's plane, or a point on its edge below the surface: mrt_shade.h crit_check) are listed
     by the fast kernel and traced again by the exact arithmetic, whose radiance replaces theirs
     before the fold.  A C2 render large enough to hold a
     few hundred of them: (1) the listed count is reported (mrt_kernel_info.handed_over); (2) the
     image differs from the one without the hand-over (MRT_RETRACE=0) only in pixels holding such a
-    path, and it moves towards the exact contract's image there."""
+    path, and it moves towards the exact contract's image there.  Through the shape-specialised
+    Cornell walk and through the interpreter (MRT_NO_SIG=1), whose tolerance-contract program is
+    rewritten (a room's slab test, one-step box instances): the exact retrace walks the program as
+    compiled."""
+    if walk == "interpreter":
+        monkeypatch.setenv("MRT_NO_SIG", "1")
     w, h, spp = 250, 250, 256
     sc = gpu.select_scene(5, 1.0)
     d = gpu.render_desc(w, h, spp, numerics="fast")
