@@ -183,6 +183,17 @@ static constexpr bool kCrit = MRT_CRIT && MRT_FAST && (F & FT_BIASED) != 0;
 // argument segment
 template <uint32_t F>
 static constexpr uint32_t kCritOff = kCrit<F> ? (uint32_t)offsetof(PathParams, rt) : 0u;
+// the path kernel's scene arguments (P.sc) through an opaque pointer into the argument segment (P is
+// the kernel's only argument: it starts the segment): read where used, not held in registers
+MRT_DFN const DScene& kernarg_scene() {
+    const MRT_CONST_AS DScene* sp =
+        (const MRT_CONST_AS DScene*)((const MRT_CONST_AS char*)__builtin_amdgcn_kernarg_segment_ptr() + offsetof(PathParams, sc));
+    asm volatile("" : "+s"(sp));
+    return *(const DScene*)sp;
+}
+#ifndef MRT_OPAQUE_RESUME
+#define MRT_OPAQUE_RESUME 0  // the same in the room + mesh kernels' resumable loop: measured C3 -0.6%, C4 0 (A/B hook)
+#endif
 template <uint32_t F> struct PathQ {
     static constexpr bool on = MRT_PATHQ && (F & FT_MESH) == 0 && !TreeOf<F>::on;
     // LDS words per lane slot: o, dir, time, PCG state + inc, index (12); + the wave's claim state
@@ -566,6 +577,10 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
         w.hdone = false;
         HitRec rec;
         for (;;) {
+#if MRT_OPAQUE_RESUME
+            const DScene& S = kernarg_scene();  // (shadows P.sc for this iteration)
+            const MRT_CONST_AS LinOp* prog = const_ptr(S.prog);
+#endif
             take_paths([&](float u, float v) {
                 ps.r = camera_ray(S, ps.rng, u, v);
                 phase = PH_BEGIN;
@@ -640,11 +655,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
             // the scene's kernel arguments re-derived each iteration through an opaque constant
             // pointer: its fields are scalar-loaded at their uses in the segment instead of held in
             // SGPRs across the path loop (which spilled them into VGPR lanes)
-            // (P is the kernel's only argument: it starts the kernarg segment)
-            const MRT_CONST_AS DScene* sp = (const MRT_CONST_AS DScene*)((const MRT_CONST_AS char*)__builtin_amdgcn_kernarg_segment_ptr() +
-                                                                         offsetof(PathParams, sc));
-            asm volatile("" : "+s"(sp));
-            const DScene& Sseg = *(const DScene*)sp;
+            const DScene& Sseg = kernarg_scene();
 #else
             const DScene& Sseg = S;
 #endif
