@@ -15,7 +15,15 @@ BASE="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-fast-math -fno-slp-vectori
 /opt/rocm/bin/hipcc $BASE -DMRT_TABLE_FAST=1 $flags -c miniraytracer_amd/csrc/mrt_kernels.hip -o exp/obj_$tag/mrt_kernels_fast.o
 # the denormal-flushing build of the same flags (the kFtzVariant variants; run with MRT_FTZ=0 to A/B
 # without it)
-/opt/rocm/bin/hipcc $BASE -DMRT_TABLE_FAST=1 $flags -fgpu-flush-denormals-to-zero -DMRT_TABLE_FTZ=1 -c miniraytracer_amd/csrc/mrt_kernels.hip -o exp/obj_$tag/mrt_kernels_fastz.o
+# (FTZ_PLAIN=1: the Makefile's FTZ build instead -- for flags only one translation unit may carry,
+# e.g. -DMRT_PHASES; run with MRT_FTZ=0)
+FZ=exp/obj_$tag/mrt_kernels_fastz.o
+if [ -n "${FTZ_PLAIN:-}" ]; then
+  make -s build/obj/mrt_kernels_fastz.o
+  FZ=build/obj/mrt_kernels_fastz.o
+else
+  /opt/rocm/bin/hipcc $BASE -DMRT_TABLE_FAST=1 $flags -fgpu-flush-denormals-to-zero -DMRT_TABLE_FTZ=1 -c miniraytracer_amd/csrc/mrt_kernels.hip -o $FZ
+fi
 EX=build/obj/mrt_kernels_exact.o
 # host defines (MRT_NPART, MRT_BATCH, ...) change PathParams / the claim protocol: the exact TU must
 # be built with them too, or the exact kernel reads a foreign parameter layout (a GPU memory fault)
@@ -35,6 +43,6 @@ if [ -n "${PEX_FLAGS:-}" ]; then  # ... or built with extra flags
   /opt/rocm/bin/hipcc $BASE -ffp-contract=off $(make -s -f Makefile -p 2>/dev/null | sed -n 's/^PEXFLAGS = //p') $PEX_FLAGS -c miniraytracer_amd/csrc/mrt_kernels.hip -o exp/obj_$tag/mrt_kernels_pex.o
   PX=exp/obj_$tag/mrt_kernels_pex.o
 fi
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $RO $EX $PX exp/obj_$tag/mrt_kernels_fast.o exp/obj_$tag/mrt_kernels_fastz.o \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $RO $EX $PX exp/obj_$tag/mrt_kernels_fast.o $FZ \
     build/obj/mrt_cpu.o build/obj/scene_builder.o build/obj/mrt_common.o -ldl -o exp/libmrt_$tag.so
 echo "built exp/libmrt_$tag.so"
