@@ -98,14 +98,15 @@ def samplers(st, sq, n, which):
 
 
 # ---- the reference binary (oracle/_ref) ----
-def ref_binary(exact=True):
-    p = os.path.join(REF_DIR, "mrt_ref_exact" if exact else "mrt_ref")
+def ref_binary(exact=True, name=None):
+    p = os.path.join(REF_DIR, name or ("mrt_ref_exact" if exact else "mrt_ref"))
     return p if os.path.exists(p) else None
 
 
-def run_ref(args, exact=True, cwd=None, timeout=3600):
-    """Run the reference oracle binary; returns the parsed JSON of its last stdout line."""
-    b = ref_binary(exact)
+def run_ref(args, exact=True, cwd=None, timeout=3600, name=None):
+    """Run the reference oracle binary (or the build `name` in oracle/_ref); returns the parsed JSON
+    of its last stdout line."""
+    b = ref_binary(exact, name)
     if b is None:
         raise FileNotFoundError("oracle/_ref not built")
     out = subprocess.run([b] + [str(a) for a in args], capture_output=True, text=True, cwd=cwd, timeout=timeout,

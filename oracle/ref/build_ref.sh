@@ -9,6 +9,8 @@
 #                  x86 FMA wherever one scalar expression multiplies and adds), glibc libm.
 #                  -march=x86-64-v3 instead of -march=native so the binary also runs on the GPU
 #                  box's host CPU (it is the cpu_baseline of bench.py); both have FMA.
+#   mrt_ref_v4     the same with -march=x86-64-v4 (AVX-512): what -march=native gives on an AVX-512
+#                  host; bench.py times it too where the host CPU has AVX-512F.
 #   mrt_ref_exact  the same build (same flags, so the same fused multiply-adds) with the float libm
 #                  calls interposed by (float)f((double)x) (harness.cpp, MRT_MATHMATCH): the
 #                  reference as shipped with the project's transcendentals.  This is the bit-exact
@@ -59,6 +61,7 @@ build() {  # name extra-flags
 }
 
 build mrt_ref
+build mrt_ref_v4 -march=x86-64-v4
 build mrt_ref_exact -DMRT_MATHMATCH
 # numerics-diagnosis builds (MRT_REF_VARIANTS=1): the reference with no contraction at all (with
 # the project's transcendentals: the rounds 1-3 pin; with glibc) and with unrestricted contraction
