@@ -334,6 +334,9 @@ MRT_DFN void lin_untransform(const OP& io, HitRec& rec) {
 #ifndef MRT_BOXINST
 #define MRT_BOXINST 1  // the one-step box instance (MRT_F_BOXINST)
 #endif
+#ifndef MRT_BOXINST_AABB
+#define MRT_BOXINST_AABB 0  // 1: the one-step box instance tests its instance's box first (measured 2.7% slower, A/B hook)
+#endif
 #ifndef MRT_LIN_PREFETCH_INST
 #define MRT_LIN_PREFETCH_INST 1
 #endif
@@ -474,10 +477,10 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
             bool in = on;
             if (kind == MRT_K_TRROTY) {
                 ci = moved_ray<kFastUnit<F>>(cur, sub(cur.o, f3{o.f[8], o.f[9], o.f[10]}));
-                if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, ci, tmin, closest);
+                if (MRT_BOXINST_AABB && in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, ci, tmin, closest);
                 ci = rotate_ray<kFastUnit<F>>(ci, o.f[6], o.f[7]);
             } else if (kind == MRT_K_ROTY) {
-                if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, ci, tmin, closest);
+                if (MRT_BOXINST_AABB && in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, ci, tmin, closest);
                 ci = rotate_ray<kFastUnit<F>>(ci, o.f[6], o.f[7]);
             } else {
                 ci = moved_ray<kFastUnit<F>>(cur, sub(cur.o, f3{o.f[0], o.f[1], o.f[2]}));

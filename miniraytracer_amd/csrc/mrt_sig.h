@@ -205,6 +205,17 @@ inline std::vector<LinOp> lin_rewrite_fast(const std::vector<LinOp>& prog) {
             depth--;
         }
     }
+    // the root object_list (op 0, its LIST_END just before the END op): its box test only rejects
+    // rays that miss the whole scene, and its two ops cost the lockstep walk two dispatch steps per
+    // ray; dropped (the children are tested by every lane anyway, at level 0)
+#ifndef MRT_REWRITE_ROOT
+#define MRT_REWRITE_ROOT 1
+#endif
+    if (MRT_REWRITE_ROOT && n >= 3 && (prog[0].code & 0xFFu) == LOP_LIST && prog[0].skip == n - 2 &&
+        (prog[n - 2].code & 0xFFu) == LOP_LIST_END && (prog[n - 1].code & 0xFFu) == LOP_END) {
+        del[0] = 1;
+        del[n - 2] = 1;
+    }
     // compact: each room's first wall becomes ROOM + ROOMDATA, the other walls go; skips re-linked
     std::vector<uint32_t> at(n + 1, 0);
     std::vector<LinOp> out;

@@ -316,20 +316,24 @@ def _lin_program(mrt, sid, rewritten):
 def test_program_rewrite_structure(mrt, sid):
     """The tolerance contract's program rewrite (mrt_sig.h lin_rewrite_fast): the Cornell rooms'
     inward-facing walls become one LOP_ROOM + LOP_ROOMDATA pair, an instance of one box.h list is
-    flagged MRT_F_BOXINST, nothing else changes, and every LIST / INST skip still lands on its END
-    op.  Scenes without rooms (0, 7) keep their program."""
-    LIST, LIST_END, INST, INST_END, ROOM, ROOMDATA = 3, 4, 5, 6, 10, 11
+    flagged MRT_F_BOXINST, the root object_list's LIST / LIST_END pair is dropped, nothing else
+    changes, and every LIST / INST skip still lands on its END op.  Scenes without rooms (0, 7) keep
+    their program but for the root pair."""
+    LIST, LIST_END, INST, INST_END, ROOM, ROOMDATA, END = 3, 4, 5, 6, 10, 11, 0
     c0, s0 = _lin_program(mrt, sid, False)
     c1, s1 = _lin_program(mrt, sid, True)
     op0, op1 = c0 & 0xFF, c1 & 0xFF
     assert ROOM not in op0 and ROOMDATA not in op0
+    root = bool(op0[0] == LIST and s0[0] == len(op0) - 2 and op0[-2] == LIST_END and op0[-1] == END)
+    assert root == (sid != 0)  # (an object_list at the root; scene 0 is a bvh_node)
     rooms = int((op1 == ROOM).sum())
     if sid in (5, 8, 9):
         assert rooms == 1 and op1[list(op1).index(ROOM) + 1] == ROOMDATA
-        # the room's walls (five rects in these scenes) replaced by the pair
-        assert len(op1) == len(op0) - 5 + 2
+        # the room's walls (five rects in these scenes) replaced by the pair, the root pair gone
+        assert len(op1) == len(op0) - 5 + 2 - 2
     else:
-        assert rooms == 0 and np.array_equal(c0 & ~np.uint32(0x20 << 16), c1 & ~np.uint32(0x20 << 16))
+        kept = np.concatenate([c0[1:-2], c0[-1:]]) if root else c0
+        assert rooms == 0 and np.array_equal(kept & ~np.uint32(0x20 << 16), c1 & ~np.uint32(0x20 << 16))
     boxinst = [(c >> 16) & 0x20 for c, o in zip(c1, op1) if o == INST]
     assert sum(1 for b in boxinst if b) == (1 if sid == 5 else 0)
     for i, (o, k) in enumerate(zip(op1, s1)):
