@@ -232,6 +232,16 @@ inline std::vector<LinOp> lin_rewrite_fast(const std::vector<LinOp>& prog) {
         const uint32_t op = o.code & 0xFFu;
         if ((op == LOP_LIST || op == LOP_INST || op == LOP_INST_END) && o.skip <= n) o.skip = at[o.skip];
     }
+    // MRT_F_LAST on the op the interpreter leaves for the END op (the room op steps over its data op,
+    // a one-step box instance or box.h list over its body): the walk ends there without one more
+    // dispatch step
+    for (uint32_t i = 0; i < out.size(); i++) {
+        const uint32_t op = out[i].code & 0xFFu, fl = (out[i].code >> 16) & 0xFFu;
+        uint32_t next = i + 1;
+        if (op == LOP_ROOM) next = i + 2;
+        else if ((op == LOP_INST && (fl & MRT_F_BOXINST)) || (op == LOP_LIST && (fl & MRT_F_BOX6))) next = out[i].skip + 1;
+        if (op != LOP_END && next < out.size() && (out[next].code & 0xFFu) == LOP_END) out[i].code |= MRT_F_LAST << 16;
+    }
     return out;
 }
 

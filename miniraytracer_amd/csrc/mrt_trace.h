@@ -160,6 +160,7 @@ struct DScene {
 #define MRT_F_NEEDUV 0x4u   /* set on upload when the node's material samples uv */
 #define MRT_F_BOX6 0x10u    /* set on upload on an object_list that is box.h's six rects (planes in f[6..11]) */
 #define MRT_F_BOXINST 0x20u /* tolerance-contract program: an instance outside instances whose body is one MRT_F_BOX6 list */
+#define MRT_F_LAST 0x40u    /* tolerance-contract program: the op after which the interpreter reaches the END op */
 #define MRT_K_TRROTY 11u    /* upload fuses translate(rotate_y(x)) into one instance node */
 #define MRT_K_BVHW 12u      /* upload: a bvh_node subtree over primitives / object_lists as wide nodes */
 

@@ -316,8 +316,9 @@ def _lin_program(mrt, sid, rewritten):
 def test_program_rewrite_structure(mrt, sid):
     """The tolerance contract's program rewrite (mrt_sig.h lin_rewrite_fast): the Cornell rooms'
     inward-facing walls become one LOP_ROOM + LOP_ROOMDATA pair, an instance of one box.h list is
-    flagged MRT_F_BOXINST, the root object_list's LIST / LIST_END pair is dropped, nothing else
-    changes, and every LIST / INST skip still lands on its END op.  Scenes without rooms (0, 7) keep
+    flagged MRT_F_BOXINST, the root object_list's LIST / LIST_END pair is dropped, the op after
+    which the walk reaches END is flagged MRT_F_LAST (exactly one), nothing else changes, and every
+    LIST / INST skip still lands on its END op.  Scenes without rooms (0, 7) keep
     their program but for the root pair."""
     LIST, LIST_END, INST, INST_END, ROOM, ROOMDATA, END = 3, 4, 5, 6, 10, 11, 0
     c0, s0 = _lin_program(mrt, sid, False)
@@ -333,7 +334,8 @@ def test_program_rewrite_structure(mrt, sid):
         assert len(op1) == len(op0) - 5 + 2 - 2
     else:
         kept = np.concatenate([c0[1:-2], c0[-1:]]) if root else c0
-        assert rooms == 0 and np.array_equal(kept & ~np.uint32(0x20 << 16), c1 & ~np.uint32(0x20 << 16))
+        assert rooms == 0 and np.array_equal(kept & ~np.uint32(0x60 << 16), c1 & ~np.uint32(0x60 << 16))
+    assert int(((c1 >> 16) & 0x40 != 0).sum()) == 1 and not ((c0 >> 16) & 0x40).any()
     boxinst = [(c >> 16) & 0x20 for c, o in zip(c1, op1) if o == INST]
     assert sum(1 for b in boxinst if b) == (1 if sid == 5 else 0)
     for i, (o, k) in enumerate(zip(op1, s1)):
