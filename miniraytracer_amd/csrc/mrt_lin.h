@@ -388,6 +388,60 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
             hinst = h ? inst : hinst;
             hdone = h ? false : hdone;
             PH_MARK(ph, 9);
+        } else if (MRT_FAST_ROOM && kLinSlabOps<F> && op == LOP_ROOM) {
+            float t;
+            uint32_t face;
+            const bool h = on & lin_room_hit(o, cur, tmin, closest, &t, &face);
+            // LOP_ROOMDATA (the next op): each face's node, read at a per-lane index (selecting it
+            // from the op's six uniform words instead measured 3.5% slower, profiles/r05_ab.txt 17)
+            const MRT_CONST_AS uint32_t* fnode = reinterpret_cast<const MRT_CONST_AS uint32_t*>(prog[pc + 1].f);
+            closest = h ? t : closest;
+            hnode = h ? fnode[face] : hnode;
+            hinst = h ? inst : hinst;
+            hdone = h ? false : hdone;
+            pc++;
+        } else if (MRT_BOXINST && kLinSlabOps<F> && INST && op == LOP_INST && (LOP_FLAGS(o) & MRT_F_BOXINST)) {  // uniform
+            // an instance of one box.h list, outside instances (cur is the query ray): the instance
+            // ray from it in registers, the instance's box test and the list's slab test, the body
+            // skipped -- the operations of the INST / LIST / LIST_END / INST_END steps below, without
+            // parking and reloading the query ray
+            const uint32_t kind = LOP_KIND(o);
+            Ray ci = cur;
+            bool in = on;
+            if (kind == MRT_K_TRROTY) {
+                ci = moved_ray<kFastUnit<F>>(cur, sub(cur.o, f3{o.f[8], o.f[9], o.f[10]}));
+                if (MRT_BOXINST_AABB && in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, ci, tmin, closest);
+                ci = rotate_ray<kFastUnit<F>>(ci, o.f[6], o.f[7]);
+            } else if (kind == MRT_K_ROTY) {
+                if (MRT_BOXINST_AABB && in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, ci, tmin, closest);
+                ci = rotate_ray<kFastUnit<F>>(ci, o.f[6], o.f[7]);
+            } else {
+                ci = moved_ray<kFastUnit<F>>(cur, sub(cur.o, f3{o.f[0], o.f[1], o.f[2]}));
+            }
+            const auto lo = op_at(pc + 1);
+            float t;
+            uint32_t c;
+            const bool h = in & lin_box6_hit(lo, ci, tmin, closest, &t, &c);
+            closest = h ? t : closest;
+            hnode = h ? prog[pc + 2 + c].node : hnode;
+            hinst = h ? pc : hinst;
+            hdone = h ? false : hdone;
+            if (h) {  // the instance-frame ray of the hit, for the record (as at LOP_INST_END)
+                float* b = L.save + L.lane + 9 * 64;
+                b[0] = ci.o.x; b[64] = ci.o.y; b[128] = ci.o.z;
+                b[192] = ci.d.x; b[256] = ci.d.y; b[320] = ci.d.z;
+            }
+            pc = o.skip;  // its LOP_INST_END
+        } else if (MRT_FAST_BOX && kLinSlabOps<F> && op == LOP_LIST && (LOP_FLAGS(o) & MRT_F_BOX6)) {  // uniform
+            // box.h's six rects as one slab test (its own box test implied), the list skipped
+            float t;
+            uint32_t c;
+            const bool h = on & lin_box6_hit(o, cur, tmin, closest, &t, &c);
+            closest = h ? t : closest;
+            hnode = h ? prog[pc + 1 + c].node : hnode;
+            hinst = h ? inst : hinst;
+            hdone = h ? false : hdone;
+            pc = o.skip;  // past its LOP_LIST_END
         } else if ((F & FT_MESH) && op == LOP_MESH) {
             if (on && mesh_hit<true>(S, ld_node(const_ptr(S.nodes) + o.node), cur, tmin, closest, rec, true, L)) {
                 closest = rec.t;
@@ -443,66 +497,12 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
                 hdone = true;
             }
             PH_MARK(ph, 11);
-        } else if (MRT_FAST_ROOM && kLinSlabOps<F> && op == LOP_ROOM) {
-            float t;
-            uint32_t face;
-            const bool h = on & lin_room_hit(o, cur, tmin, closest, &t, &face);
-            // LOP_ROOMDATA (the next op): each face's node, read at a per-lane index (selecting it
-            // from the op's six uniform words instead measured 3.5% slower, profiles/r05_ab.txt 17)
-            const MRT_CONST_AS uint32_t* fnode = reinterpret_cast<const MRT_CONST_AS uint32_t*>(prog[pc + 1].f);
-            closest = h ? t : closest;
-            hnode = h ? fnode[face] : hnode;
-            hinst = h ? inst : hinst;
-            hdone = h ? false : hdone;
-            pc++;
-        } else if (MRT_FAST_BOX && kLinSlabOps<F> && op == LOP_LIST && (LOP_FLAGS(o) & MRT_F_BOX6)) {  // uniform
-            // box.h's six rects as one slab test (its own box test implied), the list skipped
-            float t;
-            uint32_t c;
-            const bool h = on & lin_box6_hit(o, cur, tmin, closest, &t, &c);
-            closest = h ? t : closest;
-            hnode = h ? prog[pc + 1 + c].node : hnode;
-            hinst = h ? inst : hinst;
-            hdone = h ? false : hdone;
-            pc = o.skip;  // past its LOP_LIST_END
         } else if (op == LOP_LIST) {  // object_list::hit box reject (scene_object.h:83)
             bool in = on;
             if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, cur, tmin, closest);
             lvl++;
             act = (act & ~(1u << lvl)) | ((uint32_t)in << lvl);
             if (!any_lane(in)) pc = o.skip - 1;
-        } else if (MRT_BOXINST && kLinSlabOps<F> && INST && op == LOP_INST && (LOP_FLAGS(o) & MRT_F_BOXINST)) {  // uniform
-            // an instance of one box.h list, outside instances (cur is the query ray): the instance
-            // ray from it in registers, the instance's box test and the list's slab test, the body
-            // skipped -- the operations of the INST / LIST / LIST_END / INST_END steps below, without
-            // parking and reloading the query ray
-            const uint32_t kind = LOP_KIND(o);
-            Ray ci = cur;
-            bool in = on;
-            if (kind == MRT_K_TRROTY) {
-                ci = moved_ray<kFastUnit<F>>(cur, sub(cur.o, f3{o.f[8], o.f[9], o.f[10]}));
-                if (MRT_BOXINST_AABB && in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, ci, tmin, closest);
-                ci = rotate_ray<kFastUnit<F>>(ci, o.f[6], o.f[7]);
-            } else if (kind == MRT_K_ROTY) {
-                if (MRT_BOXINST_AABB && in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, ci, tmin, closest);
-                ci = rotate_ray<kFastUnit<F>>(ci, o.f[6], o.f[7]);
-            } else {
-                ci = moved_ray<kFastUnit<F>>(cur, sub(cur.o, f3{o.f[0], o.f[1], o.f[2]}));
-            }
-            const auto lo = op_at(pc + 1);
-            float t;
-            uint32_t c;
-            const bool h = in & lin_box6_hit(lo, ci, tmin, closest, &t, &c);
-            closest = h ? t : closest;
-            hnode = h ? prog[pc + 2 + c].node : hnode;
-            hinst = h ? pc : hinst;
-            hdone = h ? false : hdone;
-            if (h) {  // the instance-frame ray of the hit, for the record (as at LOP_INST_END)
-                float* b = L.save + L.lane + 9 * 64;
-                b[0] = ci.o.x; b[64] = ci.o.y; b[128] = ci.o.z;
-                b[192] = ci.d.x; b[256] = ci.d.y; b[320] = ci.d.z;
-            }
-            pc = o.skip;  // its LOP_INST_END
         } else if (INST && op == LOP_INST) {
             const uint32_t kind = LOP_KIND(o);
             bool in = on;
