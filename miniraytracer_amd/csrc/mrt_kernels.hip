@@ -66,6 +66,12 @@ using namespace mrtd;
 #ifndef MRT_WPE_MESH
 #define MRT_WPE_MESH 7
 #endif
+// the room + mesh walk of the tolerance contract, fast arithmetic (C3) and path-exact (C4): 8 waves
+// (fast: 62 VGPRs, no VGPR spill; path-exact: 64, 9 spilled).  Round 5 against 7: teapot 17.01 vs
+// 17.51 ms per step, bunny 40.60 vs 41.07 (profiles/r05_ab.txt sections 22-23)
+#ifndef MRT_WPE_ROOM_MESH
+#define MRT_WPE_ROOM_MESH ((MRT_FAST || MRT_TABLE_PEX) ? 8 : MRT_WPE_MESH)
+#endif
 #ifndef MRT_WPE_LIN_GEN
 // the interpreter's compact variants (no program shape): 6 waves (80 VGPRs, spill-free).  Round 4
 // held them at 5 (96 VGPRs): the room op's per-lane axis select had become a lookup table in
@@ -77,7 +83,8 @@ using namespace mrtd;
 template <uint32_t F> struct PathOcc {
     static constexpr bool kWide = (F & (FT_BVHW | FT_TEX | FT_VOLUME)) != 0 || !(F & FT_LIN);
     static constexpr int W = kWide ? (!(F & FT_LIN) ? 4 : MRT_WPE_WIDE)
-                             : ((F & FT_MESH) != 0 ? MRT_WPE_MESH : (MRT_SIG_OF(F) != SIG_NONE ? MRT_WPE_LIN : MRT_WPE_LIN_GEN));
+                             : ((F & FT_MESH) != 0 ? (MRT_SIG_OF(F) == SIG_ROOM_MESH ? MRT_WPE_ROOM_MESH : MRT_WPE_MESH)
+                                                   : (MRT_SIG_OF(F) != SIG_NONE ? MRT_WPE_LIN : MRT_WPE_LIN_GEN));
 };
 #if defined(MRT_EXPERIMENTS) && defined(MRT_PHASES)  // build ONE of the two TUs with it
 __device__ unsigned long long g_phases[12];
