@@ -202,9 +202,10 @@ MRT_DFN f3 biased_pdf_generate(const DScene& S, f3 origin, float time, Pcg& rng,
 //      its earlier bounces: a window of MRT_CRIT_TOL relative to the origin's height (2^-16, ~140
 //      ulps at the Cornell light's 554);
 //  (2) the sampled point lies on the light's edge (a draw within MRT_EDGE_TOL of 0 or 1, 2^-18:
-//      ~0.5 ulp of 555 on the Cornell light's 130-wide side, a few times the rounding of the hit
-//      point pdf_value recomputes from the origin) and below the surface: the recomputed point can
-//      fall outside the rect by rounding, pdf 0, and with the cosine pdf 0 too the sample is 0 / 0.
+//      5e-4 on the Cornell light's 130-wide side, ~8 ulps of 555, a few times the rounding of the
+//      hit point pdf_value recomputes from the origin) and below the surface: the recomputed point
+//      can fall outside the rect by rounding, pdf 0, and with the cosine pdf 0 too the sample is
+//      0 / 0.
 // Under the fast arithmetic these events fall on other paths than the reference's (C3 at 4096
 // spp: 98% of the tolerance contract's squared error in 100 such pixels).  Such paths are traced
 // again with the exact arithmetic (mrt_retrace_kernel), whose radiance replaces the fast one; the
