@@ -78,11 +78,12 @@ def parse():
                          "step (the gather's device-side work; the xGMI transfer itself is not emulated)")
     ap.add_argument("--chunk-samples", type=int, default=0,
                     help="samples per path-kernel launch (0: the library's choice)")
-    ap.add_argument("--fold", choices=["auto", "lean", "full"], default="full",
-                    help="mode-0 fold kernel: full (after its render's path kernel; the default), lean "
-                         "(MRT_RF_FOLD_BEHIND, beside the other contexts' path kernels: 8.35-8.45 ms per "
-                         "C2 step in most runs but 9.8-10.1 in about one of five, against a steady 8.62 "
-                         "for full), auto = lean from ~96 M paths per rank")
+    ap.add_argument("--fold", choices=["auto", "lean", "full", "async"], default="auto",
+                    help="mode-0 fold: async (MRT_RF_FOLD_ASYNC, one context: each render's fold on the context's "
+                         "own stream, beside the next render's path kernel; C2 8.28 ms per step against 8.65 for "
+                         "full), full (after its render's path kernel), lean (MRT_RF_FOLD_BEHIND, beside the other "
+                         "contexts' path kernels: 8.35-8.45 ms per C2 step in most runs but 9.8-10.1 in about one "
+                         "of five); auto (default) = async at one context, full with several")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="render contexts used round-robin on their own HIP streams (0 = auto: 3 when a rank "
                          "traces fewer than ~100 M paths per step, else 1).  With several contexts the GPU "
@@ -366,11 +367,14 @@ def main():
     # needs ~ns load round trips whatever the pixel count: it wins while the rank's path kernel is
     # long (C2 per-rank share, lean vs full, ms/step: 1 rank 8.36 / 8.59, 2: 4.16 / 4.30, 4: 2.19 /
     # 2.16, 8: 1.19 / 1.15; round 2) -- auto: lean from ~96 M paths per rank, with several contexts
-    lean_fold = args.fold == "lean" or (args.fold == "auto" and npipe > 1 and n_paths_local >= 96_000_000)
+    lean_fold = args.fold == "lean"
+    # auto: one context -> each render's fold beside the next render's path kernel (C2: 8.28 vs 8.65
+    # ms per step, profiles/r05_ab.txt section 27); several contexts -> the full fold after the kernel
+    async_fold = args.fold == "async" or (args.fold == "auto" and npipe == 1)
     def desc_of(numerics):
         return m.render_desc(args.width, args.height, args.samples, depth=args.depth, tile_size=args.tile_size,
                              rank=d_rank, world=d_world, numerics=numerics, chunk_samples=args.chunk_samples,
-                             flags=m._lib.RF_FOLD_BEHIND if lean_fold else 0)
+                             flags=m._lib.RF_FOLD_BEHIND if lean_fold else (m._lib.RF_FOLD_ASYNC if async_fold else 0))
 
     desc = desc_of(args.numerics)
     for r in rnds:
@@ -395,6 +399,9 @@ def main():
     rays = torch.zeros(1, dtype=torch.int64, device=dev)  # every context adds its rays here (device atomics)
     stream = torch.cuda.current_stream(dev)
     streams = [stream] + [torch.cuda.Stream(dev) for _ in range(npipe - 1)]
+    # async fold: the gather waits for a render's fold on a stream of its own, so the next render's
+    # path kernel is not ordered after it
+    gstream = torch.cuda.Stream(dev) if (async_fold and world > 1) else None
 
     pending = [None]
     sent = [None] * nbuf  # the gather that last read output buffer b
@@ -416,7 +423,12 @@ def main():
                 # the next render: finish the previous step's gather, then start this one's
                 if pending[0] is not None:
                     tg.finish(pending[0])
-                pending[0] = sent[b] = tg.start(outs[b])
+                if gstream is not None:
+                    ctx[0][j].join(gstream.cuda_stream)
+                    with torch.cuda.stream(gstream):
+                        pending[0] = sent[b] = tg.start(outs[b])
+                else:
+                    pending[0] = sent[b] = tg.start(outs[b])
             elif eg is not None:
                 eg.scatter()  # rehearsal: rank 0's device-side share of the gather
 
@@ -588,7 +600,7 @@ def main():
                                    f"{desc.sqrt_samples ** 2} spp, depth {args.depth}, draw() accumulation",
                        "scene": args.scene, "width": args.width, "height": args.height,
                        "spp": desc.sqrt_samples ** 2, "depth": args.depth, "parallelism": f"tiles{world}",
-                       "tile_size": args.tile_size, "pipeline": npipe, "fold": "lean" if lean_fold else "full", "numerics": args.numerics,
+                       "tile_size": args.tile_size, "pipeline": npipe, "fold": "lean" if lean_fold else ("async" if async_fold else "full"), "numerics": args.numerics,
                        **({"emulated_share": f"rank {d_rank} of {d_world}" + (", + rank 0's scatter" if eg is not None else "")}
                           if d_world != world else {}),
                        "rays_per_step": nrays // args.steps},

@@ -9,6 +9,7 @@
  *   mrt_scene_upload                      (new) scene -> HBM, once, outside the timed region (main.cpp:309 vs 375)
  *   mrt_render / mrt_render_device        std::thread(draw|draw2) x N over work_queue + trace()
  *                                         main.cpp:66-118, 138-243, 347-382; work_queue.cpp:133-175
+ *   mrt_render_join                       the worker threads' join()             main.cpp:490-493
  *   mrt_progress                          work_queue::getPercentDone        work_queue.cpp:142-149, 168-175
  *   rays_out                              G_rayCounter                      main.cpp:55, 68, 403-405
  *   cancel                                G_isRunning                       main.cpp:54, 180, 235
@@ -133,6 +134,12 @@ typedef struct mrt_render_desc {
                                    another context's persistent path kernel instead of after it --
                                    for callers that pipeline renders on several streams; slower
                                    when nothing else runs (same bits either way) */
+#define MRT_RF_FOLD_ASYNC 0x20u /* GPU, one launch per render, no preview: the fold runs on the
+                                   context's own stream, beside the NEXT render's path kernel (two
+                                   radiance buffers used in turn; the path kernel leaves one wave slot
+                                   per SIMD for it) instead of after its own.  The output is complete
+                                   once mrt_render_join has ordered a stream after it (or the device
+                                   is synchronised).  Same bits as the fold in stream order. */
 #define MRT_RF_REF_ORDER 0x10u  /* CPU backend: the reference's own RNG order -- worker i draws from
                                    one PCG stream seeded by mrt_set_worker_seeds' i-th pair; mode 0 =
                                    draw() over work_queue_seq (tile -> pixel -> sample), mode 1 =
@@ -156,6 +163,10 @@ mrt_status mrt_render(mrt_scene* s, const mrt_render_desc* d, float* rgb_out, ui
  * `stream` (hipStream_t or NULL); rays are accumulated into the device uint64 *d_rays; nothing is
  * synchronised and nothing is allocated when the scene's workspace already fits (capturable). */
 mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, float* d_local, uint64_t* d_rays, void* stream);
+/* GPU backend only.  Enqueue on `stream` a wait for the context's last mrt_render_device (its
+ * fold, on the context's own stream under MRT_RF_FOLD_ASYNC): work enqueued on `stream` afterwards
+ * sees its output.  (No-op order for renders whose fold ran on their own stream.) */
+mrt_status mrt_render_join(mrt_scene* s, void* stream);
 /* Allocate/grow the scene's workspace for d (call once before timing mrt_render_device). */
 mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d);
 /* Per-path radiance (n_local*spp*3 floats, sample-major: [s][local pixel]) and ray counts of the

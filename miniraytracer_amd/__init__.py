@@ -173,6 +173,11 @@ class Renderer:
         check(lib().mrt_render_device(self._h, C.byref(desc), C.c_void_p(d_out_ptr), C.c_void_p(d_rays_ptr),
                                       C.c_void_p(stream_ptr)), "mrt_render_device")
 
+    def join(self, stream_ptr=0):
+        """Order a HIP stream after this context's last render_device (its fold runs on the context's
+        own stream under RF_FOLD_ASYNC): the worker threads' join() (main.cpp:490-493)."""
+        check(lib().mrt_render_join(self._h, C.c_void_p(stream_ptr)), "mrt_render_join")
+
     def preview(self, width, height):
         """The running render as the reference's UI thread sees G_linearBackBuffer (main.cpp:387-444):
         (H, W, 4) float32 image after `samples` samples of every pixel, callable from another thread

@@ -18,6 +18,7 @@ RF_PATH_DEBUG = 0x1
 RF_FAST = 0x2  # tolerance numerics contract (include/mrt.h MRT_RF_FAST)
 RF_PREVIEW = 0x4  # keep a progressive preview for mrt_preview (include/mrt.h MRT_RF_PREVIEW)
 RF_FOLD_BEHIND = 0x8  # mode-0 fold that runs beside another context's path kernel (include/mrt.h)
+RF_FOLD_ASYNC = 0x20  # the fold beside the next render's path kernel, on the context's own stream (include/mrt.h)
 RF_REF_ORDER = 0x10  # CPU backend: the reference's own RNG order (worker streams, work_queue order)
 DEVICE_CPU = -1  # mrt_scene_upload device of the CPU backend (include/mrt.h MRT_DEVICE_CPU)
 
@@ -109,6 +110,8 @@ def lib():
     L.mrt_render.restype = st
     L.mrt_render_device.argtypes = [C.c_void_p, C.POINTER(MrtRenderDesc), C.c_void_p, C.c_void_p, C.c_void_p]
     L.mrt_render_device.restype = st
+    L.mrt_render_join.argtypes = [C.c_void_p, C.c_void_p]
+    L.mrt_render_join.restype = st
     L.mrt_prepare.argtypes = [C.c_void_p, C.POINTER(MrtRenderDesc)]
     L.mrt_prepare.restype = st
     L.mrt_render_debug.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
@@ -151,7 +154,7 @@ EXPORTS = [
     "mrt_default_params", "mrt_parse_argv", "mrt_select_scene", "mrt_scene_blob_view",
     "mrt_scene_blob_dump_json", "mrt_free_string", "mrt_scene_blob_free", "mrt_init",
     "mrt_scene_upload", "mrt_scene_free", "mrt_default_render_desc", "mrt_local_pixels",
-    "mrt_render", "mrt_render_device", "mrt_prepare", "mrt_render_debug", "mrt_progress",
+    "mrt_render", "mrt_render_device", "mrt_render_join", "mrt_prepare", "mrt_render_debug", "mrt_progress",
     "mrt_tonemap_argb", "mrt_strerror", "mrt_last_error", "mrt_kernel_ms", "mrt_pack_obj",
     "mrt_scene_kernel_info", "mrt_preview", "mrt_lum_max_device", "mrt_tonemap_device", "mrt_worker_seeds", "mrt_set_worker_seeds",
 ]

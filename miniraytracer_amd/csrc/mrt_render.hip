@@ -145,6 +145,46 @@ __global__ void __launch_bounds__(256) mrt_fold_kernel(const float* __restrict__
     }
 }
 
+// The fold of an MRT_RF_FOLD_ASYNC render, on the context's own stream beside the next render's
+// path kernel, which leaves it one wave slot per SIMD (and its registers, MRT_WPE_LIN): one
+// 256-thread group per CU, each lane folding pixels grid-strided with FOLD_ASYNC_DEPTH samples in
+// flight -- the same operations in the same order as mrt_fold_kernel (bit-identical).
+#ifndef MRT_FOLD_ASYNC_GROUPS
+#define MRT_FOLD_ASYNC_GROUPS 1  // 256-thread groups per CU: one wave per SIMD
+#endif
+#ifndef FOLD_ASYNC_DEPTH
+#define FOLD_ASYNC_DEPTH 8
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
+mrt_fold_async_kernel(const float* __restrict__ rad, uint32_t npix, uint32_t ns, uint32_t mode, float max_lum, FoldEnd fe) {
+    const uint32_t step = gridDim.x * blockDim.x;
+    const uint32_t nthr = max(npix, fe.nreset);
+    for (uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x; lp < nthr; lp += step) {
+        reset_counters(fe, lp);
+        if (lp >= npix) continue;
+        f3 c{0.0f, 0.0f, 0.0f};  // one launch per render: from +0
+        const float* q = rad + (size_t)lp * 3;
+        const size_t stride = (size_t)npix * 3;
+        uint32_t s = 0;
+        for (; s + FOLD_ASYNC_DEPTH <= ns; s += FOLD_ASYNC_DEPTH) {
+            f3 v[FOLD_ASYNC_DEPTH];
+#pragma unroll
+            for (int k = 0; k < FOLD_ASYNC_DEPTH; k++) {
+                const float* e = q + (size_t)(s + k) * stride;
+                v[k] = f3{__builtin_nontemporal_load(e), __builtin_nontemporal_load(e + 1), __builtin_nontemporal_load(e + 2)};
+            }
+#pragma unroll
+            for (int k = 0; k < FOLD_ASYNC_DEPTH; k++) c = fold_sample(c, v[k], s + k, mode, max_lum);
+        }
+        for (; s < ns; s++) {
+            const float* e = q + (size_t)s * stride;
+            c = fold_sample(c, f3{e[0], e[1], e[2]}, s, mode, max_lum);
+        }
+        c = final_pixel(c, fe.ns, mode, max_lum);
+        fe.out[lp] = make_float4(c.x, c.y, c.z, 0.0f);
+    }
+}
+
 // draw()'s fold (mode 0) in 8 VGPRs: the persistent path kernel fills 7 waves per SIMD with 72
 // VGPRs each (504 of 512), so only a kernel this lean fits the 8th wave slot beside it -- the fold
 // of one render then runs under the next render's path kernel (bench.py --pipeline, two contexts
@@ -356,6 +396,18 @@ struct mrt_scene {
     // never sees its buffers rewritten or freed
     hipEvent_t ev_done = nullptr;
     bool ev_done_pending = false;
+    // MRT_RF_FOLD_ASYNC: renders alternate between two radiance buffers / counter slots (parity);
+    // the fold of parity p runs on fstream and ev_fold[p] marks its end, which the next path kernel
+    // writing parity p's buffers waits for
+    hipStream_t fstream = nullptr;
+    hipEvent_t ev_kern = nullptr;
+    hipEvent_t ev_fold[2] = {nullptr, nullptr};
+    bool fold_pending[2] = {false, false};
+    uint32_t par = 0;
+    float* d_rad2 = nullptr;
+    size_t rad2_cap = 0;
+    uint32_t n_cu = 0;
+    uint32_t prog_base = 0;  // launch slot of the current render's counters and progress snapshots
     unsigned long long* d_rays = nullptr;
     uint32_t features = 0, variant = 0;
     uint32_t lds_frames = 0, lds_rays = 0, lds_mesh = 0, lds_save = 0;
@@ -944,6 +996,7 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     const std::vector<BvhWide>& bwide = T.bwide;
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
+    s->n_cu = (uint32_t)prop.multiProcessorCount;
     // resident workgroups per CU: one 256-thread group = one wave per SIMD (a 64-thread group =
     // a quarter of that); VGPRs (512 per SIMD lane, granule 8) and LDS (160 KiB per CU) bound it.
     // (The runtime occupancy query under-counts gfx950 register budgets, so it is computed from
@@ -1028,7 +1081,10 @@ extern "C" void mrt_scene_free(mrt_scene* s) {
     if (s->h_prev) (void)hipHostFree(s->h_prev);
     if (s->h_seq) (void)hipHostFree(s->h_seq);
     if (s->ev_done) (void)hipEventDestroy(s->ev_done);
-    for (void* p : {(void*)s->d_counters, (void*)s->d_pixels, (void*)s->d_sdist, (void*)s->d_rad, (void*)s->d_path_rays, (void*)s->d_acc,
+    if (s->fstream) (void)hipStreamDestroy(s->fstream);
+    for (hipEvent_t e : {s->ev_kern, s->ev_fold[0], s->ev_fold[1]})
+        if (e) (void)hipEventDestroy(e);
+    for (void* p : {(void*)s->d_rad2, (void*)s->d_counters, (void*)s->d_pixels, (void*)s->d_sdist, (void*)s->d_rad, (void*)s->d_path_rays, (void*)s->d_acc,
                     (void*)s->d_lev, (void*)s->d_out, (void*)s->d_prev, (void*)s->d_rt})
         if (p) (void)hipFree(p);
     delete s;
@@ -1126,6 +1182,16 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
     s->chunk = chunk;
     size_t paths = (size_t)s->npix * s->chunk;
     if ((st = grow(s, (void**)&s->d_rad, &s->rad_cap, paths * 12))) return st;
+    if (d->flags & MRT_RF_FOLD_ASYNC) {
+        if (s->chunk != ns || (d->flags & (MRT_RF_PREVIEW | MRT_RF_PATH_DEBUG | MRT_RF_FOLD_BEHIND)))
+            return mrt_internal_fail(MRT_ERR_INVALID, "MRT_RF_FOLD_ASYNC: one launch per render (chunk_samples 0 or spp), "
+                                                      "no preview, debug or lean fold");
+        if ((st = grow(s, (void**)&s->d_rad2, &s->rad2_cap, paths * 12))) return st;
+        if (!s->fstream) HIPCHK(hipStreamCreateWithFlags(&s->fstream, hipStreamNonBlocking));
+        if (!s->ev_kern) HIPCHK(hipEventCreateWithFlags(&s->ev_kern, hipEventDisableTiming));
+        for (hipEvent_t& e : s->ev_fold)
+            if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
     if ((d->flags & MRT_RF_FAST) && !(d->flags & MRT_RF_PATH_DEBUG) && s->pl[1].handover &&
         (st = grow(s, (void**)&s->d_rt, &s->rt_cap, (size_t)kRtCap * sizeof(uint32_t))))
         return st;
@@ -1157,6 +1223,7 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
     s->lev_rows = std::max<uint32_t>(d->max_bounces, 1);
     if ((st = grow(s, (void**)&s->d_lev, &s->lev_cap, (size_t)s->lev_rows * s->max_threads * 16))) return st;
     uint32_t launches = (ns + s->chunk - 1) / s->chunk;
+    launches = std::max(launches, 2u);  // (slots 0 / 1: the two parities of MRT_RF_FOLD_ASYNC renders)
     const size_t cnt_words = (size_t)MRT_CNT_SLOTS * MRT_COUNTER_STRIDE;  // per launch
     {
         void* const before = s->d_counters;
@@ -1223,6 +1290,20 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
     s->n_launch = 0;
     s->last_numerics = (d->flags & MRT_RF_FAST) ? 1u : 0u;
     const bool preview = (d->flags & MRT_RF_PREVIEW) != 0;
+    // MRT_RF_FOLD_ASYNC: this render writes the radiance buffer and counter slot of its parity, whose
+    // last fold (an earlier render's, on fstream) must have ended; any other render waits for both
+    const bool async = (d->flags & MRT_RF_FOLD_ASYNC) != 0;
+    const uint32_t par = async ? s->par : 0u;
+    if (async) s->par ^= 1u;
+    for (uint32_t p = 0; p < 2; p++)
+        if (s->fold_pending[p] && (!async || p == par)) HIPCHK(hipStreamWaitEvent(q, s->ev_fold[p], 0));
+    {
+        std::lock_guard<std::mutex> lk(s->prog_mu);
+        s->prog_base = par;
+    }
+    float* const d_rad = par ? s->d_rad2 : s->d_rad;
+    unsigned long long* const d_cnt = (unsigned long long*)(s->d_counters + (size_t)par * MRT_CNT_SLOTS * MRT_COUNTER_STRIDE);
+    unsigned long long* const h_prog = (unsigned long long*)(s->h_prog + (size_t)par * MRT_NPART);
     uint32_t seq = 0;
     if (preview) {  // a new render: no snapshot yet (sequence 0), in stream order
         std::lock_guard<std::mutex> lk(s->prog_mu);
@@ -1268,10 +1349,10 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         }
         P.seed = d->seed;
         P.max_bounces = d->max_bounces;
-        P.rad = s->d_rad;
+        P.rad = d_rad;
         P.path_rays = (d->flags & MRT_RF_PATH_DEBUG) ? s->d_path_rays : nullptr;
-        P.counter = (unsigned long long*)(s->d_counters + (size_t)s->n_launch * MRT_CNT_SLOTS * MRT_COUNTER_STRIDE);
-        P.hprog = (unsigned long long*)(s->h_prog + (size_t)s->n_launch * MRT_NPART);
+        P.counter = d_cnt + (size_t)s->n_launch * MRT_CNT_SLOTS * MRT_COUNTER_STRIDE;
+        P.hprog = h_prog + (size_t)s->n_launch * MRT_NPART;
         P.cancel = (const int*)(s->d_counter + 4);
         P.rays = d_rays ? (unsigned long long*)d_rays : s->d_rays;
         P.lev = s->d_lev;
@@ -1294,6 +1375,18 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
             hipLaunchKernelGGL(PL.retrace, dim3(kRetraceGroups), dim3(64), PL.retrace_lds, q, PR);
             HIPCHK(hipGetLastError());
         }
+        if (async) {  // (one launch: mrt_prepare) the fold beside the next render's path kernel
+            HIPCHK(hipEventRecord(s->ev_kern, q));
+            HIPCHK(hipStreamWaitEvent(s->fstream, s->ev_kern, 0));
+            FoldEnd fe{(float4*)d_local, ns, d_cnt, h_prog, MRT_CNT_SLOTS, MRT_NPART};
+            hipLaunchKernelGGL(mrt_fold_async_kernel, dim3(s->n_cu * MRT_FOLD_ASYNC_GROUPS), dim3(256), 0, s->fstream, d_rad, s->npix, ns,
+                               d->mode, d->max_luminance, fe);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipEventRecord(s->ev_fold[par], s->fstream));
+            s->fold_pending[par] = true;
+            s->last_paths = P.n_paths;
+            continue;
+        }
         // the last chunk's full fold finishes the render (no preview: no snapshot of acc needed;
         // the 8-VGPR lean fold cannot take the division as well: a final kernel follows it)
         const bool lean = (d->flags & MRT_RF_FOLD_BEHIND) && d->mode == 0;
@@ -1303,9 +1396,9 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         const uint32_t nthr = std::max(s->npix, fe.nreset);
         if (lean)
             hipLaunchKernelGGL(mrt_fold_lean_kernel, dim3((s->npix + MRT_FOLD_LEAN_WG - 1) / MRT_FOLD_LEAN_WG), dim3(MRT_FOLD_LEAN_WG), 0, q,
-                               s->d_rad, s->d_acc, s->npix, s1 - s0, (uint32_t)(s0 == 0));
+                               d_rad, s->d_acc, s->npix, s1 - s0, (uint32_t)(s0 == 0));
         else
-            hipLaunchKernelGGL(mrt_fold_kernel, dim3((nthr + 255) / 256), dim3(256), 0, q, s->d_rad, s->d_acc, s->npix, s0, s1, d->mode,
+            hipLaunchKernelGGL(mrt_fold_kernel, dim3((nthr + 255) / 256), dim3(256), 0, q, d_rad, s->d_acc, s->npix, s0, s1, d->mode,
                                d->max_luminance, fe);
         HIPCHK(hipGetLastError());
         if (preview) {  // the image after s1 samples, copied under the sequence lock
@@ -1328,7 +1421,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
                            d->max_luminance, (unsigned long long*)s->d_counters, (unsigned long long*)s->h_prog, nreset, launches * MRT_NPART);
         HIPCHK(hipGetLastError());
     }
-    HIPCHK(hipEventRecord(s->ev_done, q));
+    HIPCHK(hipEventRecord(s->ev_done, async ? s->fstream : q));
     s->ev_done_pending = true;
     s->n_chunks.store(launches, std::memory_order_release);  // progress reads start once every launch and its events are enqueued
     return MRT_OK;
@@ -1380,6 +1473,17 @@ extern "C" mrt_status mrt_render(mrt_scene* s, const mrt_render_desc* d, float* 
     return MRT_OK;
 }
 
+// the worker threads' join (main.cpp:490-493) as stream order: `stream` waits for the context's
+// last render, including a fold on the context's own stream (MRT_RF_FOLD_ASYNC)
+extern "C" mrt_status mrt_render_join(mrt_scene* s, void* stream) {
+    MRT_GPU_ONLY(s, "mrt_render_join");
+    if (!s) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_render_join: null");
+    if (!s->ev_done) return MRT_OK;  // no render yet
+    HIPCHK(hipSetDevice(s->device));
+    HIPCHK(hipStreamWaitEvent((hipStream_t)stream, s->ev_done, 0));
+    return MRT_OK;
+}
+
 extern "C" mrt_status mrt_render_debug(mrt_scene* s, float* path_rgb, uint32_t* path_rays, uint64_t n_paths) {
     MRT_GPU_ONLY(s, "mrt_render_debug");
     if (!s || !(s->wdesc.flags & MRT_RF_PATH_DEBUG) || n_paths != s->last_paths)
@@ -1400,7 +1504,7 @@ extern "C" mrt_status mrt_progress(mrt_scene* s, float* pct) {
     if (s->cpu) return mrt_cpu_progress(s->cpu, pct);
     std::lock_guard<std::mutex> lk(s->prog_mu);
     const size_t n = s->n_chunks.load(std::memory_order_acquire);
-    if (n == 0 || !s->h_prog || s->h_prog_cap < n || s->ev.size() < 2 * n || s->h_seen.size() < n * MRT_NPART) return MRT_OK;  // not started
+    if (n == 0 || !s->h_prog || s->h_prog_cap < s->prog_base + n || s->ev.size() < 2 * n || s->h_seen.size() < n * MRT_NPART) return MRT_OK;  // not started
     double done = 0, total = 0;
     for (size_t k = 0; k < n; k++) {
         total += (double)s->chunk_paths[k];
@@ -1411,7 +1515,7 @@ extern "C" mrt_status mrt_progress(mrt_scene* s, float* pct) {
             // different waves land out of order: report the largest seen so far
             const uint64_t np = s->chunk_paths[k];
             for (uint32_t j = 0; j < MRT_NPART; j++) {
-                uint64_t c = __atomic_load_n(&s->h_prog[k * MRT_NPART + j], __ATOMIC_RELAXED);
+                uint64_t c = __atomic_load_n(&s->h_prog[(s->prog_base + k) * MRT_NPART + j], __ATOMIC_RELAXED);
                 c = std::max(c, s->h_seen[k * MRT_NPART + j]);
                 s->h_seen[k * MRT_NPART + j] = c;
                 done += (double)std::min<uint64_t>(c, np * (j + 1) / MRT_NPART - np * j / MRT_NPART);

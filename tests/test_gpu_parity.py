@@ -482,6 +482,44 @@ def test_lean_fold_equals_fold(gpu, numerics, chunk):
         c.close()
 
 
+@pytest.mark.parametrize("numerics,mode", [("exact", 0), ("fast", 0), ("fast", 1)])
+def test_async_fold_equals_fold(gpu, numerics, mode):
+    """MRT_RF_FOLD_ASYNC (bench.py --fold async): each render's fold on the context's own stream,
+    beside the next render's path kernel, the renders alternating between two radiance buffers and
+    counter slots.  Back-to-back renders into different outputs, then join(): every image equals the
+    blocking render bit for bit, the ray counter is the sum, and a plain render afterwards (both
+    parities' counters reset by their folds) is still exact.  Invalid combinations are refused."""
+    import torch
+    w, h, spp = 96, 80, 64
+    sc, r0 = renderer(gpu, 5, w, h)
+    ref, rays1 = r0.render(gpu.render_desc(w, h, spp, numerics=numerics, mode=mode))
+    d = gpu.render_desc(w, h, spp, numerics=numerics, mode=mode, flags=gpu._lib.RF_FOLD_ASYNC)
+    c = gpu.Renderer(sc, 0)
+    c.prepare(d)
+    px = gpu.local_pixels(d)
+    dev = torch.device("cuda", 0)
+    outs = [torch.zeros((len(px), 4), dtype=torch.float32, device=dev) for _ in range(5)]
+    rays_d = torch.zeros(1, dtype=torch.int64, device=dev)
+    s = torch.cuda.Stream(dev)
+    torch.cuda.synchronize(dev)
+    for o in outs:
+        c.render_device(d, o.data_ptr(), rays_d.data_ptr(), s.cuda_stream)
+    c.join(s.cuda_stream)
+    s.synchronize()
+    assert int(rays_d.item()) == len(outs) * rays1
+    for o in outs:
+        im = np.zeros((w * h, 4), dtype=np.float32)
+        im[px] = o.cpu().numpy()
+        assert np.array_equal(im.reshape(h, w, 4)[..., :3].view(np.uint32), ref[..., :3].view(np.uint32))
+    assert c.progress() == pytest.approx(100.0)
+    img, rays = c.render(gpu.render_desc(w, h, spp, numerics=numerics, mode=mode))
+    assert rays == rays1 and np.array_equal(img[..., :3].view(np.uint32), ref[..., :3].view(np.uint32))
+    for bad in (dict(chunk_samples=16), dict(preview=True)):
+        with pytest.raises(gpu.MrtError, match="FOLD_ASYNC"):
+            c.prepare(gpu.render_desc(w, h, spp, numerics=numerics, mode=mode, flags=gpu._lib.RF_FOLD_ASYNC, **bad))
+    c.close()
+
+
 # Tolerance of the small shipped fixtures (Cornell, bunny, teapot 128x128 at C2's 1024 spp; book2
 # 64x64 at 4096 spp): the north-star per-pixel bar, 1e-3, under both contracts.  The difference
 # between two renders on the same path streams comes only from paths that diverge (a rounding

@@ -82,7 +82,7 @@ def test_render_flags_match_header(mrt):
     """The ctypes mirror's MRT_RF_* bits are the header's (include/mrt.h)."""
     hdr = open(os.path.join(os.path.dirname(__file__), "..", "include", "mrt.h")).read()
     bits = {m.group(1): int(m.group(2), 16) for m in re.finditer(r"#define MRT_RF_(\w+) (0x[0-9a-fA-F]+)u", hdr)}
-    assert set(bits) == {"PATH_DEBUG", "FAST", "PREVIEW", "FOLD_BEHIND", "REF_ORDER"}
+    assert set(bits) == {"PATH_DEBUG", "FAST", "PREVIEW", "FOLD_BEHIND", "FOLD_ASYNC", "REF_ORDER"}
     for name, v in bits.items():
         assert getattr(mrt._lib, "RF_" + name) == v, name
 
