@@ -134,12 +134,12 @@ typedef struct mrt_render_desc {
                                    another context's persistent path kernel instead of after it --
                                    for callers that pipeline renders on several streams; slower
                                    when nothing else runs (same bits either way) */
-#define MRT_RF_FOLD_ASYNC 0x20u /* GPU, one launch per render, no preview: the fold runs on the
-                                   context's own stream, beside the NEXT render's path kernel (two
-                                   radiance buffers used in turn; the path kernel leaves one wave slot
-                                   per SIMD for it) instead of after its own.  The output is complete
-                                   once mrt_render_join has ordered a stream after it (or the device
-                                   is synchronised).  Same bits as the fold in stream order. */
+#define MRT_RF_FOLD_ASYNC 0x20u /* GPU, no preview / debug / lean fold: each launch's fold runs on
+                                   the context's own stream, beside the NEXT launch's (or render's)
+                                   path kernel, instead of after its own (two radiance buffers used in
+                                   turn).  The output is complete once mrt_render_join has ordered a
+                                   stream after it (or the device is synchronised).  Same bits as the
+                                   fold in stream order. */
 #define MRT_RF_REF_ORDER 0x10u  /* CPU backend: the reference's own RNG order -- worker i draws from
                                    one PCG stream seeded by mrt_set_worker_seeds' i-th pair; mode 0 =
                                    draw() over work_queue_seq (tile -> pixel -> sample), mode 1 =

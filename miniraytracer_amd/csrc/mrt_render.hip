@@ -145,10 +145,11 @@ __global__ void __launch_bounds__(256) mrt_fold_kernel(const float* __restrict__
     }
 }
 
-// The fold of an MRT_RF_FOLD_ASYNC render, on the context's own stream beside the next render's
-// path kernel, which leaves it one wave slot per SIMD (and its registers, MRT_WPE_LIN): one
-// 256-thread group per CU, each lane folding pixels grid-strided with FOLD_ASYNC_DEPTH samples in
-// flight -- the same operations in the same order as mrt_fold_kernel (bit-identical).
+// The fold of an MRT_RF_FOLD_ASYNC launch, on the context's own stream beside the next launch's
+// path kernel: one 256-thread group per CU (one wave slot per SIMD while it runs), each lane folding
+// pixels grid-strided with FOLD_ASYNC_DEPTH samples in flight -- the same operations in the same
+// order as mrt_fold_kernel (bit-identical): from +0 or the accumulator, into the accumulator or,
+// for the render's last launch, finished into the output with the counters reset.
 #ifndef MRT_FOLD_ASYNC_GROUPS
 #define MRT_FOLD_ASYNC_GROUPS 1  // 256-thread groups per CU: one wave per SIMD
 #endif
@@ -156,32 +157,41 @@ __global__ void __launch_bounds__(256) mrt_fold_kernel(const float* __restrict__
 #define FOLD_ASYNC_DEPTH 8
 #endif
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
-mrt_fold_async_kernel(const float* __restrict__ rad, uint32_t npix, uint32_t ns, uint32_t mode, float max_lum, FoldEnd fe) {
+mrt_fold_async_kernel(const float* __restrict__ rad, float4* __restrict__ acc, uint32_t npix, uint32_t s0, uint32_t s1, uint32_t mode,
+                      float max_lum, FoldEnd fe) {
     const uint32_t step = gridDim.x * blockDim.x;
     const uint32_t nthr = max(npix, fe.nreset);
     for (uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x; lp < nthr; lp += step) {
         reset_counters(fe, lp);
         if (lp >= npix) continue;
-        f3 c{0.0f, 0.0f, 0.0f};  // one launch per render: from +0
+        f3 c{0.0f, 0.0f, 0.0f};
+        if (s0 != 0) {
+            const float4 a = acc[lp];
+            c = f3{a.x, a.y, a.z};
+        }
         const float* q = rad + (size_t)lp * 3;
         const size_t stride = (size_t)npix * 3;
-        uint32_t s = 0;
-        for (; s + FOLD_ASYNC_DEPTH <= ns; s += FOLD_ASYNC_DEPTH) {
+        uint32_t s = s0;
+        for (; s + FOLD_ASYNC_DEPTH <= s1; s += FOLD_ASYNC_DEPTH) {
             f3 v[FOLD_ASYNC_DEPTH];
 #pragma unroll
             for (int k = 0; k < FOLD_ASYNC_DEPTH; k++) {
-                const float* e = q + (size_t)(s + k) * stride;
+                const float* e = q + (size_t)(s - s0 + k) * stride;
                 v[k] = f3{__builtin_nontemporal_load(e), __builtin_nontemporal_load(e + 1), __builtin_nontemporal_load(e + 2)};
             }
 #pragma unroll
             for (int k = 0; k < FOLD_ASYNC_DEPTH; k++) c = fold_sample(c, v[k], s + k, mode, max_lum);
         }
-        for (; s < ns; s++) {
-            const float* e = q + (size_t)s * stride;
+        for (; s < s1; s++) {
+            const float* e = q + (size_t)(s - s0) * stride;
             c = fold_sample(c, f3{e[0], e[1], e[2]}, s, mode, max_lum);
         }
-        c = final_pixel(c, fe.ns, mode, max_lum);
-        fe.out[lp] = make_float4(c.x, c.y, c.z, 0.0f);
+        if (fe.out) {
+            c = final_pixel(c, fe.ns, mode, max_lum);
+            fe.out[lp] = make_float4(c.x, c.y, c.z, 0.0f);
+        } else {
+            acc[lp] = make_float4(c.x, c.y, c.z, 0.0f);
+        }
     }
 }
 
@@ -396,14 +406,15 @@ struct mrt_scene {
     // never sees its buffers rewritten or freed
     hipEvent_t ev_done = nullptr;
     bool ev_done_pending = false;
-    // MRT_RF_FOLD_ASYNC: renders alternate between two radiance buffers / counter slots (parity);
-    // the fold of parity p runs on fstream and ev_fold[p] marks its end, which the next path kernel
-    // writing parity p's buffers waits for
+    // MRT_RF_FOLD_ASYNC: launches alternate between two radiance buffers (parity lpar), renders
+    // between two sets of counter slots (rpar); the fold of parity p runs on fstream and ev_fold[p]
+    // marks its end, which the next path kernel writing parity p's radiance buffer waits for (folds
+    // run in order on fstream, so it also orders every earlier fold)
     hipStream_t fstream = nullptr;
     hipEvent_t ev_kern = nullptr;
     hipEvent_t ev_fold[2] = {nullptr, nullptr};
     bool fold_pending[2] = {false, false};
-    uint32_t par = 0;
+    uint32_t lpar = 0, rpar = 0;
     float* d_rad2 = nullptr;
     size_t rad2_cap = 0;
     uint32_t n_cu = 0;
@@ -1183,9 +1194,8 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
     size_t paths = (size_t)s->npix * s->chunk;
     if ((st = grow(s, (void**)&s->d_rad, &s->rad_cap, paths * 12))) return st;
     if (d->flags & MRT_RF_FOLD_ASYNC) {
-        if (s->chunk != ns || (d->flags & (MRT_RF_PREVIEW | MRT_RF_PATH_DEBUG | MRT_RF_FOLD_BEHIND)))
-            return mrt_internal_fail(MRT_ERR_INVALID, "MRT_RF_FOLD_ASYNC: one launch per render (chunk_samples 0 or spp), "
-                                                      "no preview, debug or lean fold");
+        if (d->flags & (MRT_RF_PREVIEW | MRT_RF_PATH_DEBUG | MRT_RF_FOLD_BEHIND))
+            return mrt_internal_fail(MRT_ERR_INVALID, "MRT_RF_FOLD_ASYNC: no preview, debug or lean fold");
         if ((st = grow(s, (void**)&s->d_rad2, &s->rad2_cap, paths * 12))) return st;
         if (!s->fstream) HIPCHK(hipStreamCreateWithFlags(&s->fstream, hipStreamNonBlocking));
         if (!s->ev_kern) HIPCHK(hipEventCreateWithFlags(&s->ev_kern, hipEventDisableTiming));
@@ -1223,7 +1233,7 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
     s->lev_rows = std::max<uint32_t>(d->max_bounces, 1);
     if ((st = grow(s, (void**)&s->d_lev, &s->lev_cap, (size_t)s->lev_rows * s->max_threads * 16))) return st;
     uint32_t launches = (ns + s->chunk - 1) / s->chunk;
-    launches = std::max(launches, 2u);  // (slots 0 / 1: the two parities of MRT_RF_FOLD_ASYNC renders)
+    launches *= 2;  // (two sets of slots: consecutive MRT_RF_FOLD_ASYNC renders alternate)
     const size_t cnt_words = (size_t)MRT_CNT_SLOTS * MRT_COUNTER_STRIDE;  // per launch
     {
         void* const before = s->d_counters;
@@ -1290,20 +1300,21 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
     s->n_launch = 0;
     s->last_numerics = (d->flags & MRT_RF_FAST) ? 1u : 0u;
     const bool preview = (d->flags & MRT_RF_PREVIEW) != 0;
-    // MRT_RF_FOLD_ASYNC: this render writes the radiance buffer and counter slot of its parity, whose
-    // last fold (an earlier render's, on fstream) must have ended; any other render waits for both
+    // MRT_RF_FOLD_ASYNC: each launch writes the radiance buffer of its parity, whose last fold (on
+    // fstream) must have ended first; the render uses the counter slots of its parity (the previous
+    // render's folds may still reset theirs).  Any other render waits for every pending fold.
     const bool async = (d->flags & MRT_RF_FOLD_ASYNC) != 0;
-    const uint32_t par = async ? s->par : 0u;
-    if (async) s->par ^= 1u;
-    for (uint32_t p = 0; p < 2; p++)
-        if (s->fold_pending[p] && (!async || p == par)) HIPCHK(hipStreamWaitEvent(q, s->ev_fold[p], 0));
+    const uint32_t rpar = async ? s->rpar : 0u;
+    if (async) s->rpar ^= 1u;
+    if (!async)
+        for (uint32_t p = 0; p < 2; p++)
+            if (s->fold_pending[p]) HIPCHK(hipStreamWaitEvent(q, s->ev_fold[p], 0));
     {
         std::lock_guard<std::mutex> lk(s->prog_mu);
-        s->prog_base = par;
+        s->prog_base = rpar * launches;
     }
-    float* const d_rad = par ? s->d_rad2 : s->d_rad;
-    unsigned long long* const d_cnt = (unsigned long long*)(s->d_counters + (size_t)par * MRT_CNT_SLOTS * MRT_COUNTER_STRIDE);
-    unsigned long long* const h_prog = (unsigned long long*)(s->h_prog + (size_t)par * MRT_NPART);
+    unsigned long long* const d_cnt = (unsigned long long*)(s->d_counters + (size_t)rpar * launches * MRT_CNT_SLOTS * MRT_COUNTER_STRIDE);
+    unsigned long long* const h_prog = (unsigned long long*)(s->h_prog + (size_t)rpar * launches * MRT_NPART);
     uint32_t seq = 0;
     if (preview) {  // a new render: no snapshot yet (sequence 0), in stream order
         std::lock_guard<std::mutex> lk(s->prog_mu);
@@ -1313,6 +1324,12 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
     }
     for (uint32_t s0 = 0; s0 < ns; s0 += s->chunk) {
         uint32_t s1 = std::min(ns, s0 + s->chunk);
+        const uint32_t par = async ? s->lpar : 0u;
+        if (async) {
+            s->lpar ^= 1u;
+            if (s->fold_pending[par]) HIPCHK(hipStreamWaitEvent(q, s->ev_fold[par], 0));
+        }
+        float* const d_rad = par ? s->d_rad2 : s->d_rad;
         PathParams P{};
         P.sc = s->S;
         // the interpreter's tolerance-contract program (rooms and box.h lists as slab tests); the
@@ -1375,12 +1392,14 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
             hipLaunchKernelGGL(PL.retrace, dim3(kRetraceGroups), dim3(64), PL.retrace_lds, q, PR);
             HIPCHK(hipGetLastError());
         }
-        if (async) {  // (one launch: mrt_prepare) the fold beside the next render's path kernel
+        if (async) {  // the fold beside the next launch's path kernel
             HIPCHK(hipEventRecord(s->ev_kern, q));
             HIPCHK(hipStreamWaitEvent(s->fstream, s->ev_kern, 0));
-            FoldEnd fe{(float4*)d_local, ns, d_cnt, h_prog, MRT_CNT_SLOTS, MRT_NPART};
-            hipLaunchKernelGGL(mrt_fold_async_kernel, dim3(s->n_cu * MRT_FOLD_ASYNC_GROUPS), dim3(256), 0, s->fstream, d_rad, s->npix, ns,
-                               d->mode, d->max_luminance, fe);
+            const bool last = s1 == ns;
+            FoldEnd fe{last ? (float4*)d_local : nullptr, ns, last ? d_cnt : nullptr, last ? h_prog : nullptr,
+                       last ? launches * MRT_CNT_SLOTS : 0u, last ? launches * MRT_NPART : 0u};
+            hipLaunchKernelGGL(mrt_fold_async_kernel, dim3(s->n_cu * MRT_FOLD_ASYNC_GROUPS), dim3(256), 0, s->fstream, d_rad, s->d_acc, s->npix,
+                               s0, s1, d->mode, d->max_luminance, fe);
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(s->ev_fold[par], s->fstream));
             s->fold_pending[par] = true;

@@ -482,18 +482,19 @@ def test_lean_fold_equals_fold(gpu, numerics, chunk):
         c.close()
 
 
-@pytest.mark.parametrize("numerics,mode", [("exact", 0), ("fast", 0), ("fast", 1)])
-def test_async_fold_equals_fold(gpu, numerics, mode):
-    """MRT_RF_FOLD_ASYNC (bench.py --fold async): each render's fold on the context's own stream,
-    beside the next render's path kernel, the renders alternating between two radiance buffers and
-    counter slots.  Back-to-back renders into different outputs, then join(): every image equals the
-    blocking render bit for bit, the ray counter is the sum, and a plain render afterwards (both
-    parities' counters reset by their folds) is still exact.  Invalid combinations are refused."""
+@pytest.mark.parametrize("numerics,mode,chunk", [("exact", 0, 0), ("fast", 0, 0), ("fast", 1, 0), ("fast", 0, 24), ("exact", 1, 24)])
+def test_async_fold_equals_fold(gpu, numerics, mode, chunk):
+    """MRT_RF_FOLD_ASYNC (bench.py --fold async): each launch's fold on the context's own stream,
+    beside the next launch's path kernel, the launches alternating between two radiance buffers and
+    the renders between two sets of counter slots (chunk 24 of 64 spp: three launches per render).
+    Back-to-back renders into different outputs, then join(): every image equals the blocking render
+    bit for bit, the ray counter is the sum, and a plain render afterwards (every counter reset by
+    the folds) is still exact.  Invalid combinations are refused."""
     import torch
     w, h, spp = 96, 80, 64
     sc, r0 = renderer(gpu, 5, w, h)
     ref, rays1 = r0.render(gpu.render_desc(w, h, spp, numerics=numerics, mode=mode))
-    d = gpu.render_desc(w, h, spp, numerics=numerics, mode=mode, flags=gpu._lib.RF_FOLD_ASYNC)
+    d = gpu.render_desc(w, h, spp, numerics=numerics, mode=mode, chunk_samples=chunk, flags=gpu._lib.RF_FOLD_ASYNC)
     c = gpu.Renderer(sc, 0)
     c.prepare(d)
     px = gpu.local_pixels(d)
@@ -514,9 +515,9 @@ def test_async_fold_equals_fold(gpu, numerics, mode):
     assert c.progress() == pytest.approx(100.0)
     img, rays = c.render(gpu.render_desc(w, h, spp, numerics=numerics, mode=mode))
     assert rays == rays1 and np.array_equal(img[..., :3].view(np.uint32), ref[..., :3].view(np.uint32))
-    for bad in (dict(chunk_samples=16), dict(preview=True)):
+    for bad in (dict(flags=gpu._lib.RF_FOLD_ASYNC | gpu._lib.RF_PATH_DEBUG), dict(flags=gpu._lib.RF_FOLD_ASYNC, preview=True)):
         with pytest.raises(gpu.MrtError, match="FOLD_ASYNC"):
-            c.prepare(gpu.render_desc(w, h, spp, numerics=numerics, mode=mode, flags=gpu._lib.RF_FOLD_ASYNC, **bad))
+            c.prepare(gpu.render_desc(w, h, spp, numerics=numerics, mode=mode, **bad))
     c.close()
 
 
