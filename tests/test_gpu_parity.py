@@ -513,6 +513,8 @@ def test_async_fold_equals_fold(gpu, numerics, mode, chunk):
         im[px] = o.cpu().numpy()
         assert np.array_equal(im.reshape(h, w, 4)[..., :3].view(np.uint32), ref[..., :3].view(np.uint32))
     assert c.progress() == pytest.approx(100.0)
+    img, rays = c.render(d)  # mrt_render (host output) waits for the fold on the context's stream
+    assert rays == rays1 and np.array_equal(img[..., :3].view(np.uint32), ref[..., :3].view(np.uint32))
     img, rays = c.render(gpu.render_desc(w, h, spp, numerics=numerics, mode=mode))
     assert rays == rays1 and np.array_equal(img[..., :3].view(np.uint32), ref[..., :3].view(np.uint32))
     for bad in (dict(flags=gpu._lib.RF_FOLD_ASYNC | gpu._lib.RF_PATH_DEBUG), dict(flags=gpu._lib.RF_FOLD_ASYNC, preview=True)):
