@@ -156,7 +156,13 @@ __global__ void __launch_bounds__(256) mrt_fold_kernel(const float* __restrict__
 #ifndef FOLD_ASYNC_DEPTH
 #define FOLD_ASYNC_DEPTH 8
 #endif
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
+#ifndef MRT_FOLD_ASYNC_WG
+#define MRT_FOLD_ASYNC_WG 256  // threads per group
+#endif
+#ifndef MRT_FOLD_ASYNC_WPE
+#define MRT_FOLD_ASYNC_WPE 8  // (register cap 64: FOLD_ASYNC_DEPTH 8 takes 46)
+#endif
+__global__ void __launch_bounds__(MRT_FOLD_ASYNC_WG) __attribute__((amdgpu_waves_per_eu(MRT_FOLD_ASYNC_WPE)))
 mrt_fold_async_kernel(const float* __restrict__ rad, float4* __restrict__ acc, uint32_t npix, uint32_t s0, uint32_t s1, uint32_t mode,
                       float max_lum, FoldEnd fe) {
     const uint32_t step = gridDim.x * blockDim.x;
@@ -1398,7 +1404,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
             const bool last = s1 == ns;
             FoldEnd fe{last ? (float4*)d_local : nullptr, ns, last ? d_cnt : nullptr, last ? h_prog : nullptr,
                        last ? launches * MRT_CNT_SLOTS : 0u, last ? launches * MRT_NPART : 0u};
-            hipLaunchKernelGGL(mrt_fold_async_kernel, dim3(s->n_cu * MRT_FOLD_ASYNC_GROUPS), dim3(256), 0, s->fstream, d_rad, s->d_acc, s->npix,
+            hipLaunchKernelGGL(mrt_fold_async_kernel, dim3(s->n_cu * MRT_FOLD_ASYNC_GROUPS), dim3(MRT_FOLD_ASYNC_WG), 0, s->fstream, d_rad, s->d_acc, s->npix,
                                s0, s1, d->mode, d->max_luminance, fe);
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(s->ev_fold[par], s->fstream));
