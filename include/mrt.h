@@ -139,7 +139,8 @@ typedef struct mrt_render_desc {
                                    path kernel, instead of after its own (two radiance buffers used in
                                    turn).  The output is complete once mrt_render_join has ordered a
                                    stream after it (or the device is synchronised).  Same bits as the
-                                   fold in stream order. */
+                                   fold in stream order.  Not for stream capture (the fold's stream is
+                                   the context's own). */
 #define MRT_RF_REF_ORDER 0x10u  /* CPU backend: the reference's own RNG order -- worker i draws from
                                    one PCG stream seeded by mrt_set_worker_seeds' i-th pair; mode 0 =
                                    draw() over work_queue_seq (tile -> pixel -> sample), mode 1 =
