@@ -18,7 +18,7 @@ OBJDIR   = build/obj
 
 LIB_OBJS = $(OBJDIR)/mrt_render.o $(OBJDIR)/mrt_kernels_exact.o $(OBJDIR)/mrt_kernels_fast.o $(OBJDIR)/mrt_kernels_fastz.o \
            $(OBJDIR)/mrt_kernels_pex.o \
-           $(OBJDIR)/mrt_cpu.o $(OBJDIR)/scene_builder.o $(OBJDIR)/mrt_common.o
+           $(OBJDIR)/mrt_cpu.o $(OBJDIR)/scene_builder.o $(OBJDIR)/mrt_common.o $(OBJDIR)/mrt_comm.o
 # the path kernels twice: exact contract (no contraction, IEEE division) and tolerance contract
 # (FMA contraction, reciprocal division, hardware rcp/sqrt/rsq, f32 transcendentals)
 # (-fno-hip-fp32-correctly-rounded-divide-sqrt: f32 division by v_rcp_f32 + multiply instead of

@@ -170,6 +170,7 @@ def cpu_baseline(args):
                 res["sample"] = sample + (f", reference build oracle/_ref/mrt_ref_v4 as shipped with -march=x86-64-v4 (AVX-512; "
                                           f"the v3 build: {res['value_v3']} Mrays/s), {r4['rays']} rays in "
                                           f"{r4['trace_seconds']:.2f} s on {used} threads")
+        res["binary"] = ref_provenance(b if res.get("value_v4") != res["value"] else oracle.ref_binary(name="mrt_ref_v4"))
         res.update(contention_free(args, used, sample))
         return res
     import miniraytracer_amd as m
@@ -181,6 +182,25 @@ def cpu_baseline(args):
     return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": used, "cores_used": used,
             "cores_total": total, "cores_quota": quota, "kind": "port",
             "sample": sample + f", C restatement oracle/liboracle.so, {rays} rays in {dt:.2f} s"}
+
+
+def ref_provenance(path):
+    """Which binary the baseline ran: its sha256 now, and the recipe commit / compiler / sha256 that
+    oracle/ref/build_ref.sh recorded when it built it (oracle/_ref/BUILD_INFO.json; the binaries
+    travel to the GPU box untracked, /root/reference is absent there)."""
+    import hashlib
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    out = {"path": os.path.relpath(path, ROOT), "sha256": h.hexdigest()}
+    try:
+        info = json.load(open(os.path.join(os.path.dirname(path), "BUILD_INFO.json")))
+        out.update({k: info.get(k) for k in ("recipe", "recipe_commit", "recipe_dirty", "compiler", "built_utc")})
+        out["sha256_matches_build"] = info.get("sha256", {}).get(os.path.basename(path)) == out["sha256"]
+    except (OSError, ValueError) as e:
+        out["build_info"] = f"unavailable: {e}"[:120]
+    return out
 
 
 def contention_free(args, threads, sample):

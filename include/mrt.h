@@ -134,13 +134,15 @@ typedef struct mrt_render_desc {
                                    another context's persistent path kernel instead of after it --
                                    for callers that pipeline renders on several streams; slower
                                    when nothing else runs (same bits either way) */
-#define MRT_RF_FOLD_ASYNC 0x20u /* GPU, no preview / debug / lean fold: each launch's fold runs on
+#define MRT_RF_FOLD_ASYNC 0x40u /* GPU, no preview / debug / lean fold: each launch's fold runs on
                                    the context's own stream, beside the NEXT launch's (or render's)
                                    path kernel, instead of after its own (two radiance buffers used in
                                    turn).  The output is complete once mrt_render_join has ordered a
                                    stream after it (or the device is synchronised).  Same bits as the
                                    fold in stream order.  Not for stream capture (the fold's stream is
-                                   the context's own). */
+                                   the context's own).  (ABI 6: was 0x20, the bit of the removed
+                                   MRT_RF_SPLIT; 0x20 and every other unknown bit are now rejected
+                                   with MRT_ERR_INVALID instead of silently changing meaning.) */
 #define MRT_RF_REF_ORDER 0x10u  /* CPU backend: the reference's own RNG order -- worker i draws from
                                    one PCG stream seeded by mrt_set_worker_seeds' i-th pair; mode 0 =
                                    draw() over work_queue_seq (tile -> pixel -> sample), mode 1 =
@@ -148,6 +150,13 @@ typedef struct mrt_render_desc {
                                    work_queue.cpp:133-166).  One thread reproduces the reference's
                                    -threads 1 run bit for bit (its deterministic mode,
                                    cmdline_parser.h:15); world must be 1 */
+#define MRT_RF_ALL (MRT_RF_PATH_DEBUG | MRT_RF_FAST | MRT_RF_PREVIEW | MRT_RF_FOLD_BEHIND | MRT_RF_REF_ORDER | MRT_RF_FOLD_ASYNC)
+
+/* ABI version of this header: bumped whenever a flag's meaning or a struct layout changes (6: the
+ * MRT_RF_FOLD_ASYNC bit moved to 0x40, mrt_kernel_info gained handover_lost, mrt_comm_* added).
+ * A binding checks mrt_abi_version() == MRT_ABI_VERSION before its first call. */
+#define MRT_ABI_VERSION 6u
+uint32_t mrt_abi_version(void);
 
 void mrt_default_render_desc(const mrt_params* p, mrt_render_desc* d);
 
@@ -197,10 +206,12 @@ mrt_status mrt_kernel_ms(mrt_scene* s, float* path_ms, uint32_t* launches);
 typedef struct mrt_kernel_info {
     uint32_t features, kernel_features, lds_bytes, grid, prog_ops, vgprs, wg, tree_nodes, build;
     /* handed_over: paths the fast-arithmetic kernels listed for the exact arithmetic since the
-       scene's upload (rounding-critical light samples) -- reading it waits
-       for the scene's renders; pad: 0 */
+       scene's upload (rounding-critical light samples); handover_lost: listed
+       paths beyond a launch's list capacity (they keep their fast radiance; 0 in every BASELINE
+       config).  Reading them waits for the scene's last render (its fold included).  pad: 0 */
     uint32_t pad;
     uint64_t handed_over;
+    uint64_t handover_lost;
 } mrt_kernel_info;
 mrt_status mrt_scene_kernel_info(const mrt_scene* s, mrt_kernel_info* out);
 
@@ -213,6 +224,41 @@ mrt_status mrt_tonemap_argb(const float* rgb, uint32_t width, uint32_t height, u
  * Pixel order is free (e.g. the local-pixel order of mrt_render_device); enqueued on `stream`. */
 mrt_status mrt_lum_max_device(const float* d_rgb, uint32_t n, float* d_lwmax, void* stream);
 mrt_status mrt_tonemap_device(const float* d_rgb, uint32_t n, const float* d_lwmax, uint32_t* d_argb, void* stream);
+
+/* ---- multi-GPU: the framebuffer gather over RCCL (xGMI) ---------------------------------------
+ * The reference's seam is main.cpp:347-382 (the worker threads over one work_queue) writing
+ * G_linearBackBuffer (main.cpp:58): here each rank renders the work_queue tiles dealt to it
+ * (mrt_render_desc.rank / world) on its own GPU, and ONE RCCL gather of the equal-size padded shards
+ * to the root plus one device scatter assembles the W*H framebuffer on the root's GPU; ray counts
+ * are summed with one all-reduce.  RCCL is loaded at mrt_comm_init_* (librccl.so.1: the copy already
+ * in the process, else the loader's search path, else /opt/rocm/lib; $MRT_RCCL_LIB overrides);
+ * without it those calls fail with MRT_ERR_NO_DEVICE.  Collective calls (mrt_gather_frame,
+ * mrt_render_gather) are made by every rank of the communicator, one host thread (or process) per
+ * rank. */
+typedef struct mrt_comm mrt_comm;
+#define MRT_COMM_ID_BYTES 128
+/* one process per GPU: rank 0 makes the id (ncclGetUniqueId) and hands it to the others out of band */
+mrt_status mrt_comm_unique_id(uint8_t id[MRT_COMM_ID_BYTES]);
+mrt_status mrt_comm_init_rank(int device, uint32_t world, uint32_t rank, const uint8_t id[MRT_COMM_ID_BYTES], mrt_comm** out);
+/* one process driving `world` GPUs (ncclCommInitAll): comms_out[r] is rank r on devices[r] */
+mrt_status mrt_comm_init_all(uint32_t world, const int* devices, mrt_comm** comms_out);
+void mrt_comm_free(mrt_comm* c);
+/* Pixels of the largest rank shard of d's tile deal (the gather's padded shard, in pixels). */
+mrt_status mrt_gather_shard_pixels(const mrt_render_desc* d, uint32_t* n_out);
+/* Collective, enqueued on `stream` (the caller has ordered it after its render, mrt_render_join):
+ * this rank's d_local (mrt_render_device output: n_local float4 in mrt_local_pixels order, d.rank
+ * = the communicator's rank, d.world = its size, no pixel list) goes to the root with one
+ * ncclGather of the padded shards; on the root the shards are scattered into d_frame (W*H float4,
+ * row-major, row 0 = bottom, like G_linearBackBuffer; other ranks pass NULL).  d_rays (device
+ * uint64, may be NULL) is summed over the ranks in place (ncclAllReduce), in the same group. */
+mrt_status mrt_gather_frame(mrt_comm* c, const mrt_render_desc* d, const float* d_local, float* d_frame, uint64_t* d_rays,
+                            void* stream);
+/* The drop-in for one worker thread of main.cpp:347-382 on its own GPU: renders this rank's tiles
+ * (mrt_render_device into the communicator's buffers), gathers the frame to the root over RCCL and,
+ * on the root, copies it to rgb_out (W*H*4 floats, every pixel; other ranks may pass NULL).  The ray
+ * total of all ranks goes to *rays_out on every rank (may be NULL).  Returns when this rank's part is
+ * done. */
+mrt_status mrt_render_gather(mrt_scene* s, mrt_comm* c, const mrt_render_desc* d, float* rgb_out, uint64_t* rays_out);
 
 const char* mrt_strerror(mrt_status s);
 const char* mrt_last_error(void);

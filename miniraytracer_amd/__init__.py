@@ -224,6 +224,67 @@ class Renderer:
             pass
 
 
+def comm_unique_id():
+    """ncclGetUniqueId for mrt_comm_init_rank (rank 0 makes it, the others receive it out of band)."""
+    buf = (C.c_uint8 * _lib.COMM_ID_BYTES)()
+    check(lib().mrt_comm_unique_id(buf), "mrt_comm_unique_id")
+    return bytes(buf)
+
+
+def gather_shard_pixels(desc):
+    """Pixels of the largest rank shard of desc's tile deal (the RCCL gather's padded shard)."""
+    n = C.c_uint32()
+    check(lib().mrt_gather_shard_pixels(C.byref(desc), C.byref(n)), "mrt_gather_shard_pixels")
+    return n.value
+
+
+class Comm:
+    """One rank of an RCCL communicator for the framebuffer gather (include/mrt.h "multi-GPU"):
+    Comm(device, world, rank, uid) per process (mrt_comm_init_rank), or Comm.init_all(devices) for one
+    process driving every GPU (mrt_comm_init_all)."""
+
+    def __init__(self, device=0, world=1, rank=0, uid=None, _handle=None):
+        self.device, self.world, self.rank = device, world, rank
+        self._h = C.c_void_p(_handle)
+        if _handle is None:
+            buf = (C.c_uint8 * _lib.COMM_ID_BYTES).from_buffer_copy(uid if uid is not None else comm_unique_id())
+            check(lib().mrt_comm_init_rank(device, world, rank, buf, C.byref(self._h)), "mrt_comm_init_rank")
+
+    @classmethod
+    def init_all(cls, devices):
+        n = len(devices)
+        devs = (C.c_int * n)(*devices)
+        hs = (C.c_void_p * n)()
+        check(lib().mrt_comm_init_all(n, devs, hs), "mrt_comm_init_all")
+        return [cls(devices[r], n, r, _handle=hs[r]) for r in range(n)]
+
+    def gather_frame(self, desc, d_local_ptr, d_frame_ptr, d_rays_ptr=0, stream_ptr=0):
+        """Collective: this rank's shard (render_device output) to the root's W*H float4 frame, rays
+        all-reduced in place (device pointers, e.g. torch data_ptr()s; enqueued on a HIP stream)."""
+        check(lib().mrt_gather_frame(self._h, C.byref(desc), C.c_void_p(d_local_ptr), C.c_void_p(d_frame_ptr or None),
+                                     C.c_void_p(d_rays_ptr or None), C.c_void_p(stream_ptr)), "mrt_gather_frame")
+
+    def render_gather(self, renderer, desc):
+        """Collective render + RCCL gather: the whole (H, W, 4) image on the root (None elsewhere) and
+        the ray total of all ranks."""
+        img = np.zeros((desc.height, desc.width, 4), dtype=np.float32) if self.rank == 0 else None
+        rays = C.c_uint64()
+        check(lib().mrt_render_gather(renderer._h, self._h, C.byref(desc), img.ctypes.data if img is not None else None,
+                                      C.byref(rays)), "mrt_render_gather")
+        return img, rays.value
+
+    def close(self):
+        if self._h:
+            lib().mrt_comm_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def tonemap_device(d_rgb_ptr, n, d_lwmax_ptr, d_argb_ptr, stream_ptr=0, reduce=True):
     """Device tone map of n float4 pixels (torch data_ptr()s).  reduce=True first max-reduces the
     luminance into *d_lwmax (which the caller zeroed); pass reduce=False after combining L_wmax

@@ -18,9 +18,11 @@ RF_PATH_DEBUG = 0x1
 RF_FAST = 0x2  # tolerance numerics contract (include/mrt.h MRT_RF_FAST)
 RF_PREVIEW = 0x4  # keep a progressive preview for mrt_preview (include/mrt.h MRT_RF_PREVIEW)
 RF_FOLD_BEHIND = 0x8  # mode-0 fold that runs beside another context's path kernel (include/mrt.h)
-RF_FOLD_ASYNC = 0x20  # the fold beside the next render's path kernel, on the context's own stream (include/mrt.h)
+RF_FOLD_ASYNC = 0x40  # the fold beside the next render's path kernel, on the context's own stream (include/mrt.h; ABI 6)
 RF_REF_ORDER = 0x10  # CPU backend: the reference's own RNG order (worker streams, work_queue order)
 DEVICE_CPU = -1  # mrt_scene_upload device of the CPU backend (include/mrt.h MRT_DEVICE_CPU)
+ABI_VERSION = 6  # include/mrt.h MRT_ABI_VERSION: checked against mrt_abi_version() at load
+COMM_ID_BYTES = 128  # include/mrt.h MRT_COMM_ID_BYTES
 
 
 class MrtParams(C.Structure):
@@ -64,7 +66,7 @@ class KernelInfo(C.Structure):
     _fields_ = [("features", C.c_uint32), ("kernel_features", C.c_uint32), ("lds_bytes", C.c_uint32),
                 ("grid", C.c_uint32), ("prog_ops", C.c_uint32), ("vgprs", C.c_uint32), ("wg", C.c_uint32),
                 ("tree_nodes", C.c_uint32), ("build", C.c_uint32), ("pad", C.c_uint32),
-                ("handed_over", C.c_uint64)]
+                ("handed_over", C.c_uint64), ("handover_lost", C.c_uint64)]
 BUILDS = ("exact", "fast", "fastz", "pex")  # MRT_BUILD_*: the kernel build (mrt_path_kernel[_fast|_fastz|_pex])
 
 
@@ -87,6 +89,9 @@ def lib():
         raise MrtError(f"{LIB_PATH} not built: run `make` (or __graft_entry__.build())")
     L = C.CDLL(LIB_PATH)
     st = C.c_int
+    L.mrt_abi_version.restype = C.c_uint32
+    if L.mrt_abi_version() != ABI_VERSION:
+        raise MrtError(f"{LIB_PATH}: ABI {L.mrt_abi_version()}, this binding is ABI {ABI_VERSION}: rebuild (make)")
     L.mrt_default_params.argtypes = [C.POINTER(MrtParams)]
     L.mrt_parse_argv.argtypes = [C.c_int, C.POINTER(C.c_char_p), C.POINTER(MrtParams)]
     L.mrt_parse_argv.restype = st
@@ -139,6 +144,19 @@ def lib():
     L.mrt_strerror.argtypes = [C.c_int]
     L.mrt_strerror.restype = C.c_char_p
     L.mrt_last_error.restype = C.c_char_p
+    L.mrt_comm_unique_id.argtypes = [C.c_void_p]
+    L.mrt_comm_unique_id.restype = st
+    L.mrt_comm_init_rank.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_void_p, C.POINTER(C.c_void_p)]
+    L.mrt_comm_init_rank.restype = st
+    L.mrt_comm_init_all.argtypes = [C.c_uint32, C.c_void_p, C.c_void_p]
+    L.mrt_comm_init_all.restype = st
+    L.mrt_comm_free.argtypes = [C.c_void_p]
+    L.mrt_gather_shard_pixels.argtypes = [C.POINTER(MrtRenderDesc), C.POINTER(C.c_uint32)]
+    L.mrt_gather_shard_pixels.restype = st
+    L.mrt_gather_frame.argtypes = [C.c_void_p, C.POINTER(MrtRenderDesc), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.mrt_gather_frame.restype = st
+    L.mrt_render_gather.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(MrtRenderDesc), C.c_void_p, C.POINTER(C.c_uint64)]
+    L.mrt_render_gather.restype = st
     _lib = L
     return L
 
@@ -157,4 +175,6 @@ EXPORTS = [
     "mrt_render", "mrt_render_device", "mrt_render_join", "mrt_prepare", "mrt_render_debug", "mrt_progress",
     "mrt_tonemap_argb", "mrt_strerror", "mrt_last_error", "mrt_kernel_ms", "mrt_pack_obj",
     "mrt_scene_kernel_info", "mrt_preview", "mrt_lum_max_device", "mrt_tonemap_device", "mrt_worker_seeds", "mrt_set_worker_seeds",
+    "mrt_abi_version", "mrt_comm_unique_id", "mrt_comm_init_rank", "mrt_comm_init_all", "mrt_comm_free",
+    "mrt_gather_shard_pixels", "mrt_gather_frame", "mrt_render_gather",
 ]

@@ -9,6 +9,11 @@
 // on one GPU as on eight); with -backend cpu each rank is a CPU-backend context of -threads workers.  -backend cpu renders on the host instead (the CPU backend: the
 // same hot-path code compiled for the host, exact contract), with -threads worker threads as the
 // reference's -threads (0 = every core).  -numerics exact|fast picks the GPU's arithmetic contract.
+// -gather rccl|host: how a multi-GPU frame is assembled.  rccl (the default when every rank has a
+// GPU of its own): each rank's mrt_render_gather renders its shard into device memory and one RCCL
+// gather over xGMI plus a device scatter assemble the frame on GPU 0 (mrt_comm_init_all: one
+// communicator per GPU in this process); host: each rank's mrt_render copies its own pixels into the
+// shared host framebuffer (the only choice when ranks share a GPU, or with -backend cpu).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -28,8 +33,15 @@ int main(int argc, char** argv) {
     mrt_params p;
     if (mrt_parse_argv(argc, argv, &p) != MRT_OK) return 0;  // -help
     const char* out = nullptr;
-    for (int i = 1; i + 1 < argc; i++)
+    const char* gather = nullptr;
+    for (int i = 1; i + 1 < argc; i++) {
         if (!strcmp(argv[i], "-o")) out = argv[i + 1];
+        if (!strcmp(argv[i], "-gather")) gather = argv[i + 1];
+    }
+    if (gather && strcmp(gather, "rccl") && strcmp(gather, "host")) {
+        fprintf(stderr, "-gather: rccl or host\n");
+        return 1;
+    }
 
     auto t_gen = std::chrono::steady_clock::now();
     mrt_scene_blob* blob = nullptr;
@@ -72,6 +84,18 @@ int main(int argc, char** argv) {
         if ((st = mrt_set_worker_seeds(scenes[0], n, is.data(), iq.data()))) return fail("set_worker_seeds", st);
         descs[0].threads = n;
     }
+    // the RCCL gather needs a GPU per rank (RCCL refuses two ranks on one device)
+    const bool use_rccl = !cpu && world <= ndev && (gather ? !strcmp(gather, "rccl") : world > 1);
+    if (gather && !strcmp(gather, "rccl") && !use_rccl) {
+        fprintf(stderr, "-gather rccl: needs the GPU backend and a GPU per rank (%d ranks, %d GPUs)\n", world, ndev);
+        return 1;
+    }
+    std::vector<mrt_comm*> comms(world, nullptr);
+    if (use_rccl) {
+        std::vector<int> devs(world);
+        for (int r = 0; r < world; r++) devs[r] = r;
+        if ((st = mrt_comm_init_all((uint32_t)world, devs.data(), comms.data()))) return fail("comm_init_all", st);
+    }
     std::vector<float> img((size_t)p.buffer_width * p.buffer_height * 4, 0.0f);
     std::vector<uint64_t> rays(world, 0);
     std::vector<mrt_status> sts(world, MRT_OK);
@@ -79,20 +103,25 @@ int main(int argc, char** argv) {
     auto t0 = std::chrono::steady_clock::now();  // main.cpp:375
     std::vector<std::thread> th;
     for (int r = 0; r < world; r++)
-        th.emplace_back([&, r] { sts[r] = mrt_render(scenes[r], &descs[r], img.data(), &rays[r], nullptr); });
+        th.emplace_back([&, r] {
+            sts[r] = use_rccl ? mrt_render_gather(scenes[r], comms[r], &descs[r], r == 0 ? img.data() : nullptr, &rays[r])
+                              : mrt_render(scenes[r], &descs[r], img.data(), &rays[r], nullptr);
+        });
     for (auto& t : th) t.join();
     double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     for (int r = 0; r < world; r++)
         if (sts[r]) return fail("render", sts[r]);
     uint64_t total = 0;
-    for (uint64_t x : rays) total += x;
+    if (use_rccl) total = rays[0];  // (all-reduced over the ranks)
+    else
+        for (uint64_t x : rays) total += x;
     char where[64];
     if (cpu) {
         mrt_kernel_info ki{};
         mrt_scene_kernel_info(scenes[0], &ki);
         snprintf(where, sizeof where, "CPU, %d x %u threads", world, ki.grid);
     } else if (world <= ndev) {
-        snprintf(where, sizeof where, "%d x MI355X", world);
+        snprintf(where, sizeof where, use_rccl ? "%d x MI355X, RCCL gather" : "%d x MI355X", world);
     } else {
         snprintf(where, sizeof where, "%d ranks on %d x MI355X", world, ndev);
     }
@@ -121,6 +150,7 @@ int main(int argc, char** argv) {
         }
         fclose(f);
     }
+    for (auto* c : comms) mrt_comm_free(c);
     for (auto* s : scenes) mrt_scene_free(s);
     mrt_scene_blob_free(blob);
     return 0;

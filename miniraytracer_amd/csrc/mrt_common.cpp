@@ -35,6 +35,8 @@ std::string mrt_internal_package_dir() {
 
 extern "C" const char* mrt_last_error(void) { return g_last_error.c_str(); }
 
+extern "C" uint32_t mrt_abi_version(void) { return MRT_ABI_VERSION; }
+
 extern "C" const char* mrt_strerror(mrt_status s) {
     switch (s) {
     case MRT_OK: return "ok";
@@ -141,6 +143,8 @@ extern "C" mrt_status mrt_parse_argv(int argc, char** argv, mrt_params* out) {
                "  -mode     \t[0, 1]\t\tAccumulation mode (0 per-pixel mean, 1 progressive average)\n"
                "  -scene    \t[0, 9]\t\tSelect the scene (9 = wt_teapot in the Cornell box)\n"
                "  -seed     \t<value>\t\tPath stream-key seed\n"
+               "  -gather   \t[rccl, host]\tMulti-GPU frame assembly: one RCCL gather to GPU 0 (default\n"
+               "            \t\t\twhen every rank has its own GPU) or per-rank host copies\n"
                "  -o        \t<file>\t\tOutput image (.pfm linear, .ppm tone-mapped)\n"
                "  -delay    \t\t\tAccepted for compatibility (no window)\n");
         if (out) *out = p;
@@ -306,6 +310,10 @@ std::vector<uint32_t> mrt_internal_local_pixels(const mrt_render_desc* d) {
 }
 
 mrt_status mrt_internal_check_pixels(const mrt_render_desc* d) {
+    // unknown flag bits fail instead of meaning something else (0x20 was MRT_RF_SPLIT until ABI 5)
+    if (d->flags & ~MRT_RF_ALL)
+        return mrt_internal_fail(MRT_ERR_INVALID, (d->flags & 0x20u) ? "render desc: flag 0x20 (the removed MRT_RF_SPLIT; MRT_RF_FOLD_ASYNC is 0x40 since ABI 6)"
+                                                                      : "render desc: unknown flag bits");
     if (!d->pixels) return MRT_OK;
     if (d->n_pixels == 0) return mrt_internal_fail(MRT_ERR_INVALID, "render desc: empty pixel list");
     const uint64_t wh = (uint64_t)d->width * d->height;

@@ -23,5 +23,7 @@ std::vector<uint32_t> mrt_internal_local_pixels(const mrt_render_desc* d);
 // The work items of one render call: the rank's tiles in work_queue order, or (d->pixels) one 1x1
 // tile per listed pixel in list order.
 std::vector<mrt_tile> mrt_internal_render_tiles(const mrt_render_desc* d);
-// d->pixels, if set, is non-empty, inside the image and free of repeats
+// d->pixels, if set, is non-empty, inside the image and free of repeats; d->flags has no unknown bits
 mrt_status mrt_internal_check_pixels(const mrt_render_desc* d);
+// the HIP device of a GPU-backend scene (MRT_DEVICE_CPU for the CPU backend)
+int mrt_internal_scene_device(const mrt_scene* s);

@@ -720,8 +720,10 @@ __global__ void __launch_bounds__(64) mrt_retrace_kernel(PathParams P) {
     const LevStore<0> lev{nullptr, 0u, 0u, 0u};
     const DScene& S = P.sc;
     PhaseClock ph{};
-    const uint32_t n = min(__hip_atomic_load(P.rt.n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), P.rt.cap);
+    const uint32_t listed = __hip_atomic_load(P.rt.n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t n = min(listed, P.rt.cap);
     if (blockIdx.x == 0 && lane == 0 && n) atomicAdd(P.rt.total, (unsigned long long)n);
+    if (blockIdx.x == 0 && lane == 0 && listed > n) atomicAdd(P.rt.lost, (unsigned long long)(listed - n));  // (kept fast)
     for (uint32_t i = blockIdx.x * 64u + lane; i < n; i += gridDim.x * 64u) {
         const uint32_t idx = P.rt.idx[i];
         uint32_t lp, sl;

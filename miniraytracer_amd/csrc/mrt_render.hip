@@ -390,7 +390,7 @@ struct mrt_scene {
     uint32_t prev_w = 0, prev_h = 0;
     uint32_t lev_rows = 0;
     uint64_t* d_counter = nullptr;   // 64 B scratch: [0] paths handed to the exact arithmetic since upload, [2] ray total of mrt_render, [4] cancel flag,
-                                     // [1] rounding-critical paths listed (u32), [3] retrace groups done (u32)
+                                     // [1] rounding-critical paths listed (u32), [3] retrace groups done (u32), [5] listed beyond the cap since upload
     uint32_t* d_rt = nullptr;        // rounding-critical paths listed for the retrace kernel (path indices)
     size_t rt_cap = 0;
     uint64_t* d_counters = nullptr;  // one work counter per chunk launch (progress reads them)
@@ -425,6 +425,7 @@ struct mrt_scene {
     size_t rad2_cap = 0;
     uint32_t n_cu = 0;
     uint32_t prog_base = 0;  // launch slot of the current render's counters and progress snapshots
+    uint32_t slot_half = 0;  // launch slots per set (renders use set rpar at rpar * slot_half; mrt_prepare)
     unsigned long long* d_rays = nullptr;
     uint32_t features = 0, variant = 0;
     uint32_t lds_frames = 0, lds_rays = 0, lds_mesh = 0, lds_save = 0;
@@ -1238,8 +1239,17 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
         if ((st = grow(s, (void**)&s->d_path_rays, &s->pr_cap, paths * 4))) return st;
     s->lev_rows = std::max<uint32_t>(d->max_bounces, 1);
     if ((st = grow(s, (void**)&s->d_lev, &s->lev_cap, (size_t)s->lev_rows * s->max_threads * 16))) return st;
-    uint32_t launches = (ns + s->chunk - 1) / s->chunk;
-    launches *= 2;  // (two sets of slots: consecutive MRT_RF_FOLD_ASYNC renders alternate)
+    // Two sets of counter slots / progress snapshots, `slot_half` launches each, at FIXED offsets 0
+    // and slot_half: consecutive MRT_RF_FOLD_ASYNC renders alternate between them, because a render's
+    // last fold still resets its set while the next render's kernels count in the other.  The stride
+    // must not follow each render's own launch count: a render of 1 launch after one of 4 would
+    // otherwise start its set inside the previous render's (whose reset then lands mid-claim).  The
+    // set is grown only after quiesce() (no render pending), and render R+2 -- the next user of R's
+    // set -- waits for R's last fold (its first launch waits for the fold of the same radiance
+    // parity, and folds run in order on the context's stream).
+    const uint32_t need = (ns + s->chunk - 1) / s->chunk;
+    const uint32_t half = std::max(s->slot_half, need);
+    const uint32_t launches = 2 * half;
     const size_t cnt_words = (size_t)MRT_CNT_SLOTS * MRT_COUNTER_STRIDE;  // per launch
     {
         void* const before = s->d_counters;
@@ -1260,6 +1270,7 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
             memset(s->h_prog, 0, (size_t)launches * MRT_NPART * 8);  // later: reset by each render's final kernel
             s->h_prog_cap = launches;
         }
+        s->slot_half = half;  // (both buffers now hold 2 * half launches)
         if (s->h_seen.size() < (size_t)launches * MRT_NPART) s->h_seen.resize((size_t)launches * MRT_NPART, 0);
         if (s->chunk_paths.size() < launches) s->chunk_paths.resize(launches, 0);
         while (s->ev.size() < 2 * (size_t)launches) {
@@ -1317,10 +1328,10 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
             if (s->fold_pending[p]) HIPCHK(hipStreamWaitEvent(q, s->ev_fold[p], 0));
     {
         std::lock_guard<std::mutex> lk(s->prog_mu);
-        s->prog_base = rpar * launches;
+        s->prog_base = rpar * s->slot_half;
     }
-    unsigned long long* const d_cnt = (unsigned long long*)(s->d_counters + (size_t)rpar * launches * MRT_CNT_SLOTS * MRT_COUNTER_STRIDE);
-    unsigned long long* const h_prog = (unsigned long long*)(s->h_prog + (size_t)rpar * launches * MRT_NPART);
+    unsigned long long* const d_cnt = (unsigned long long*)(s->d_counters + (size_t)rpar * s->slot_half * MRT_CNT_SLOTS * MRT_COUNTER_STRIDE);
+    unsigned long long* const h_prog = (unsigned long long*)(s->h_prog + (size_t)rpar * s->slot_half * MRT_NPART);
     uint32_t seq = 0;
     if (preview) {  // a new render: no snapshot yet (sequence 0), in stream order
         std::lock_guard<std::mutex> lk(s->prog_mu);
@@ -1384,7 +1395,8 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         // (whose radiance is the fast kernel's own)
         const bool handover = PL.handover && !(d->flags & MRT_RF_PATH_DEBUG);
         if (handover)
-            P.rt = RetraceList{s->d_rt, (uint32_t*)(s->d_counter + 1), kRtCap, (uint32_t*)(s->d_counter + 3), (unsigned long long*)s->d_counter};
+            P.rt = RetraceList{s->d_rt, (uint32_t*)(s->d_counter + 1), kRtCap, (uint32_t*)(s->d_counter + 3), (unsigned long long*)s->d_counter,
+                               (unsigned long long*)(s->d_counter + 5)};
         HIPCHK(hipEventRecord(s->ev[2 * s->n_launch], q));
         hipLaunchKernelGGL(PL.fn, dim3(PL.grid), dim3(PL.wg), PL.lds_bytes, q, P);
         HIPCHK(hipGetLastError());
@@ -1500,6 +1512,8 @@ extern "C" mrt_status mrt_render(mrt_scene* s, const mrt_render_desc* d, float* 
 
 // the worker threads' join (main.cpp:490-493) as stream order: `stream` waits for the context's
 // last render, including a fold on the context's own stream (MRT_RF_FOLD_ASYNC)
+int mrt_internal_scene_device(const mrt_scene* s) { return s->cpu ? MRT_DEVICE_CPU : s->device; }
+
 extern "C" mrt_status mrt_render_join(mrt_scene* s, void* stream) {
     MRT_GPU_ONLY(s, "mrt_render_join");
     if (!s) return mrt_internal_fail(MRT_ERR_INVALID, "mrt_render_join: null");
@@ -1613,11 +1627,18 @@ extern "C" mrt_status mrt_scene_kernel_info(const mrt_scene* s, mrt_kernel_info*
                                                                      : MRT_BUILD_FAST;
     out->pad = 0;
     out->handed_over = 0;
-    if (s->d_counter) {  // (after the scene's last render: the synchronous copy waits for it)
-        uint64_t n = 0;
-        if (hipMemcpy(&n, s->d_counter, 8, hipMemcpyDeviceToHost) != hipSuccess)
+    out->handover_lost = 0;
+    if (s->d_counter) {
+        // after the scene's last render, its fold included: ev_done is recorded on the render's
+        // stream (or the context's fold stream), which the legacy null stream of a plain hipMemcpy
+        // is not ordered after
+        HIPCHK(hipSetDevice(s->device));
+        if (s->ev_done_pending) HIPCHK(hipEventSynchronize(s->ev_done));
+        uint64_t n[6] = {};
+        if (hipMemcpy(n, s->d_counter, sizeof n, hipMemcpyDeviceToHost) != hipSuccess)
             return mrt_internal_fail(MRT_ERR_HIP, "mrt_scene_kernel_info: counter read");
-        out->handed_over = n;
+        out->handed_over = n[0];
+        out->handover_lost = n[5];
     }
     return MRT_OK;
 }

@@ -223,6 +223,7 @@ struct RetraceList {
     uint32_t cap;
     uint32_t* __restrict__ done;             // retrace groups finished (the last one clears n)
     unsigned long long* __restrict__ total;  // paths listed since the scene's upload (mrt_kernel_info)
+    unsigned long long* __restrict__ lost;   // entries beyond cap since the upload (mrt_kernel_info.handover_lost)
 };
 // where a shading step lists its path when its light sample is rounding-critical: the path's index
 // and the byte offset of the launch's RetraceList in the kernel's argument segment (a compile-time

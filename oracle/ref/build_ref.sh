@@ -58,7 +58,9 @@ build() {  # name extra-flags
     for p in "${pids[@]}"; do wait "$p"; done
     $CXX "$odir"/*.o -lpthread -o "$OUT/$name"
     echo "build_ref: built $OUT/$name"
+    BUILT+=("$name")
 }
+BUILT=()
 
 build mrt_ref
 build mrt_ref_v4 -march=x86-64-v4
@@ -71,3 +73,23 @@ if [ -n "${MRT_REF_VARIANTS:-}" ]; then
     build mrt_ref_glibc -ffp-contract=off
     build mrt_ref_fastc -ffp-contract=fast
 fi
+# provenance of the binaries (they travel to the GPU box untracked, where /root/reference is absent):
+# sha256 of each, the commit of this recipe, the compiler -- bench.py's cpu_baseline reports them
+{
+    echo "{"
+    echo "  \"recipe\": \"oracle/ref/build_ref.sh\","
+    echo "  \"recipe_commit\": \"$(git -C "$HERE" log -1 --format=%H -- build_ref.sh harness.cpp 2>/dev/null || echo unknown)\","
+    echo "  \"recipe_dirty\": $( [ -n "$(git -C "$HERE" status --porcelain -- build_ref.sh harness.cpp 2>/dev/null)" ] && echo true || echo false ),"
+    echo "  \"compiler\": \"$($CXX --version | head -1 | sed 's/\"/\x27/g')\","
+    echo "  \"reference\": \"$REF\","
+    echo "  \"built_utc\": \"$(date -u +%Y-%m-%dT%H:%M:%SZ)\","
+    echo "  \"sha256\": {"
+    n=${#BUILT[@]}; i=0
+    for b in "${BUILT[@]}"; do
+        i=$((i + 1)); sep=","; [ $i -eq $n ] && sep=""
+        echo "    \"$b\": \"$(sha256sum "$OUT/$b" | cut -d' ' -f1)\"$sep"
+    done
+    echo "  }"
+    echo "}"
+} > "$OUT/BUILD_INFO.json"
+echo "build_ref: provenance in $OUT/BUILD_INFO.json"

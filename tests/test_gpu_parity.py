@@ -523,6 +523,91 @@ def test_async_fold_equals_fold(gpu, numerics, mode, chunk):
     c.close()
 
 
+def test_async_fold_renders_of_different_shapes(gpu):
+    """MRT_RF_FOLD_ASYNC renders of different launch counts back to back on one context (spp 64 in
+    chunks of 16 = 4 launches, spp 16 in one launch, alternating): the two counter-slot
+    sets sit at fixed offsets, so a 1-launch render never counts in the slots the previous 4-launch
+    render's last fold resets.  Every output equals the blocking render of its own desc bit for bit
+    and the ray counter is the sum."""
+    import torch
+    w, h = 96, 80
+    sc, r0 = renderer(gpu, 5, w, h)
+    descs = [gpu.render_desc(w, h, 64, numerics="fast", chunk_samples=16, flags=gpu._lib.RF_FOLD_ASYNC),
+             gpu.render_desc(w, h, 16, numerics="fast", chunk_samples=16, flags=gpu._lib.RF_FOLD_ASYNC)]
+    refs = [r0.render(gpu.render_desc(w, h, spp, numerics="fast")) for spp in (64, 16)]
+    c = gpu.Renderer(sc, 0)
+    px = gpu.local_pixels(descs[0])
+    dev = torch.device("cuda", 0)
+    order = [0, 1, 0, 1, 1, 0]
+    outs = [torch.zeros((len(px), 4), dtype=torch.float32, device=dev) for _ in order]
+    rays_d = torch.zeros(1, dtype=torch.int64, device=dev)
+    s = torch.cuda.Stream(dev)
+    torch.cuda.synchronize(dev)
+    for k, o in zip(order, outs):
+        c.render_device(descs[k], o.data_ptr(), rays_d.data_ptr(), s.cuda_stream)
+    c.join(s.cuda_stream)
+    s.synchronize()
+    assert int(rays_d.item()) == sum(refs[k][1] for k in order)
+    for k, o in zip(order, outs):
+        im = np.zeros((w * h, 4), dtype=np.float32)
+        im[px] = o.cpu().numpy()
+        assert np.array_equal(im.reshape(h, w, 4)[..., :3].view(np.uint32), refs[k][0][..., :3].view(np.uint32)), k
+    c.close()
+
+
+def test_rccl_gather_one_rank_through_the_c_abi(gpu):
+    """The north-star gather behind the C-ABI (include/mrt.h mrt_comm_*, mrt_gather_frame,
+    mrt_render_gather): a one-device RCCL communicator (a real ncclGather to self + ncclAllReduce of
+    the ray count + the device scatter), both ways of making it -- mrt_comm_init_rank with a unique id
+    (one process per GPU) and mrt_comm_init_all (one process driving the GPUs).  The frame equals the
+    one-rank mrt_render image bit for bit under both contracts (the exact one = the reference fixture)."""
+    import torch
+    g = golden_stream("stream_5.npz")
+    w, h = g["w"], g["h"]
+    sc, r = renderer(gpu, 5, w, h)
+    d = gpu.render_desc(w, h, g["spp"], depth=g["depth"], mode=g["mode"])
+    assert gpu.gather_shard_pixels(d) == w * h
+    for comm in (gpu.Comm(0, 1, 0, gpu.comm_unique_id()), gpu.Comm.init_all([0])[0]):
+        img, rays = comm.render_gather(r, d)
+        assert rays == g["rays"]
+        assert np.array_equal(img[..., :3].view(np.uint32), g["image"].view(np.uint32))
+        comm.close()
+    # the low-level collective on caller-owned device buffers, after an async-fold render (joined)
+    comm = gpu.Comm.init_all([0])[0]
+    df = gpu.render_desc(w, h, g["spp"], depth=g["depth"], mode=g["mode"], numerics="fast", flags=gpu._lib.RF_FOLD_ASYNC)
+    ref, rays_f = r.render(gpu.render_desc(w, h, g["spp"], depth=g["depth"], mode=g["mode"], numerics="fast"))
+    dev = torch.device("cuda", 0)
+    loc = torch.zeros((w * h, 4), dtype=torch.float32, device=dev)
+    frame = torch.full((h, w, 4), -1.0, dtype=torch.float32, device=dev)
+    rays_d = torch.zeros(1, dtype=torch.int64, device=dev)
+    st = torch.cuda.Stream(dev)
+    torch.cuda.synchronize(dev)
+    r.render_device(df, loc.data_ptr(), rays_d.data_ptr(), st.cuda_stream)
+    r.join(st.cuda_stream)
+    comm.gather_frame(df, loc.data_ptr(), frame.data_ptr(), rays_d.data_ptr(), st.cuda_stream)
+    st.synchronize()
+    assert int(rays_d.item()) == rays_f
+    assert np.array_equal(frame.cpu().numpy()[..., :3].view(np.uint32), ref[..., :3].view(np.uint32))
+    comm.close()
+
+
+def test_cli_rccl_gather_writes_reference_image(gpu, tmp_path):
+    """bin/mrt -gather rccl (the default whenever every rank has a GPU of its own): each rank renders
+    into device memory and the frame is assembled on GPU 0 by one RCCL gather; on one GPU (-gpus 1)
+    the written PFM is the reference's image bit for bit and the ray total its G_rayCounter."""
+    import subprocess
+    from conftest import ROOT
+    g = golden_stream("stream_5.npz")
+    out = tmp_path / "rccl.pfm"
+    r = subprocess.run([os.path.join(ROOT, "bin", "mrt"), "-scene", "5", "-width", str(g["w"]), "-height", str(g["h"]),
+                        "-samples", str(g["spp"]), "-depth", str(g["depth"]), "-mode", str(g["mode"]), "-gpus", "1",
+                        "-gather", "rccl", "-numerics", "exact", "-o", str(out)],
+                       capture_output=True, text=True, timeout=120, check=True)
+    assert "RCCL gather" in r.stdout, r.stdout
+    assert int(r.stdout.split("rays ")[-1].split()[0]) == g["rays"]
+    assert np.array_equal(gpu.read_pfm(str(out)).view(np.uint32), g["image"].view(np.uint32))
+
+
 # Tolerance of the small shipped fixtures (Cornell, bunny, teapot 128x128 at C2's 1024 spp; book2
 # 64x64 at 4096 spp): the north-star per-pixel bar, 1e-3, under both contracts.  The difference
 # between two renders on the same path streams comes only from paths that diverge (a rounding
@@ -715,7 +800,8 @@ def test_c3_whole_image_own_spp_within_tolerance(gpu, numerics):
     _, r = renderer(gpu, 9, w, h)
     img, rays = r.render(gpu.render_desc(w, h, spp, depth=depth, numerics=numerics))
     c = compare(img, rays, p)
-    print(c)
+    print(c, r.kernel_info()["handed_over"])
+    assert r.kernel_info()["handover_lost"] == 0  # every listed path fitted its launch's list
     assert c["rmse"] < 1e-3, c
     assert c["rmse"] < {"exact": 1e-4, "fast": 3e-4}[numerics], c
     assert c["mean_delta"] < 1e-4, c

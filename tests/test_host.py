@@ -32,6 +32,24 @@ def test_library_exports_every_declared_symbol(mrt):
     assert set(mrt._lib.EXPORTS) <= decl
 
 
+def test_abi_version_and_unknown_flags(mrt):
+    """ABI 6: the binding checks mrt_abi_version() at load; MRT_RF_FOLD_ASYNC moved to
+    0x40, and the bit it used to share with the removed MRT_RF_SPLIT (0x20), like every unknown bit,
+    is refused with MRT_ERR_INVALID by every entry point that reads a desc, instead of silently
+    meaning something else.  The RCCL gather's padded shard is the largest rank's pixel count."""
+    assert mrt.lib().mrt_abi_version() == mrt._lib.ABI_VERSION == 6
+    assert mrt._lib.RF_FOLD_ASYNC == 0x40
+    for bad in (0x20, 0x80, 1 << 31):
+        with pytest.raises(mrt.MrtError, match="0x20" if bad == 0x20 else "unknown flag"):
+            mrt.local_pixels(mrt.render_desc(64, 48, 4, flags=bad))
+    with pytest.raises(mrt.MrtError, match="0x20"):
+        mrt.Renderer(mrt.select_scene(5, 1.0), "cpu").render(mrt.render_desc(16, 16, 1, flags=0x20))
+    for world in (1, 3, 8):
+        counts = [len(mrt.local_pixels(mrt.render_desc(200, 100, 4, tile_size=16, rank=r, world=world))) for r in range(world)]
+        assert sum(counts) == 200 * 100
+        assert mrt.gather_shard_pixels(mrt.render_desc(200, 100, 4, tile_size=16, world=world)) == max(counts)
+
+
 def test_oracle_is_not_linked_into_the_product(mrt):
     # the product .so never references the oracle (test infrastructure only)
     data = open(mrt._lib.LIB_PATH, "rb").read()
