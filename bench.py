@@ -78,6 +78,14 @@ def parse():
     ap.add_argument("--emulate-gather", action="store_true",
                     help="with --emulate-world: also run rank 0's framebuffer scatter of all N shards each "
                          "step (the gather's device-side work; the xGMI transfer itself is not emulated)")
+    ap.add_argument("--gather", choices=["capi", "torch"], default="capi",
+                    help="N > 1: how the tile shards reach rank 0 -- capi (default): the C-ABI's RCCL gather "
+                         "(mrt_gather_frame on a communicator from mrt_comm_init_rank; one ncclGather of the padded "
+                         "shards + the device scatter, include/mrt.h), torch: miniraytracer_amd.dist.TileGather "
+                         "(dist.gather + index_copy_)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="test hook: take the multi-rank path (process group, gather to rank 0 every step) even at "
+                         "one rank -- on one GPU the C-ABI's RCCL gather then runs to itself")
     ap.add_argument("--chunk-samples", type=int, default=0,
                     help="samples per path-kernel launch (0: the library's choice)")
     ap.add_argument("--fold", choices=["auto", "lean", "full", "async"], default="auto",
@@ -363,7 +371,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if os.environ.get("MRT_SAME_GPU"):  # rehearsal hook: every rank on GPU 0 (one-GPU box)
         local = 0
-    if world > 1:
+    multi = world > 1 or args.force_dist  # the multi-rank path (process group, per-step gather)
+    if multi:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:
+            import socket
+            sk = socket.socket()
+            sk.bind(("127.0.0.1", 0))
+            os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+            sk.close()
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         torch.cuda.set_device(local)
         backend = os.environ.get("MRT_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI; gloo: rehearsal hook
         if backend == "nccl":
@@ -404,8 +422,19 @@ def main():
     px = m.local_pixels(desc)
     n_local = len(px)
     n_rows = n_local
-    tg = eg = None
-    if world > 1:
+    tg = eg = comm = frame = None
+    if multi and args.gather == "capi" and os.environ.get("MRT_SAME_GPU"):
+        args.gather = "torch"  # RCCL refuses two ranks on one device: the rehearsal gathers over torch.distributed
+    if multi and args.gather == "capi":
+        # the C-ABI's RCCL gather (include/mrt.h mrt_comm_*): rank 0's communicator id to every rank
+        # over torch.distributed, one communicator per rank on its GPU; the shards are gathered to
+        # rank 0 and scattered into `frame` by mrt_gather_frame on ONE stream (gstream below), so the
+        # communicator's collectives and buffers are used in issue order
+        obj = [m.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        comm = m.Comm(local, world, rank, obj[0])
+        frame = torch.zeros((args.width * args.height, 4), dtype=torch.float32, device=dev) if rank == 0 else None
+    elif multi:
         from miniraytracer_amd.dist import TileGather
         tg = TileGather(args.width, args.height, args.samples, args.depth, world, rank, dev, tile_size=args.tile_size)
         assert tg.n_local == n_local
@@ -414,16 +443,16 @@ def main():
         from miniraytracer_amd.dist import TileGather
         eg = TileGather(args.width, args.height, args.samples, args.depth, d_world, 0, dev, tile_size=args.tile_size)
         n_rows = eg.n_max
-    # output buffers: one per context, two per context when a gather reads them (world > 1) so a
+    # output buffers: one per context, two per context when a gather reads them (multi) so a
     # render never waits for the previous gather of its own buffer (one context, C2 on 1-2 ranks)
-    nbuf = npipe * (2 if world > 1 else 1)
+    nbuf = npipe * (2 if multi else 1)
     outs = [torch.zeros((n_rows, 4), dtype=torch.float32, device=dev) for _ in range(nbuf)]
     rays = torch.zeros(1, dtype=torch.int64, device=dev)  # every context adds its rays here (device atomics)
     stream = torch.cuda.current_stream(dev)
     streams = [stream] + [torch.cuda.Stream(dev) for _ in range(npipe - 1)]
     # async fold: the gather waits for a render's fold on a stream of its own, so the next render's
     # path kernel is not ordered after it
-    gstream = torch.cuda.Stream(dev) if (async_fold and world > 1) else None
+    gstream = torch.cuda.Stream(dev) if (multi and (async_fold or comm is not None)) else None
 
     pending = [None]
     sent = [None] * nbuf  # the gather that last read output buffer b
@@ -440,7 +469,18 @@ def main():
             if sent[b] is not None:  # the gather of this buffer's previous render has read it
                 sent[b].wait()
             ctx[0][j].render_device(d, outs[b].data_ptr(), rays.data_ptr(), streams[j].cuda_stream)
-            if world > 1:
+            if comm is not None:
+                # the one RCCL collective of the data path, on the gather stream after the render
+                # (after its fold on the context's own stream under the async fold)
+                if async_fold:
+                    ctx[0][j].join(gstream.cuda_stream)
+                else:
+                    gstream.wait_stream(streams[j])
+                comm.gather_frame(d, outs[b].data_ptr(), frame.data_ptr() if frame is not None else 0, 0, gstream.cuda_stream)
+                ev = torch.cuda.Event()
+                ev.record(gstream)
+                sent[b] = ev  # the next render into outs[b] waits for it
+            elif multi:
                 # the one RCCL collective of the data path (tile shards -> rank 0), overlapped with
                 # the next render: finish the previous step's gather, then start this one's
                 if pending[0] is not None:
@@ -491,7 +531,7 @@ def main():
                 ctx[0][0].render_device(d, outs[0].data_ptr(), rays.data_ptr(), streams[0].cuda_stream)
             torch.cuda.synchronize(dev)
         rays.zero_()
-        if world > 1:
+        if multi:
             dist.barrier()
         torch.cuda.synchronize(dev)
         note("timed steps")
@@ -505,7 +545,7 @@ def main():
                 evs.append(e)
         drain()
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if multi:
             dist.barrier()
         t1 = time.perf_counter()
         # the path kernel's time inside the timed region: HIP events recorded around each launch on
@@ -521,7 +561,7 @@ def main():
                              "mean_ms": round(float(iv.mean()), 4), "intervals": len(iv)}
         elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
         total_rays = rays.clone()
-        if world > 1:
+        if multi:
             dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
             dist.all_reduce(total_rays, op=dist.ReduceOp.SUM)
         return float(elapsed.item()), int(total_rays.item()), int(rays.item()) // max(args.steps, 1)
@@ -531,7 +571,9 @@ def main():
 
     def last_image():
         """The assembled framebuffer of the last timed step (rank 0; None elsewhere)."""
-        if world > 1:
+        if comm is not None:
+            return frame.view(args.height, args.width, 4).cpu().numpy() if rank == 0 else None
+        if multi:
             return tg.full.view(args.height, args.width, 4).cpu().numpy() if rank == 0 else None
         full = np.zeros((args.width * args.height, 4), dtype=np.float32)
         full[px] = outs[(it[0] - 1) % nbuf][:n_local].cpu().numpy()
@@ -622,7 +664,7 @@ def main():
                                    f"{desc.sqrt_samples ** 2} spp, depth {args.depth}, draw() accumulation",
                        "scene": args.scene, "width": args.width, "height": args.height,
                        "spp": desc.sqrt_samples ** 2, "depth": args.depth, "parallelism": f"tiles{world}",
-                       "tile_size": args.tile_size, "pipeline": npipe, "fold": "lean" if lean_fold else ("async" if async_fold else "full"), "numerics": args.numerics,
+                       "tile_size": args.tile_size, "pipeline": npipe, **({"gather": args.gather} if multi else {}), "fold": "lean" if lean_fold else ("async" if async_fold else "full"), "numerics": args.numerics,
                        **({"emulated_share": f"rank {d_rank} of {d_world}" + (", + rank 0's scatter" if eg is not None else "")}
                           if d_world != world else {}),
                        "rays_per_step": nrays // args.steps},
@@ -642,7 +684,10 @@ def main():
             except Exception as e:  # the baseline never blocks the GPU number
                 res["cpu_baseline"] = {"error": str(e)[:200]}
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if comm is not None:
+        torch.cuda.synchronize(dev)
+        comm.close()
+    if multi:
         dist.destroy_process_group()
 
 

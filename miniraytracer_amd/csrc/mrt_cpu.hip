@@ -142,7 +142,7 @@ struct Stacks {
     std::vector<v4f> lev;
     Stacks(const SceneTables& T, uint32_t rows)
         : frames((size_t)std::max(T.max_frames, 1) * 128), mesh((size_t)std::max(T.max_mesh, 1) * 64),
-          rays((size_t)std::max(T.max_rays, 1) * 11 * 64), save(15 * 64), lev(rows) {}
+          rays((size_t)std::max(T.max_rays, 1) * 11 * 64), save(9 * 64), lev(rows) {}
 };
 
 // trace() of one path (main.cpp:66-118) to its end: the same segments the GPU runs one loop

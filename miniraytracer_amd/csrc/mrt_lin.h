@@ -309,6 +309,20 @@ MRT_DFN bool lin_box(const OP& o, const Ray& r, float tmin, float tmax) {
     return aabb_hit(b, b + 3, r, tmin, tmax);
 }
 
+// The instance-frame ray of instance op `io` for the query ray r -- the walk's own operations at
+// LOP_INST and at the one-step box instance (translate::hit / rotate_y::hit, scene_object.cpp:9-18,
+// 70-98) -- recomputed after the walk for the record of a hit inside the instance, instead of
+// parking the 6 words of the instance ray in LDS at the hit (round 6: the LDS freed holds more
+// treelet nodes).  Only its origin and direction are read; from the same query ray and op they are
+// the walk's bits.
+template <bool U, typename OP>
+MRT_DFN Ray inst_ray(const OP& io, const Ray& r) {
+    const uint32_t kind = LOP_KIND(io);
+    if (kind == MRT_K_TRROTY) return rotate_ray<U>(moved_ray<U>(r, sub(r.o, f3{io.f[8], io.f[9], io.f[10]})), io.f[6], io.f[7]);
+    if (kind == MRT_K_ROTY) return rotate_ray<U>(r, io.f[6], io.f[7]);
+    return moved_ray<U>(r, sub(r.o, f3{io.f[0], io.f[1], io.f[2]}));
+}
+
 // record frames of instance hits, back to the world (scene_object.cpp:13-16, 85-93)
 template <typename OP>
 MRT_DFN void lin_untransform(const OP& io, HitRec& rec) {
@@ -324,8 +338,8 @@ MRT_DFN void lin_untransform(const OP& io, HitRec& rec) {
 }
 
 // r: the query ray; on return it holds the same values (reloaded from LDS when instances exist).
-// LDS per lane (L.save): [0..8] the query ray, [9..14] origin/direction of the instance ray of
-// the closest hit (written at the instance's END op when that hit lies inside it).
+// LDS per lane (L.save): [0..8] the query ray (the instance ray of the closest hit is recomputed
+// after the walk, inst_ray).
 // The interpreter's slab-test ops (LOP_ROOM of the tolerance contract's program rewrite, an
 // object_list flagged MRT_F_BOX6) are compiled into the kernels of scenes without bvh_node
 // subtrees, volumes, textures or motion only: in the catch-all interpreter kernel their two cases
@@ -426,11 +440,6 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
             hnode = h ? prog[pc + 2 + c].node : hnode;
             hinst = h ? pc : hinst;
             hdone = h ? false : hdone;
-            if (h) {  // the instance-frame ray of the hit, for the record (as at LOP_INST_END)
-                float* b = L.save + L.lane + 9 * 64;
-                b[0] = ci.o.x; b[64] = ci.o.y; b[128] = ci.o.z;
-                b[192] = ci.d.x; b[256] = ci.d.y; b[320] = ci.d.z;
-            }
             pc = o.skip;  // its LOP_INST_END
         } else if (MRT_FAST_BOX && kLinSlabOps<F> && op == LOP_LIST && (LOP_FLAGS(o) & MRT_F_BOX6)) {  // uniform
             // box.h's six rects as one slab test (its own box test implied), the list skipped
@@ -524,11 +533,6 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
             if (kind == MRT_K_TRROTY || kind == MRT_K_ROTY) cur = rotate_ray<kFastUnit<F>>(cur, o.f[6], o.f[7]);
             else cur = moved_ray<kFastUnit<F>>(r0, sub(r0.o, f3{o.f[0], o.f[1], o.f[2]}));
         } else if (INST && op == LOP_INST_END) {
-            if (hinst == inst) {  // keep the instance-frame ray of the hit for the record
-                float* b = L.save + L.lane + 9 * 64;
-                b[0] = cur.o.x; b[64] = cur.o.y; b[128] = cur.o.z;
-                b[192] = cur.d.x; b[256] = cur.d.y; b[320] = cur.d.z;
-            }
             cur = lin_load_ray(L);
             inst = MRT_NONE;
             lvl--;
@@ -564,10 +568,10 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
         const LinOp& io = S.prog[hinst];
 #endif
         if (!hdone) {
-            const float* b = L.save + L.lane + 9 * 64;
+            const Ray ci = inst_ray<kFastUnit<F>>(io, r);
             Ray ir = r;
-            ir.o = f3{b[0], b[64], b[128]};
-            ir.d = f3{b[192], b[256], b[320]};
+            ir.o = ci.o;
+            ir.d = ci.d;
             lin_prim_rec<F>(S, hnode, ir, closest, rec);
         }
         lin_untransform(io, rec);

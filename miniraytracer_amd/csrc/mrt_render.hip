@@ -1002,7 +1002,7 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     s->lds_rays = lin_kernel ? 0 : (uint32_t)T.max_rays;
     s->lds_mesh = (uint32_t)T.max_mesh;
     // the query ray parked in LDS: instances (scene_hit_lin)
-    s->lds_save = (lin_kernel && (kVariants[s->variant] & FT_INST)) ? 15u : 0u;
+    s->lds_save = (lin_kernel && (kVariants[s->variant] & FT_INST)) ? 9u : 0u;  // (round 6: 15 -> 9, mrt_lin.h inst_ray)
     // resumable mesh walk: deeper pod_bvh trees keep the wave walking longer
     s->walk_min = T.wide.size() >= 2048 ? 40u : 32u;  // inner nodes: bunny 2937, teapot ~1045
     bool walk_min_env = false;

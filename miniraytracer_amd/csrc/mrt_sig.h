@@ -345,11 +345,6 @@ struct SigWalk {
                     if constexpr (kind == MRT_K_TRROTY || kind == MRT_K_ROTY) w.cur = rotate_ray(w.cur, o.f[6], o.f[7]);
                     else w.cur = moved_ray(r0, sub(r0.o, f3{o.f[0], o.f[1], o.f[2]}));
                     run<PC + 1, skip>(S, prog, tmin, w, in, rec, L);
-                    if (w.hinst == PC) {  // keep the instance-frame ray of the hit for the record
-                        float* b = L.save + L.lane + 9 * 64;
-                        b[0] = w.cur.o.x; b[64] = w.cur.o.y; b[128] = w.cur.o.z;
-                        b[192] = w.cur.d.x; b[256] = w.cur.d.y; b[320] = w.cur.d.z;
-                    }
                 }
                 w.cur = lin_load_ray(L);
                 run<skip + 1, END>(S, prog, tmin, w, on, rec, L);
@@ -706,13 +701,18 @@ MRT_DFN bool scene_hit_sig(const DScene& S, Ray& r, float tmin, HitRec& rec, con
     SigWalk<F, SIG>::template run<0, kSigs[SIG].n - 1>(S, prog, tmin, w, true, rec, L);
     if (INST) r = lin_load_ray(L);
     if (w.hnode == MRT_NONE) return false;
+    // the instance-frame ray of a hit inside an instance: recomputed from the query ray (inst_ray,
+    // the walk's own operations; no longer parked in LDS at the hit)
+    auto inst_ray_of = [&](Ray ir) -> Ray {
+        constexpr uint32_t IPC = SigWalk<F, SIG>::only_inst();
+        const Ray ci = IPC != MRT_NONE ? inst_ray<MRT_FAST_UNIT>(prog[IPC == MRT_NONE ? 0 : IPC], r) : inst_ray<MRT_FAST_UNIT>(S.prog[w.hinst], r);
+        ir.o = ci.o;
+        ir.d = ci.d;
+        return ir;
+    };
     if constexpr (SigWalk<F, SIG>::kDerive) {
         Ray ir = r;
-        if (INST && any_lane(w.hinst != MRT_NONE && !w.hdone)) {  // instance-frame ray of the hit (LDS)
-            const float* b = L.save + L.lane + 9 * 64;
-            ir.o = f3{b[0], b[64], b[128]};
-            ir.d = f3{b[192], b[256], b[320]};
-        }
+        if (INST && any_lane(w.hinst != MRT_NONE && !w.hdone) && w.hinst != MRT_NONE) ir = inst_ray_of(ir);
         if (!w.hdone) SigWalk<F, SIG>::template derive<0>(prog, w, r, ir, rec);
         if (INST && w.hinst != MRT_NONE) {
             constexpr uint32_t IPC = SigWalk<F, SIG>::only_inst();
@@ -722,13 +722,7 @@ MRT_DFN bool scene_hit_sig(const DScene& S, Ray& r, float tmin, HitRec& rec, con
     } else {
         const uint32_t node = w.hnode;
         if (INST && w.hinst != MRT_NONE) {
-            if (!w.hdone) {
-                const float* b = L.save + L.lane + 9 * 64;
-                Ray ir = r;
-                ir.o = f3{b[0], b[64], b[128]};
-                ir.d = f3{b[192], b[256], b[320]};
-                lin_prim_rec<F>(S, node, ir, w.closest, rec);
-            }
+            if (!w.hdone) lin_prim_rec<F>(S, node, inst_ray_of(r), w.closest, rec);
             constexpr uint32_t IPC = SigWalk<F, SIG>::only_inst();
             if constexpr (IPC != MRT_NONE) lin_untransform(prog[IPC], rec);  // known instance: scalar loads
             else lin_untransform(S.prog[w.hinst], rec);

@@ -591,6 +591,25 @@ def test_rccl_gather_one_rank_through_the_c_abi(gpu):
     comm.close()
 
 
+def test_bench_multi_rank_path_over_the_c_abi_gather(gpu):
+    """bench.py's multi-rank step (process group, a render per step into its shard, the C-ABI RCCL
+    gather to rank 0 on the gather stream, the next render into a buffer waiting for the gather that
+    read it) taken at one rank (--force-dist: the gather runs to itself over RCCL): the assembled frame
+    of the last timed step equals a one-context render bit for bit (--verify), both folds."""
+    import json
+    import subprocess
+    import sys
+    from conftest import ROOT
+    for fold in ("async", "full"):
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--force-dist", "--fold", fold, "--steps", "4", "--warmup", "1",
+                            "--samples", "64", "--verify", "--no-cpu-baseline", "--no-compare-numerics", "--no-other-walk", "--no-parity"],
+                           capture_output=True, text=True, timeout=240, cwd=ROOT)
+        assert r.returncode == 0, r.stderr[-2000:]
+        j = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+        assert j["config"]["gather"] == "capi" and j["config"]["fold"] == fold
+        assert j["verify_bit_exact"] is True, j
+
+
 def test_cli_rccl_gather_writes_reference_image(gpu, tmp_path):
     """bin/mrt -gather rccl (the default whenever every rank has a GPU of its own): each rank renders
     into device memory and the frame is assembled on GPU 0 by one RCCL gather; on one GPU (-gpus 1)

@@ -9,7 +9,7 @@ set -e
 cd "$(dirname "$0")/.."
 tag=$1; shift
 flags="$*"
-make -s build/obj/scene_builder.o build/obj/mrt_common.o build/obj/mrt_render.o build/obj/mrt_kernels_exact.o build/obj/mrt_cpu.o
+make -s build/obj/scene_builder.o build/obj/mrt_common.o build/obj/mrt_render.o build/obj/mrt_kernels_exact.o build/obj/mrt_cpu.o build/obj/mrt_comm.o
 mkdir -p exp/obj_$tag
 BASE="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-fast-math -fno-slp-vectorize -w -mllvm -disable-promote-alloca-to-vector -mllvm -structurizecfg-skip-uniform-regions -DMRT_EXPERIMENTS"
 /opt/rocm/bin/hipcc $BASE -DMRT_TABLE_FAST=1 $flags -c miniraytracer_amd/csrc/mrt_kernels.hip -o exp/obj_$tag/mrt_kernels_fast.o
@@ -44,5 +44,5 @@ if [ -n "${PEX_FLAGS:-}" ]; then  # ... or built with extra flags
   PX=exp/obj_$tag/mrt_kernels_pex.o
 fi
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $RO $EX $PX exp/obj_$tag/mrt_kernels_fast.o $FZ \
-    build/obj/mrt_cpu.o build/obj/scene_builder.o build/obj/mrt_common.o -ldl -o exp/libmrt_$tag.so
+    build/obj/mrt_cpu.o build/obj/scene_builder.o build/obj/mrt_common.o build/obj/mrt_comm.o -ldl -o exp/libmrt_$tag.so
 echo "built exp/libmrt_$tag.so"

@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 CFGS=${CFGS:-1,0 2,0 4,0 8,0 8,7}
 for cfg in $CFGS; do
   IFS=, read n r <<< "$cfg"
-  timeout -k 10 300 python bench.py --no-cpu-baseline --no-compare-numerics --no-other-walk --no-parity --steps ${STEPS:-40} --warmup 4 \
+  timeout -k 10 ${RUN_TIMEOUT:-300} python bench.py --no-cpu-baseline --no-compare-numerics --no-other-walk --no-parity --steps ${STEPS:-40} --warmup ${WARMUP:-4} \
       --emulate-world $n --emulate-rank $r --emulate-gather --step-times ${SCALE_ARGS:-} > gpurun_out/scale_${n}_$r.log 2>&1 || exit 3
   python - gpurun_out/scale_${n}_$r.log $n $r <<'PY'
 import json, sys

@@ -17,7 +17,8 @@ def main():
     par = d.get("parity") or {}
     extra = f", rmse {par['rmse']:.2e}, rays x{par['ray_ratio']:.6f}" if "rmse" in par else ""
     print(f"{label:>20}: {d['ms_per_step']:.3f} ms/step, kernel {rf.get('kernel_ms')} ms, "
-          f"{d['value']:.0f} {d['unit']}, frac {rf.get('frac')}{extra}")
+          f"{d['value']:.0f} {d['unit']}, frac {rf.get('frac')}{extra} "
+          f"[vgprs {rf.get('vgprs')}, lds {rf.get('lds_bytes')}, treelet {rf.get('tree_nodes')}, wg {rf.get('wg')}]")
     return 0
 
 
