@@ -158,7 +158,17 @@ MRT_HD double mrt_atan_d(double x) { /* |x| <= 1 */
     return 4.0 * fma(t * z, p, t);
 }
 MRT_HD double mrt_atan2_d(double y, double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    /* the two constants made by the instructions themselves where used, not hoisted into register
+       pairs held across the caller's loops (book2's path kernel spilled them to scratch) */
+    int pl, ph, ql, qh;
+    __asm__ volatile("v_mov_b32 %0, 0x54442d18\n\tv_mov_b32 %1, 0x400921fb\n\tv_mov_b32 %2, 0x54442d18\n\tv_mov_b32 %3, 0x3ff921fb"
+                     : "=v"(pl), "=v"(ph), "=v"(ql), "=v"(qh));
+    const double pi = __builtin_bit_cast(double, ((unsigned long long)(unsigned)ph << 32) | (unsigned)pl);
+    const double pio2 = __builtin_bit_cast(double, ((unsigned long long)(unsigned)qh << 32) | (unsigned)ql);
+#else
     const double pi = 3.14159265358979311600e+00, pio2 = 1.57079632679489655800e+00;
+#endif
     if (x != x || y != y) return x + y;
     if (y == 0.0) {
         if (x > 0.0 || (x == 0.0 && !signbit(x))) return y;   /* +-0 */

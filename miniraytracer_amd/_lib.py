@@ -71,6 +71,7 @@ BUILDS = ("exact", "fast", "fastz", "pex")  # MRT_BUILD_*: the kernel build (mrt
 
 
 FT_LIN = 1 << 11  # kernel feature bit: linear hit program (mrt_lin.h)
+FT_VSUB = 1 << 14  # kernel feature bit: volumes bounded by sub-programs (mrt_lin.h lin_sub_t; Cornell smoke)
 
 
 class MrtError(RuntimeError):

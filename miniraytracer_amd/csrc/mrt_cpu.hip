@@ -78,7 +78,7 @@ struct mrt_cpu_scene {
 // the two hot-path instantiations of the host backend: any linear hit program through the
 // interpreter, any other graph through the generic machine (both bit-identical to the GPU's
 // shape-specialised walks, tests/test_gpu_parity.py)
-static constexpr uint32_t F_LIN = FT_LIN | FT_ALL;
+static constexpr uint32_t F_LIN = FT_LIN | FT_ALL | FT_VSUB;
 static constexpr uint32_t F_GEN = FT_ALL;
 
 mrt_status mrt_cpu_scene_create(const mrt_scene_view* v, mrt_cpu_scene** out) {

@@ -107,6 +107,9 @@ static constexpr uint32_t kVariants[] = {FT_LIN | FT_INST | FT_BIASED | MRT_SIG_
                                          // sky-lit scenes 0-4: no light sampling compiled in (its registers
                                          // pushed this 128-VGPR kernel into a spill inside the bounce loop)
                                          FT_LIN | FT_BVHW | FT_TEX | FT_METAL | FT_MOVING | FT_SKY | FT_UV,
+                                         // Cornell smoke (scene 6): box-bounded volumes as sub-programs,
+                                         // instances, light sampling
+                                         FT_LIN | FT_INST | FT_VOLUME | FT_VSUB | FT_ISO | FT_BIASED,
 #ifndef MRT_NO_B2  // (A/B hook: book2 on the catch-all interpreter kernel)
                                          // lit bvh_node scenes with volumes, textures, motion (book2, C5): no mesh
                                          // walk, no sky, no sphere in the biased list, no generic bvh walk

@@ -359,6 +359,92 @@ MRT_DFN void lin_untransform(const OP& io, HitRec& rec) {
 #endif
 template <uint32_t F>
 static constexpr bool kLinSlabOps = MRT_FAST && (F & FT_LIN) != 0 && (F & (FT_BVHW | FT_VOLUME | FT_TEX | FT_MOVING)) == 0;
+// Round 6: the records of bvh_node leaf hits and constant_volume hits made after the walk, like a
+// primitive op's, from what the walk keeps of the hit (the leaf primitive and the range it passed
+// with; the volume op), instead of inside it: the 10-word record is then not live across the rest
+// of the walk (book2's bvh_node walks ran with the ground's record held while the spheres' tree was
+// walked).  The same tests with the same rays and ranges: the same bits.
+#ifndef MRT_LIN_DEFER
+#define MRT_LIN_DEFER 1
+#endif
+enum : uint32_t { HK_PRIM = 0, HK_DONE = 1, HK_VOL = 2, HK_BVHW = 3 };  // how the record is made after the walk
+
+// t of the closest hit in [tmin, tmax] of a volume's boundary sub-program [b, e) (MRT_F_VSUB: box.h
+// lists and one level of instances, emitted after the volume op) for the volume-frame ray r0 --
+// object_list::hit / translate::hit / rotate_y::hit as the main walk runs them (scene_object.h:79-103,
+// scene_object.cpp:9-18, 70-98), the running closest narrowing, with its own nesting mask.  Only t is
+// kept: constant_volume::hit reads rec1.t / rec2.t alone (volumes.cpp:10-21).
+template <uint32_t F, typename PROG>
+MRT_DFN bool lin_sub_t(PROG prog, uint32_t b, uint32_t e, const Ray& r0, float tmin, float tmax, float* tout) {
+    Ray cur = r0;
+    float closest = tmax;
+    bool hit = false;
+    uint32_t act = 1u, lvl = 0;  // (lvl wave-uniform)
+    for (uint32_t pc = b; pc < e; pc++) {
+        const auto& o = prog[pc];
+        const uint32_t op = LOP_OP(o);
+        const bool on = (act >> lvl) & 1u;
+        if (op == LOP_PRIM) {
+            float t;
+            bool h;
+            switch (LOP_KIND(o)) {  // uniform: a scalar branch
+            case MRT_K_SPHERE: h = lin_prim_t<F, MRT_K_SPHERE>(o, cur, tmin, closest, &t); break;
+            case MRT_K_XY: h = lin_prim_t<F, MRT_K_XY>(o, cur, tmin, closest, &t); break;
+            case MRT_K_XZ: h = lin_prim_t<F, MRT_K_XZ>(o, cur, tmin, closest, &t); break;
+            default: h = lin_prim_t<F, MRT_K_YZ>(o, cur, tmin, closest, &t); break;
+            }
+            h = h & on;
+            closest = h ? t : closest;
+            hit = hit | h;
+        } else if (op == LOP_LIST) {
+            bool in = on;
+            if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, cur, tmin, closest);
+            lvl++;
+            act = (act & ~(1u << lvl)) | ((uint32_t)in << lvl);
+            if (!any_lane(in)) pc = o.skip - 1;
+        } else if (op == LOP_LIST_END) {
+            lvl--;
+        } else if (op == LOP_INST) {  // as scene_hit_lin's LOP_INST, from the volume-frame ray
+            const uint32_t kind = LOP_KIND(o);
+            bool in = on;
+            if (kind == MRT_K_TRROTY) {
+                cur = moved_ray<kFastUnit<F>>(r0, sub(r0.o, f3{o.f[8], o.f[9], o.f[10]}));
+                if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, cur, tmin, closest);
+            } else if (kind == MRT_K_ROTY) {
+                cur = r0;
+                if (in && (LOP_FLAGS(o) & MRT_F_HASBOX)) in = lin_box(o, cur, tmin, closest);
+            }
+            lvl++;
+            act = (act & ~(1u << lvl)) | ((uint32_t)in << lvl);
+            if (!any_lane(in)) {
+                pc = o.skip - 1;  // (its INST_END next)
+                continue;
+            }
+            if (kind == MRT_K_TRROTY || kind == MRT_K_ROTY) cur = rotate_ray<kFastUnit<F>>(cur, o.f[6], o.f[7]);
+            else cur = moved_ray<kFastUnit<F>>(r0, sub(r0.o, f3{o.f[0], o.f[1], o.f[2]}));
+        } else if (op == LOP_INST_END) {
+            cur = r0;
+            lvl--;
+        }
+    }
+    *tout = closest;
+    return hit;
+}
+
+// the record of a primitive op's hit (HK_PRIM: node `h`) or a constant_volume's (HK_VOL: op `h`,
+// volumes.cpp:24-31: the point at t, normal (1, 0, 0), the volume's phase-function material) for the
+// ray of the hit's frame
+template <uint32_t F, typename PROG>
+MRT_DFN void lin_hit_rec(const DScene& S, PROG prog, uint32_t hk, uint32_t h, const Ray& r, float t, HitRec& rec) {
+    if (MRT_LIN_DEFER && (F & FT_VOLUME) && hk == HK_VOL) {
+        rec.t = t;
+        rec.p = eval(r, t);
+        rec.n = f3{1, 0, 0};
+        rec.mat = prog[h].mat;
+        return;
+    }
+    lin_prim_rec<F>(S, h, r, t, rec);
+}
 
 template <uint32_t F>
 MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, const LStack& L, Pcg& rng, PhaseClock& ph) {
@@ -373,7 +459,11 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
     uint32_t inst = MRT_NONE;     // wave-uniform: op index of the enclosing instance
     uint32_t hnode = MRT_NONE;    // node of the closest hit so far (MRT_NONE: none)
     uint32_t hinst = MRT_NONE;    // op index of the instance it lies in (MRT_NONE: world frame)
-    bool hdone = false;           // rec already holds the closest hit (mesh_hit writes it)
+    // how the record is made after the walk: HK_PRIM from hnode's primitive; HK_DONE rec holds it
+    // (mesh_hit writes it); HK_VOL from volume op hnode; HK_BVHW from bvh leaf primitive hprim < htlim
+    uint32_t hk = HK_PRIM;
+    uint32_t hprim = 0;
+    float htlim = 0.0f;
     const MRT_CONST_AS LinOp* prog = const_ptr(S.prog);
     // one op: `o` is the op in place (constant memory) or its register copy (MRT_LIN_FETCH_ALL);
     // false at the program's end
@@ -400,7 +490,7 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
             closest = h ? t : closest;
             hnode = h ? o.node : hnode;
             hinst = h ? inst : hinst;
-            hdone = h ? false : hdone;
+            hk = h ? HK_PRIM : hk;
             PH_MARK(ph, 9);
         } else if (MRT_FAST_ROOM && kLinSlabOps<F> && op == LOP_ROOM) {
             float t;
@@ -412,7 +502,7 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
             closest = h ? t : closest;
             hnode = h ? fnode[face] : hnode;
             hinst = h ? inst : hinst;
-            hdone = h ? false : hdone;
+            hk = h ? HK_PRIM : hk;
             pc++;
         } else if (MRT_BOXINST && kLinSlabOps<F> && INST && op == LOP_INST && (LOP_FLAGS(o) & MRT_F_BOXINST)) {  // uniform
             // an instance of one box.h list, outside instances (cur is the query ray): the instance
@@ -439,7 +529,7 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
             closest = h ? t : closest;
             hnode = h ? prog[pc + 2 + c].node : hnode;
             hinst = h ? pc : hinst;
-            hdone = h ? false : hdone;
+            hk = h ? HK_PRIM : hk;
             pc = o.skip;  // its LOP_INST_END
         } else if (MRT_FAST_BOX && kLinSlabOps<F> && op == LOP_LIST && (LOP_FLAGS(o) & MRT_F_BOX6)) {  // uniform
             // box.h's six rects as one slab test (its own box test implied), the list skipped
@@ -449,14 +539,14 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
             closest = h ? t : closest;
             hnode = h ? prog[pc + 1 + c].node : hnode;
             hinst = h ? inst : hinst;
-            hdone = h ? false : hdone;
+            hk = h ? HK_PRIM : hk;
             pc = o.skip;  // past its LOP_LIST_END
         } else if ((F & FT_MESH) && op == LOP_MESH) {
             if (on && mesh_hit<true>(S, ld_node(const_ptr(S.nodes) + o.node), cur, tmin, closest, rec, true, L)) {
                 closest = rec.t;
                 hnode = o.node;
                 hinst = inst;
-                hdone = true;
+                hk = HK_DONE;
             }
         } else if ((F & FT_VOLUME) && op == LOP_VOLUME) {
             // constant_volume::hit (volumes.cpp:5-35): two boundary queries, then a free-flight
@@ -464,7 +554,10 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
             const MRT_CONST_AS LinOp& bo = prog[pc + 1];
             float t1, t2;
             bool h1, h2;
-            if (LOP_KIND(bo) == MRT_K_SPHERE) {
+            if ((F & FT_VSUB) && (LOP_FLAGS(o) & MRT_F_VSUB)) {  // uniform: the boundary is the sub-program
+                h1 = lin_sub_t<F>(prog, pc + 1, o.skip, cur, -FLT_MAX_, FLT_MAX_, &t1);
+                h2 = lin_sub_t<F>(prog, pc + 1, o.skip, cur, t1 + 0.0001f, FLT_MAX_, &t2);
+            } else if (LOP_KIND(bo) == MRT_K_SPHERE) {
                 h1 = lin_prim_t<F, MRT_K_SPHERE>(bo, cur, -FLT_MAX_, FLT_MAX_, &t1);
                 h2 = lin_prim_t<F, MRT_K_SPHERE>(bo, cur, t1 + 0.0001f, FLT_MAX_, &t2);
             } else if (LOP_KIND(bo) == MRT_K_XY) {
@@ -486,25 +579,42 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
                     const float hit_dist = -(1 / o.f[0]) * log_(randf(rng));
                     if (hit_dist < inside_dist) {
                         closest = a + hit_dist;
+#if MRT_LIN_DEFER
+                        hnode = pc;  // the volume op: its record after the walk
+                        hk = HK_VOL;
+#else
                         rec.t = closest;
                         rec.p = eval(cur, closest);
                         rec.n = f3{1, 0, 0};
                         rec.mat = o.mat;
                         hnode = o.node;
+                        hk = HK_DONE;
+#endif
                         hinst = inst;
-                        hdone = true;
                     }
                 }
             }
-            pc++;  // past the boundary op
+            pc = ((F & FT_VSUB) && (LOP_FLAGS(o) & MRT_F_VSUB)) ? o.skip - 1 : pc + 1;  // past the boundary
             PH_MARK(ph, 10);
         } else if ((F & FT_BVHW) && op == LOP_BVHW) {
+#if MRT_LIN_DEFER
+            HitRec tr;  // t, the leaf primitive (mat) and the range it passed with (u)
+            if (on && bvhw_walk<F>(S, S.nodes[o.node], cur, tmin, closest, tr, false, L)) {
+                closest = tr.t;
+                hnode = o.node;
+                hinst = inst;
+                hk = HK_BVHW;
+                hprim = tr.mat;
+                htlim = tr.u;
+            }
+#else
             if (on && bvhw_walk<F>(S, S.nodes[o.node], cur, tmin, closest, rec, true, L)) {
                 closest = rec.t;
                 hnode = o.node;
                 hinst = inst;
-                hdone = true;
+                hk = HK_DONE;
             }
+#endif
             PH_MARK(ph, 11);
         } else if (op == LOP_LIST) {  // object_list::hit box reject (scene_object.h:83)
             bool in = on;
@@ -553,31 +663,30 @@ MRT_DFN bool scene_hit_lin(const DScene& S, Ray& r, float tmin, HitRec& rec, con
     }
     if (INST) r = lin_load_ray(L);
     if (hnode == MRT_NONE) return false;
-    if (INST && hinst != MRT_NONE) {
-        // the instance op's words (per lane: vector loads) fetched before the record's node, so the
-        // two sets of loads are in flight together instead of one round trip after the other
-        // (only the words lin_untransform reads: its code, the offset f[0..2], rotate_y's f[6..7], the
-        // fused translation f[8..10])
+    // one copy of each record's code for hits in both frames: the ray of the hit's frame first (the
+    // instance ray recomputed, inst_ray), then the record, then the instance's transform back
+    const bool in_inst = INST && hinst != MRT_NONE;
 #if MRT_LIN_PREFETCH_INST
+    // the instance op's words (per lane: vector loads) fetched before the record's node, so the
+    // two sets of loads are in flight together instead of one round trip after the other
+    // (only the words inst_ray and lin_untransform read: its code, the offset f[0..2], rotate_y's
+    // f[6..7], the fused translation f[8..10])
+    LinOp io;
+    if (in_inst) {
         const LinOp* ip = S.prog + hinst;
-        LinOp io;
         io.code = ip->code;
         for (int k = 0; k < 3; k++) io.f[k] = ip->f[k];
         for (int k = 6; k < 11; k++) io.f[k] = ip->f[k];
-#else
-        const LinOp& io = S.prog[hinst];
-#endif
-        if (!hdone) {
-            const Ray ci = inst_ray<kFastUnit<F>>(io, r);
-            Ray ir = r;
-            ir.o = ci.o;
-            ir.d = ci.d;
-            lin_prim_rec<F>(S, hnode, ir, closest, rec);
-        }
-        lin_untransform(io, rec);
-    } else if (!hdone) {
-        lin_prim_rec<F>(S, hnode, r, closest, rec);
     }
+#else
+    const LinOp& io = S.prog[in_inst ? hinst : 0u];
+#endif
+    if (hk != HK_DONE) {
+        const Ray hr = in_inst ? inst_ray<kFastUnit<F>>(io, r) : r;
+        if (MRT_LIN_DEFER && (F & FT_BVHW) && hk == HK_BVHW) bvhw_leaf_rec<F>(S, hprim, hr, tmin, htlim, rec);
+        else lin_hit_rec<F>(S, prog, hk, hnode, hr, closest, rec);
+    }
+    if (in_inst) lin_untransform(io, rec);
     return true;
 }
 

@@ -540,6 +540,8 @@ struct LinCompiler {
     std::vector<LinOp> prog;
     int max_lvl = 0;
     uint32_t inst_pc = MRT_NONE;  // op index of the enclosing instance while its subtree is emitted
+    bool in_vsub = false;         // emitting a volume's boundary sub-program (primitives, lists, one instance level)
+    bool vsub = false;            // the program has such a volume (FT_VSUB)
     // code = op | kind << 8 | flags << 16 | nesting level << 24 (the level the op is tested at)
     LinOp op_of(uint32_t code, uint32_t id, int lvl) {
         const mrt_node& n = nodes[id];
@@ -568,20 +570,38 @@ struct LinCompiler {
             prog.push_back(leaf_op(LOP_PRIM, id, lvl));
             return true;
         case MRT_K_MESH:
+            if (in_vsub) return false;
             prog.push_back(leaf_op(LOP_MESH, id, lvl));
             return true;
         case MRT_K_BVHW: {
+            if (in_vsub) return false;
             LinOp o = leaf_op(LOP_BVHW, id, lvl);
             o.skip = n.a;  // the subtree's root ref (the op's f[0..5] are its box)
             prog.push_back(o);
             return true;
         }
-        case MRT_K_VOLUME: {  // a primitive boundary only (sphere / rect)
-            if (n.a >= nodes.size()) return false;
+        case MRT_K_VOLUME: {
+            if (n.a >= nodes.size() || in_vsub) return false;
             const uint32_t bk = nodes[n.a].kind & 0xFFu;
-            if (bk != MRT_K_SPHERE && bk != MRT_K_XY && bk != MRT_K_XZ && bk != MRT_K_YZ) return false;
-            prog.push_back(leaf_op(LOP_VOLUME, id, lvl));
-            prog.push_back(op_of(LOP_VBOUND, n.a, lvl));
+            if (bk == MRT_K_SPHERE || bk == MRT_K_XY || bk == MRT_K_XZ || bk == MRT_K_YZ) {  // a primitive boundary
+                prog.push_back(leaf_op(LOP_VOLUME, id, lvl));
+                prog.push_back(op_of(LOP_VBOUND, n.a, lvl));
+                return true;
+            }
+            // any other boundary (box.h lists, instances of them: cornell_smoke, scene.cpp:364-369)
+            // as a sub-program after the op, walked twice per query by the volume op (lin_sub_t) and
+            // skipped by the main walk; outside instances only (its instance is then the only level)
+            if (inst_depth > 0) return false;
+            const size_t at = prog.size();
+            LinOp vo = leaf_op(LOP_VOLUME, id, lvl);
+            vo.code |= MRT_F_VSUB << 16;
+            prog.push_back(vo);
+            in_vsub = true;
+            const bool ok = emit(n.a, inst_depth, 0, guard + 1);  // (levels of the sub-program from 0)
+            in_vsub = false;
+            if (!ok) return false;
+            prog[at].skip = (uint32_t)prog.size();
+            vsub = true;
             return true;
         }
         case MRT_K_LIST: {
@@ -597,9 +617,10 @@ struct LinCompiler {
             if (inst_depth > 0) return false;
             size_t at = prog.size();
             prog.push_back(op_of(LOP_INST, id, lvl));
-            inst_pc = (uint32_t)at;
+            const uint32_t outer_pc = inst_pc;
+            if (!in_vsub) inst_pc = (uint32_t)at;
             const bool ok = emit(n.a, inst_depth + 1, lvl + 1, guard + 1);
-            inst_pc = MRT_NONE;
+            inst_pc = outer_pc;
             if (!ok) return false;
             prog[at].skip = (uint32_t)prog.size();
             LinOp e = op_of(LOP_INST_END, id, lvl);
@@ -914,6 +935,7 @@ mrt_status mrt_internal_scene_tables(const mrt_scene_view* v, SceneTables* T) {
     T->features = scene_features(v, nodes, absorbed);
     const char* no_sig = getenv("MRT_NO_SIG");  // test hook: run the interpreter on known shapes too
     if (lin) T->features |= FT_LIN;
+    if (lin && lc.vsub) T->features |= FT_VSUB;
     if (lin) cornell_room_fill(lc.prog.data(), (uint32_t)lc.prog.size());  // (Cornell shape: the room into the END op)
     if (lin && !(no_sig && *no_sig && *no_sig != '0')) T->features |= MRT_SIG_BITS(lin_sig_of(lc.prog.data(), (uint32_t)lc.prog.size()));
     T->nbleaf = blist ? nodes[v->biased].b : 1u;
@@ -1404,7 +1426,11 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         s->n_launch++;
         if (handover) {  // this launch's rounding-critical paths, exact, into the radiance buffer (fold next)
             // (the exact arithmetic walks the program as compiled: the tolerance contract's rewrite has
-            // ops -- a room's slab test, one-step box instances -- only the fast builds compile)
+            // ops -- a room's slab test, one-step box instances -- only the fast builds compile).
+            // (On the context's fold stream beside the next launch -- its own list per radiance parity --
+            // it measured slower, round 6: its exact-arithmetic waves find no free registers beside the
+            // next path kernel's until that kernel ends, so the fold after it waited as long: C2 8.63
+            // against 8.32 ms per step, profiles/r06_ab.txt.)
             PathParams PR = P;
             PR.sc.prog = s->S.prog;
             hipLaunchKernelGGL(PL.retrace, dim3(kRetraceGroups), dim3(64), PL.retrace_lds, q, PR);

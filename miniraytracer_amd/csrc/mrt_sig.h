@@ -130,7 +130,7 @@ inline std::vector<LinOp> lin_rewrite_fast(const std::vector<LinOp>& prog) {
         for (uint32_t i = L + 1; i < prog[L].skip && i < n;) {
             const uint32_t op = prog[i].code & 0xFFu;
             if (op == LOP_LIST || op == LOP_INST) { i = prog[i].skip + 1; continue; }
-            if (op == LOP_VOLUME) { i += 2; continue; }
+            if (op == LOP_VOLUME) { i = ((prog[i].code >> 16) & MRT_F_VSUB) ? prog[i].skip : i + 2; continue; }
             kids.push_back(i);
             i++;
         }

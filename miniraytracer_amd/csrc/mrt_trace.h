@@ -161,6 +161,7 @@ struct DScene {
 #define MRT_F_BOX6 0x10u    /* set on upload on an object_list that is box.h's six rects (planes in f[6..11]) */
 #define MRT_F_BOXINST 0x20u /* tolerance-contract program: an instance outside instances whose body is one MRT_F_BOX6 list */
 #define MRT_F_LAST 0x40u    /* tolerance-contract program: the op after which the interpreter reaches the END op */
+#define MRT_F_VSUB 0x80u    /* linear program: a constant_volume op whose boundary is the sub-program [op + 1, skip) */
 #define MRT_K_TRROTY 11u    /* upload fuses translate(rotate_y(x)) into one instance node */
 #define MRT_K_BVHW 12u      /* upload: a bvh_node subtree over primitives / object_lists as wide nodes */
 
@@ -182,6 +183,9 @@ enum : uint32_t {
     FT_BVHW = 1u << 12,    // bvh_node subtrees as wide nodes (MRT_K_BVHW)
     FT_BIASED = 1u << 13,  // a biased (light-sampling) list: the mixture pdf of main.cpp:86-101
     FT_ALL = ((1u << 14) - 1) & ~FT_LIN,
+    // linear programs only: a constant_volume bounded by an object_list / instance subtree (box.h
+    // boundaries, cornell_smoke, scene.cpp:334-376), walked as a sub-program (mrt_lin.h lin_sub_t)
+    FT_VSUB = 1u << 14,
 };
 
 // Per-wave LDS stacks, lane-interleaved ([slot][word][lane]) so every access is conflict-free.
@@ -703,8 +707,10 @@ MRT_DFN bool bvhw_leaf(const DScene& S, uint32_t ref, const Ray& r, float tmin, 
         if (k == MRT_K_LIST) return false;
         HitRec tr;
         if (!leaf_prim_hit<F>(n, k, r, tmin, tmax, tr, false)) return false;
-        if (!full) {
+        if (!full) {  // t, and what bvhw_leaf_rec needs to make the record later
             rec.t = tr.t;
+            rec.mat = first;
+            rec.u = tmax;
             return true;
         }
         // the second test repeats the first's predicate with the same operands and range: its
@@ -747,8 +753,10 @@ MRT_DFN bool bvhw_leaf(const DScene& S, uint32_t ref, const Ray& r, float tmin, 
         closest = h ? tr.t : closest;
     }
     if (best == ~0u) return false;
-    if (!full) {
+    if (!full) {  // t, and what bvhw_leaf_rec needs to make the record later
         rec.t = closest;
+        rec.mat = first + best;
+        rec.u = t_before;
         return true;
     }
     const mrt_node c = ld_node_v(run + best);
@@ -761,6 +769,22 @@ MRT_DFN bool bvhw_leaf(const DScene& S, uint32_t ref, const Ray& r, float tmin, 
 #endif
     (void)again;
     return true;
+}
+
+// The record of a bvh_node leaf hit that bvhw_leaf(.., full = false) found: primitive `prim` of
+// S.bprims (its rec.mat) hit at or before tlim (its rec.u) -- bvhw_leaf's own second test, with the
+// same ray and range, made after the scene's walk instead of inside it (mrt_lin.h MRT_LIN_DEFER).
+template <uint32_t F>
+MRT_DFN void bvhw_leaf_rec(const DScene& S, uint32_t prim, const Ray& r, float tmin, float tlim, HitRec& rec) {
+    const mrt_node c = ld_node_v(S.bprims + prim);
+    const uint32_t ck = MRT_NODE_KIND(c);
+    bool again;  // (the same test with the same range: it hits again)
+    if (MRT_FAST_BOX && ck == MRT_K_LIST) again = box6_leaf_hit(c, r, tmin, tlim, rec, true);
+    else again = leaf_prim_hit<F>(c, ck, r, tmin, tlim, rec, true);
+#ifdef MRT_CHECK_LEAF
+    if (!again) __builtin_trap();
+#endif
+    (void)again;
 }
 
 #ifndef MRT_BVHW_BF

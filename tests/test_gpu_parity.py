@@ -152,7 +152,7 @@ def test_full_size_cornell_properties(gpu, orc):
 
 
 @pytest.mark.parametrize("sid,w,h,spp", [(5, 64, 64, 16), (9, 40, 40, 9), (8, 40, 40, 9), (2, 48, 24, 9),
-                                         (3, 48, 24, 9), (4, 48, 24, 9), (0, 48, 24, 9), (7, 40, 40, 4)])
+                                         (3, 48, 24, 9), (4, 48, 24, 9), (0, 48, 24, 9), (7, 40, 40, 4), (6, 40, 40, 9)])
 def test_linear_program_equals_generic_machine(gpu, sid, w, h, spp, monkeypatch):
     """Scenes without bvh_node/constant_volume run the linear hit program (mrt_lin.h); the generic
     explicit-stack machine (MRT_FORCE_GENERIC=1 at upload) must give the same bits per path."""
@@ -175,13 +175,15 @@ def test_linear_program_equals_generic_machine(gpu, sid, w, h, spp, monkeypatch)
 
 
 def test_kernel_selection(gpu):
-    """Volumes bounded by instances (scene 6) fall back to the generic machine; the Cornell box,
-    the meshes, the random spheres and book2 (bvh_nodes as wide nodes, sphere-bounded volumes) run
-    a linear program."""
-    for sid, want_lin in [(0, True), (6, False), (7, True), (5, True), (9, True)]:
+    """Every reference scene runs a linear program: the Cornell box, the meshes, the random spheres,
+    book2 (bvh_nodes as wide nodes, sphere-bounded volumes) and, round 6, Cornell smoke (volumes
+    bounded by instances of box.h lists, walked as sub-programs: FT_VSUB); MRT_FORCE_GENERIC keeps
+    the generic machine."""
+    for sid, want_lin, want_vsub in [(0, True, False), (6, True, True), (7, True, False), (5, True, False), (9, True, False)]:
         sc = gpu.select_scene(sid, 1.0)
         info = gpu.Renderer(sc, 0).kernel_info()
         assert bool(info["kernel_features"] & gpu._lib.FT_LIN) == want_lin, (sid, info)
+        assert bool(info["kernel_features"] & gpu._lib.FT_VSUB) == want_vsub, (sid, info)
 
 
 def test_tolerance_contract_builds(gpu):

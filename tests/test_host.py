@@ -359,3 +359,24 @@ def test_program_rewrite_structure(mrt, sid):
     for i, (o, k) in enumerate(zip(op1, s1)):
         if o in (LIST, INST):
             assert i < k < len(op1) and op1[k] == (LIST_END if o == LIST else INST_END), (i, o, k)
+
+
+def test_volume_boundary_subprogram_structure(mrt):
+    """Cornell smoke (scene 6, scene.cpp:334-376): each constant_volume bounded by
+    translate(rotate_y(box)) compiles to a LOP_VOLUME op flagged MRT_F_VSUB whose skip lands just past
+    its boundary sub-program -- the fused instance, box.h's list of six rects, their END ops -- so the
+    main walk steps over it and the volume op walks it twice per query (mrt_lin.h lin_sub_t)."""
+    PRIM, LIST, LIST_END, INST, INST_END, VOLUME, VSUB = 1, 3, 4, 5, 6, 8, 0x80
+    c, s = _lin_program(mrt, 6, False)
+    op = c & 0xFF
+    vols = [i for i, o in enumerate(op) if o == VOLUME]
+    assert len(vols) == 2
+    for i in vols:
+        assert (c[i] >> 16) & VSUB
+        body = list(op[i + 1:s[i]])
+        assert body == [INST, LIST] + [PRIM] * 6 + [LIST_END, INST_END], body
+        assert s[i + 1] == s[i] - 1 and s[i + 2] == s[i] - 2  # the instance's and the list's END ops
+    # book2's volumes keep their primitive boundary (LOP_VBOUND after the op, no flag)
+    c7, _ = _lin_program(mrt, 7, False)
+    v7 = [i for i, o in enumerate(c7 & 0xFF) if o == VOLUME]
+    assert v7 and all(not ((c7[i] >> 16) & VSUB) and (c7[i + 1] & 0xFF) == 9 for i in v7)
