@@ -78,7 +78,10 @@ using namespace mrtd;
 // scratch, which kept the query ray in scratch memory; with sel3 it is gone, 81 VGPRs at 5 waves
 // (C2 through the interpreter 43.3 -> 46.4 Grays/s), 80 at 6 (47.7), 72 + 5 spilled at 7 (44.1;
 // profiles/r05_ab.txt section 6)
-#define MRT_WPE_LIN_GEN 6
+// The exact contract's interpreter kernels keep 5 (96 VGPRs): at 6 the exact arithmetic spilled 39
+// VGPRs (C2 through the interpreter, exact: 45.2 ms per step at 6, 40.3 at 5, 43.5 at 4 waves,
+// round 6, profiles/r06_ab.txt section 4)
+#define MRT_WPE_LIN_GEN (MRT_FAST || MRT_TABLE_PEX ? 6 : 5)
 #endif
 template <uint32_t F> struct PathOcc {
     static constexpr bool kWide = (F & (FT_BVHW | FT_TEX | FT_VOLUME)) != 0 || !(F & FT_LIN);
@@ -201,6 +204,13 @@ MRT_DFN const DScene& kernarg_scene() {
 #ifndef MRT_OPAQUE_RESUME
 #define MRT_OPAQUE_RESUME 0  // the same in the room + mesh kernels' resumable loop: measured C3 -0.6%, C4 0 (A/B hook)
 #endif
+// A/B hook: the per-lane ray count kept in LDS (1 word per lane, after the wave's other slots), not in
+// a VGPR held across the path loop.  Round 6: neutral on C2 / C3 / C4, book2 -0.4% and random spheres
+// -1.5% (the word comes out of the treelet's LDS), and the exact interpreter at 5 waves keeps 7 of its
+// 8 spilled VGPRs (profiles/r06_ab.txt section 5): off
+#ifndef MRT_LDS_RAYS
+#define MRT_LDS_RAYS 0u
+#endif
 template <uint32_t F> struct PathQ {
     static constexpr bool on = MRT_PATHQ && (F & FT_MESH) == 0 && !TreeOf<F>::on;
     // LDS words per lane slot: o, dir, time, PCG state + inc, index (12); + the wave's claim state
@@ -213,7 +223,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
     // per wave: its stacks and queues ([slot][word][lane])
-    const uint32_t words = (P.lds_frames * 2 + P.lds_rays * 11 + P.lds_mesh + P.lds_save + LK * 4 + PathQ<F>::words) * 64;
+    const uint32_t words = (P.lds_frames * 2 + P.lds_rays * 11 + P.lds_mesh + P.lds_save + LK * 4 + PathQ<F>::words + MRT_LDS_RAYS) * 64;
     uint32_t* wb = lds + wave * words;
     uint32_t* const wmesh = wb + P.lds_frames * 128 + P.lds_rays * 704;
     float4* tree = nullptr;
@@ -300,7 +310,16 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
         in_tail = ((w >> 16) & 1u) != 0;
     };
     if constexpr (PathQ<F>::on) cold_store();
+#if MRT_LDS_RAYS
+    // each lane's count of the rays its finished paths traced, in the last LDS word of the wave's
+    // slots (ds_add at a path's end) instead of a register held across the path loop
+    uint32_t* const Lrays = wb + words - 64u + lane;
+    *Lrays = 0u;
+#define MRT_COUNT_RAYS(n) __hip_atomic_fetch_add(Lrays, (n), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+#else
     uint32_t done_rays = 0;
+#define MRT_COUNT_RAYS(n) (done_rays += (n))
+#endif
     PhaseClock ph{};
 #ifdef MRT_PHASES
     ph.t = __builtin_amdgcn_s_memtime();
@@ -419,7 +438,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
         }
 #endif
         if (P.path_rays) P.path_rays[idx] = ps.rays();
-        done_rays += ps.rays();
+        MRT_COUNT_RAYS(ps.rays());
         active = false;
     };
     // mesh variants keep one constructor per branch: the shared-constructor loop spills there
@@ -469,7 +488,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                     st_off = idx * 12u;
                     st_pend = true;
                     if (P.path_rays) P.path_rays[idx] = ps.rays();
-                    done_rays += ps.rays();
+                    MRT_COUNT_RAYS(ps.rays());
                     active = false;
                 } else {
                     want_ray = true;
@@ -695,7 +714,11 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
     }
 #endif
     // one 64-bit add per wave
+#if MRT_LDS_RAYS
+    uint64_t my = *Lrays;
+#else
     uint64_t my = done_rays;
+#endif
     for (int off = 32; off > 0; off >>= 1) my += __shfl_xor(my, off);
     if (lane == 0 && my) atomicAdd(P.rays, (unsigned long long)my);
 }
@@ -781,7 +804,8 @@ static KernelTable make_table(const char* numerics, std::index_sequence<I...>) {
                        {PathQ<kVariants[I]>::words...},
                        {kBox6Walk<kVariants[I]>...},
                        {(uint32_t)(kLinSlabOps<kVariants[I]> && MRT_SIG_OF(kVariants[I]) == SIG_NONE)...},
-                       {kfn_retrace<kVariants[I]>()...}};
+                       {kfn_retrace<kVariants[I]>()...},
+                       {(uint32_t)(MRT_LDS_RAYS + 0u * kVariants[I])...}};
 }
 #if MRT_TABLE_PEX
 const KernelTable& mrtd::kernel_table_fast_pex() {

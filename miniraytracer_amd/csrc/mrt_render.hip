@@ -51,6 +51,7 @@ static void take_variant(KernelTable& m, const KernelTable& s, uint32_t i) {
     m.pq[i] = s.pq[i];
     m.box6_walk[i] = s.box6_walk[i];
     m.rewrite[i] = s.rewrite[i];
+    m.lds_rays[i] = s.lds_rays[i];
 }
 static const KernelTable& fast_table() {
     static const KernelTable t = [] {
@@ -1069,7 +1070,7 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
         auto groups = [&](size_t lds) { return std::max(1, lds ? std::min<int>(nb_vgpr, (int)((160u * 1024u) / lds)) : nb_vgpr); };
         const size_t lds_core = (size_t)waves_per_wg * 64 * 4 *
                                 (s->lds_frames * 2 + s->lds_rays * 11 + L.lds_mesh + L.lds_save + tabs[k]->lev_k[s->variant] * 4 +
-                                 tabs[k]->pq[s->variant]);
+                                 tabs[k]->pq[s->variant] + tabs[k]->lds_rays[s->variant]);
         L.lds_bytes = lds_core;
         if (L.lds_bytes > (size_t)prop.sharedMemPerBlock) {
             mrt_scene_free(s);
