@@ -93,14 +93,15 @@ def parse():
                          "own stream, beside the next render's path kernel; C2 8.28 ms per step against 8.65 for "
                          "full), full (after its render's path kernel), lean (MRT_RF_FOLD_BEHIND, beside the other "
                          "contexts' path kernels: 8.35-8.45 ms per C2 step in most runs but 9.8-10.1 in about one "
-                         "of five); auto (default) = async at one context, full with several")
+                         "of five); auto (default) = async at one or two contexts, full with more")
     ap.add_argument("--pipeline", type=int, default=0,
-                    help="render contexts used round-robin on their own HIP streams (0 = auto: 3 when a rank "
+                    help="render contexts used round-robin on their own HIP streams (0 = auto: 2 when a rank "
                          "traces fewer than ~100 M paths per step, else 1).  With several contexts the GPU "
                          "runs their path kernels side by side, which hides a short launch's fixed costs "
-                         "(emulated 8-rank C2 share: 1.235 / 1.191 / 1.132 ms per step at 1 / 2 / 3 contexts) "
-                         "but gains nothing on a full C2 render and makes it bimodal (8.60-8.63 ms at 1 "
-                         "context; 8.69-8.71, and 9.3-9.4 in 2 runs of 4, at 3; DESIGN.md §4)")
+                         "(emulated 8-rank C2 share, round 6: 1.222 ms per step at 1 context, 1.102-1.114 at 2 "
+                         "with the async fold, 1.123-1.137 at 3 with the full fold) but gains nothing on a full "
+                         "C2 render and makes it bimodal (8.60-8.63 ms at 1 context; 8.69-8.71, and 9.3-9.4 in "
+                         "2 runs of 4, at 3; DESIGN.md §4)")
     ap.add_argument("--verify", action="store_true",
                     help="after timing, rank 0 checks the assembled framebuffer of the last step against a "
                          "single-context full render, bit for bit")
@@ -400,7 +401,10 @@ def main():
                                                      rank=d_rank, world=d_world))) * (int(np.sqrt(np.float32(args.samples))) ** 2)
     # contexts: several only where they pay -- a short per-rank launch (its fixed start / tail costs
     # hidden by the other contexts' kernels); a full C2 render gains nothing and turns bimodal
-    npipe = args.pipeline if args.pipeline > 0 else (3 if n_paths_local < 100_000_000 else 1)
+    # (round 6: two contexts with the async fold for the short shares -- the 8-rank C2 share 1.102-1.114
+    # against 1.123-1.137 ms per step with three contexts and the full fold, and steady: step-interval
+    # p90 1.11 ms against 2.2 ms, profiles/r06_ab.txt sections 6-7)
+    npipe = args.pipeline if args.pipeline > 0 else (2 if n_paths_local < 100_000_000 else 1)
     rnds = [m.Renderer(scene, device=local) for _ in range(npipe)]
     rnd = rnds[0]
     # The lean fold keeps one load in flight per lane, so beside the other contexts' path kernels it
@@ -408,9 +412,9 @@ def main():
     # long (C2 per-rank share, lean vs full, ms/step: 1 rank 8.36 / 8.59, 2: 4.16 / 4.30, 4: 2.19 /
     # 2.16, 8: 1.19 / 1.15; round 2) -- auto: lean from ~96 M paths per rank, with several contexts
     lean_fold = args.fold == "lean"
-    # auto: one context -> each render's fold beside the next render's path kernel (C2: 8.28 vs 8.65
-    # ms per step, profiles/r05_ab.txt section 27); several contexts -> the full fold after the kernel
-    async_fold = args.fold == "async" or (args.fold == "auto" and npipe == 1)
+    # auto: one or two contexts -> each render's fold beside the next render's path kernel (C2: 8.28 vs
+    # 8.65 ms per step, profiles/r05_ab.txt section 27); more contexts -> the full fold after the kernel
+    async_fold = args.fold == "async" or (args.fold == "auto" and npipe <= 2)
     def desc_of(numerics):
         return m.render_desc(args.width, args.height, args.samples, depth=args.depth, tile_size=args.tile_size,
                              rank=d_rank, world=d_world, numerics=numerics, chunk_samples=args.chunk_samples,

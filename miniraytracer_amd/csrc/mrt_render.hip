@@ -324,6 +324,9 @@ struct PathLaunch {
     path_kernel_t retrace = nullptr;  // the exact arithmetic for its rounding-critical paths (mrt_retrace_kernel)
     size_t retrace_lds = 0;
     bool handover = false;  // the kernel hands its rounding-critical paths to it (fast arithmetic)
+    // the retrace kernel's waves fit a path-kernel wave's registers (1-wave path groups): under the
+    // async fold it may run on the fold stream in slots the next launch leaves free (kRetraceSide)
+    bool retrace_side = false;
     uint32_t walk_min = 32;  // resumable mesh walk threshold of this build (PathParams::walk_min)
 };
 
@@ -391,7 +394,8 @@ struct mrt_scene {
     uint32_t prev_w = 0, prev_h = 0;
     uint32_t lev_rows = 0;
     uint64_t* d_counter = nullptr;   // 64 B scratch: [0] paths handed to the exact arithmetic since upload, [2] ray total of mrt_render, [4] cancel flag,
-                                     // [1] rounding-critical paths listed (u32), [3] retrace groups done (u32), [5] listed beyond the cap since upload
+                                     // [1] rounding-critical paths listed (u32), [3] retrace groups done (u32), [5] listed beyond the cap since upload,
+                                     // [6] the parity-1 list's count (u32) and retrace groups done (u32)
     uint32_t* d_rt = nullptr;        // rounding-critical paths listed for the retrace kernel (path indices)
     size_t rt_cap = 0;
     uint64_t* d_counters = nullptr;  // one work counter per chunk launch (progress reads them)
@@ -1060,6 +1064,13 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
             L.handover = k == 1 && L.retrace && L.fn != kernel_table_fast_pex().kernel[s->variant] && !(e && *e && atoi(e) == 0);
         }
         L.retrace_lds = (size_t)64 * 4 * (s->lds_frames * 2 + s->lds_rays * 11 + s->lds_mesh + s->lds_save);
+        if (L.handover) {
+            hipFuncAttributes ra{};
+            HIPCHK(hipFuncGetAttributes(&ra, reinterpret_cast<const void*>(L.retrace)));
+            hipFuncAttributes pa{};
+            HIPCHK(hipFuncGetAttributes(&pa, reinterpret_cast<const void*>(L.fn)));
+            L.retrace_side = L.wg == 64u && ((ra.numRegs + 7) & ~7) <= ((pa.numRegs + 7) & ~7);
+        }
         // the path-exact build (the metal bunny under the tolerance contract) yields at 32 walking
         // lanes: 40 -1.2%, 28 -1.7%, 48 -10% (bunny 1024x1024x64, profiles/r04_ab.txt section 13)
         L.walk_min = (!walk_min_env && L.fn == kernel_table_fast_pex().kernel[s->variant]) ? 32u : s->walk_min;
@@ -1174,6 +1185,16 @@ static constexpr uint32_t kRtCap = 1u << 20;
 // one-wave groups of the retrace kernel: 16384 lanes, a path each (more loop); its time is the longest
 // listed path's, plus the launch
 static constexpr uint32_t kRetraceGroups = 256;
+// A/B hook (round 6, off): under MRT_RF_FOLD_ASYNC each launch's retrace on the context's fold stream,
+// beside the next launch's path kernel, in kRetraceSide one-wave groups that the next path kernel
+// leaves free (it is launched with that many fewer one-wave groups; each radiance parity has its own
+// list).  On the render's stream the GPU idles for the retrace's longest path (~0.1 ms per launch) --
+// but the previous launch's fold fills that gap: moved beside the next kernel, the retrace delays the
+// fold behind it on the fold stream (which then has only the free slots), and the launch after next
+// waits for that fold: C2 8.66-8.72 against 8.27 ms per step, the 8-rank share 1.102-1.104 against
+// 1.109-1.130 ms (two contexts) (profiles/r06_ab.txt sections 2 and 7; without the free slots the
+// retrace waited for the next kernel's end: 8.61-8.72 ms).  MRT_RETRACE_SIDE=<groups> turns it on.
+static constexpr uint32_t kRetraceSide = 0;
 
 #define MRT_GPU_ONLY(s, what) \
     if ((s) && (s)->cpu) return mrt_internal_fail(MRT_ERR_INVALID, what " is a GPU-backend entry point (scene on MRT_DEVICE_CPU)")
@@ -1232,8 +1253,9 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
         for (hipEvent_t& e : s->ev_fold)
             if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
+    // (two lists: one per radiance parity, for the async fold's retrace beside the next launch)
     if ((d->flags & MRT_RF_FAST) && !(d->flags & MRT_RF_PATH_DEBUG) && s->pl[1].handover &&
-        (st = grow(s, (void**)&s->d_rt, &s->rt_cap, (size_t)kRtCap * sizeof(uint32_t))))
+        (st = grow(s, (void**)&s->d_rt, &s->rt_cap, (size_t)2 * kRtCap * sizeof(uint32_t))))
         return st;
     if ((st = grow(s, (void**)&s->d_acc, &s->acc_cap, (size_t)s->npix * 16))) return st;
     if ((st = grow(s, (void**)&s->d_out, &s->out_cap, (size_t)s->npix * 16 + 16))) return st;
@@ -1362,6 +1384,14 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         HIPCHK(hipStreamWriteValue32(q, s->h_seq, 0u, 0));
         s->prev_epoch++;
     }
+    // the rounding-critical paths' hand-over: tolerance contract, not the per-path debug output
+    // (whose radiance is the fast kernel's own); under the async fold its retrace beside the next
+    // launch (kRetraceSide) where its waves fit the path kernel's slots
+    const bool handover = PL.handover && !(d->flags & MRT_RF_PATH_DEBUG);
+    uint32_t side = (handover && async && PL.retrace_side) ? kRetraceSide : 0u;
+    if (const char* e = getenv("MRT_RETRACE_SIDE"))  // A/B hook
+        if (*e && handover && async && PL.retrace_side) side = (uint32_t)atoi(e);
+    const int grid = PL.grid - (int)std::min<uint32_t>(side, (uint32_t)PL.grid / 2u);  // one-wave groups: its waves' slots left free
     for (uint32_t s0 = 0; s0 < ns; s0 += s->chunk) {
         uint32_t s1 = std::min(ns, s0 + s->chunk);
         const uint32_t par = async ? s->lpar : 0u;
@@ -1395,13 +1425,13 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.ns = ns;
         P.s0 = s0;
         P.n_paths = s->npix * (s1 - s0);
-        P.tail_zone = (uint32_t)std::min<uint64_t>((uint64_t)PL.grid * (PL.wg / 64u) * 2 * MRT_BATCH, P.n_paths);  // ~2 big claims per wave
-        P.static_first = (uint64_t)P.n_paths < (uint64_t)PL.grid * (PL.wg / 64u) * MRT_BATCH * 64u;
+        P.tail_zone = (uint32_t)std::min<uint64_t>((uint64_t)grid * (PL.wg / 64u) * 2 * MRT_BATCH, P.n_paths);  // ~2 big claims per wave
+        P.static_first = (uint64_t)P.n_paths < (uint64_t)grid * (PL.wg / 64u) * MRT_BATCH * 64u;
         // MRT_NPART contiguous work partitions, one counter each; the waves of partition k (workgroups
         // b with b % MRT_NPART == k) take its first batches statically when P.static_first
         for (uint32_t k = 0; k <= MRT_NPART; k++) P.part_base[k] = (uint64_t)P.n_paths * k / MRT_NPART;
         for (uint32_t k = 0; k < MRT_NPART; k++) {
-            const uint64_t waves_k = (uint64_t)((PL.grid - k + MRT_NPART - 1) / MRT_NPART) * (PL.wg / 64u);
+            const uint64_t waves_k = (uint64_t)((grid - k + MRT_NPART - 1) / MRT_NPART) * (PL.wg / 64u);
             P.part_dyn[k] = P.part_base[k] + (P.static_first ? waves_k * MRT_BATCH : 0);
         }
         P.seed = d->seed;
@@ -1414,32 +1444,35 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.rays = d_rays ? (unsigned long long*)d_rays : s->d_rays;
         P.lev = s->d_lev;
         P.lev_rows = s->lev_rows;
-        // the rounding-critical paths' hand-over: tolerance contract, not the per-path debug output
-        // (whose radiance is the fast kernel's own)
-        const bool handover = PL.handover && !(d->flags & MRT_RF_PATH_DEBUG);
+        // the list of the launch's radiance parity: entries at par * kRtCap, its count and its groups-done
+        // word at d_counter[1] / [3] (parity 0) or the two halves of d_counter[6] (parity 1)
         if (handover)
-            P.rt = RetraceList{s->d_rt, (uint32_t*)(s->d_counter + 1), kRtCap, (uint32_t*)(s->d_counter + 3), (unsigned long long*)s->d_counter,
+            P.rt = RetraceList{s->d_rt + (size_t)par * kRtCap, par ? (uint32_t*)(s->d_counter + 6) : (uint32_t*)(s->d_counter + 1), kRtCap,
+                               par ? (uint32_t*)(s->d_counter + 6) + 1 : (uint32_t*)(s->d_counter + 3), (unsigned long long*)s->d_counter,
                                (unsigned long long*)(s->d_counter + 5)};
         HIPCHK(hipEventRecord(s->ev[2 * s->n_launch], q));
-        hipLaunchKernelGGL(PL.fn, dim3(PL.grid), dim3(PL.wg), PL.lds_bytes, q, P);
+        hipLaunchKernelGGL(PL.fn, dim3(grid), dim3(PL.wg), PL.lds_bytes, q, P);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(s->ev[2 * s->n_launch + 1], q));
         s->n_launch++;
-        if (handover) {  // this launch's rounding-critical paths, exact, into the radiance buffer (fold next)
-            // (the exact arithmetic walks the program as compiled: the tolerance contract's rewrite has
-            // ops -- a room's slab test, one-step box instances -- only the fast builds compile).
-            // (On the context's fold stream beside the next launch -- its own list per radiance parity --
-            // it measured slower, round 6: its exact-arithmetic waves find no free registers beside the
-            // next path kernel's until that kernel ends, so the fold after it waited as long: C2 8.63
-            // against 8.32 ms per step, profiles/r06_ab.txt.)
-            PathParams PR = P;
-            PR.sc.prog = s->S.prog;
+        // this launch's rounding-critical paths, exact, into the radiance buffer before its fold (the
+        // exact arithmetic walks the program as compiled: the tolerance contract's rewrite has ops -- a
+        // room's slab test, one-step box instances -- only the fast builds compile)
+        PathParams PR = P;
+        PR.sc.prog = s->S.prog;
+        if (handover && !side) {  // on the render's stream, the whole GPU
             hipLaunchKernelGGL(PL.retrace, dim3(kRetraceGroups), dim3(64), PL.retrace_lds, q, PR);
             HIPCHK(hipGetLastError());
         }
-        if (async) {  // the fold beside the next launch's path kernel
+        if (async) {  // (the retrace and) the fold on the fold stream, beside the next launch's path kernel
             HIPCHK(hipEventRecord(s->ev_kern, q));
             HIPCHK(hipStreamWaitEvent(s->fstream, s->ev_kern, 0));
+        }
+        if (handover && side) {  // in the slots the next path kernel leaves free (kRetraceSide)
+            hipLaunchKernelGGL(PL.retrace, dim3(side), dim3(64), PL.retrace_lds, s->fstream, PR);
+            HIPCHK(hipGetLastError());
+        }
+        if (async) {  // the fold beside the next launch's path kernel
             const bool last = s1 == ns;
             FoldEnd fe{last ? (float4*)d_local : nullptr, ns, last ? d_cnt : nullptr, last ? h_prog : nullptr,
                        last ? launches * MRT_CNT_SLOTS : 0u, last ? launches * MRT_NPART : 0u};

@@ -864,3 +864,44 @@ def test_rounding_critical_paths_retraced_exactly(gpu, monkeypatch, walk):
     err_b = np.abs(b[..., :3].astype(np.float64) - ex[..., :3])[diff].sum()
     print("changed pixels", int(diff.sum()), "|fast - exact| with / without hand-over", err_a, err_b)
     assert err_a < err_b
+
+
+@pytest.mark.parametrize("side", ["32", "0"])
+def test_async_retrace_beside_next_launch(gpu, monkeypatch, side):
+    """Under MRT_RF_FOLD_ASYNC each launch's rounding-critical paths are retraced on the render's
+    stream (MRT_RETRACE_SIDE=0, the default) or, as an A/B hook, on the context's fold stream beside
+    the next launch's path kernel, in one-wave slots that kernel leaves free (mrt_render.hip
+    kRetraceSide; each radiance parity with its own list).  Back-to-back async renders of a C2 size
+    that lists a few hundred paths per launch (three launches per render: both lists in use) equal
+    the blocking render bit for bit, with the same count of handed-over paths per render."""
+    import torch
+    monkeypatch.setenv("MRT_RETRACE_SIDE", side)
+    w, h, spp = 250, 250, 192
+    sc = gpu.select_scene(5, 1.0)
+    r0 = gpu.Renderer(sc, 0)
+    h0 = r0.kernel_info()["handed_over"]
+    ref, rays1 = r0.render(gpu.render_desc(w, h, spp, numerics="fast", chunk_samples=64))
+    listed = r0.kernel_info()["handed_over"] - h0
+    assert listed > 0
+    d = gpu.render_desc(w, h, spp, numerics="fast", chunk_samples=64, flags=gpu._lib.RF_FOLD_ASYNC)
+    c = gpu.Renderer(sc, 0)
+    c.prepare(d)
+    px = gpu.local_pixels(d)
+    dev = torch.device("cuda", 0)
+    outs = [torch.zeros((len(px), 4), dtype=torch.float32, device=dev) for _ in range(3)]
+    rays_d = torch.zeros(1, dtype=torch.int64, device=dev)
+    s = torch.cuda.Stream(dev)
+    torch.cuda.synchronize(dev)
+    h1 = c.kernel_info()["handed_over"]
+    for o in outs:
+        c.render_device(d, o.data_ptr(), rays_d.data_ptr(), s.cuda_stream)
+    c.join(s.cuda_stream)
+    s.synchronize()
+    assert c.kernel_info()["handed_over"] - h1 == len(outs) * listed
+    assert int(rays_d.item()) == len(outs) * rays1
+    for o in outs:
+        im = np.zeros((w * h, 4), dtype=np.float32)
+        im[px] = o.cpu().numpy()
+        assert np.array_equal(im.reshape(h, w, 4)[..., :3].view(np.uint32), ref[..., :3].view(np.uint32))
+    c.close()
+    r0.close()
