@@ -146,6 +146,9 @@ extern "C" int mrt_debug_bstats(unsigned long long* out, int reset) {
 #ifndef MRT_WALK_OTHER
 #define MRT_WALK_OTHER 16u
 #endif
+#ifndef MRT_WALK_UNROLL
+#define MRT_WALK_UNROLL 1
+#endif
 #if defined(MRT_EXPERIMENTS) && defined(MRT_WPE)  // experiment hook: override for every variant
 #define MRT_OCC(F) MRT_WPE
 #else
@@ -643,11 +646,14 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
             // at least one step per iteration for every walking lane (no lane starves), then more
             // while enough lanes walk or too few have anything else to do
             while (__any(phase == PH_WALK)) {
-                if (phase == PH_WALK) {
-                    const mrt_node mn = ld_node(const_ptr(S.nodes) + prog[kMeshPC].node);
-                    const uint32_t st = mesh_step<false, true>(S, mn, ps.r, 0.001f, w.closest, rec, Ls, ref, msp, w.hdone);
-                    if (st == 1u) w.hnode = kMeshPC;  // w.closest = the hit's t, w.hdone set
-                    phase = st != 0u ? PH_DONE : PH_WALK;
+#pragma unroll
+                for (int u = 0; u < MRT_WALK_UNROLL; u++) {  // (A/B hook: steps between two yield checks)
+                    if (phase == PH_WALK) {
+                        const mrt_node mn = ld_node(const_ptr(S.nodes) + prog[kMeshPC].node);
+                        const uint32_t st = mesh_step<false, true>(S, mn, ps.r, 0.001f, w.closest, rec, Ls, ref, msp, w.hdone);
+                        if (st == 1u) w.hnode = kMeshPC;  // w.closest = the hit's t, w.hdone set
+                        phase = st != 0u ? PH_DONE : PH_WALK;
+                    }
                 }
                 if ((uint32_t)__popcll(__ballot(phase == PH_WALK)) <= P.walk_min &&
                     (uint32_t)__popcll(__ballot(phase == PH_DONE || (!active && !exhausted))) >= MRT_WALK_OTHER)
