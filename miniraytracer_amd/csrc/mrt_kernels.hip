@@ -146,8 +146,18 @@ extern "C" int mrt_debug_bstats(unsigned long long* out, int reset) {
 #ifndef MRT_WALK_OTHER
 #define MRT_WALK_OTHER 16u
 #endif
+// walk steps between two yield checks of the resumable mesh walk (round 6: 2 against 1, teapot +1.5%,
+// bunny +0.8%; 3: +1.0% / +0.6%, profiles/r06_ab.txt section 8)
 #ifndef MRT_WALK_UNROLL
-#define MRT_WALK_UNROLL 1
+#define MRT_WALK_UNROLL 2
+#endif
+// leaf postponing in the resumable mesh walk (mrt_trace.h mesh_step_spec; A/B hook): a leaf step
+// once at least MRT_SPEC_LEAF lanes hold a parked run, or when no lane can take an inner step
+#ifndef MRT_MESH_SPEC
+#define MRT_MESH_SPEC 0
+#endif
+#ifndef MRT_SPEC_LEAF
+#define MRT_SPEC_LEAF 32u
 #endif
 #if defined(MRT_EXPERIMENTS) && defined(MRT_WPE)  // experiment hook: override for every variant
 #define MRT_OCC(F) MRT_WPE
@@ -599,6 +609,9 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
         static_assert(kSigs[SIG_ROOM_MESH].op[kMeshPC] == LOP_MESH, "room + mesh program shape");
         const MRT_CONST_AS LinOp* prog = const_ptr(S.prog);
         uint32_t phase = 0, ref = 0, msp = 0;
+#if MRT_MESH_SPEC
+        uint32_t pref = 0;  // the parked leaf run (mesh_step_spec)
+#endif
         SigState w;
         w.closest = FLT_MAX_;
         w.hnode = MRT_NONE;
@@ -640,6 +653,9 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                                                   0.001f, w.closest);
                 ref = mn.b;
                 msp = 0;
+#if MRT_MESH_SPEC
+                pref = 0;
+#endif
                 phase = enter ? PH_WALK : PH_DONE;
             }
             PH_MARK(ph, 1);
@@ -648,12 +664,23 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
             while (__any(phase == PH_WALK)) {
 #pragma unroll
                 for (int u = 0; u < MRT_WALK_UNROLL; u++) {  // (A/B hook: steps between two yield checks)
+#if MRT_MESH_SPEC
+                    // the wave's choice: a leaf step once enough runs are parked or no inner step is left
+                    const bool can_inner = phase == PH_WALK && ref != kMeshEnd && !((ref & MESH_LEAF) && pref != 0u);
+                    const bool leaf_iter = (uint32_t)__popcll(__ballot(phase == PH_WALK && pref != 0u)) >= MRT_SPEC_LEAF || !__any(can_inner);
+                    if (phase == PH_WALK) {
+                        const uint32_t st = mesh_step_spec<false>(S, ps.r, 0.001f, w.closest, rec, Ls, ref, pref, msp, w.hdone, leaf_iter);
+                        if (st == 1u) w.hnode = kMeshPC;  // w.closest = the hit's t, w.hdone set
+                        phase = st != 0u ? PH_DONE : PH_WALK;
+                    }
+#else
                     if (phase == PH_WALK) {
                         const mrt_node mn = ld_node(const_ptr(S.nodes) + prog[kMeshPC].node);
                         const uint32_t st = mesh_step<false, true>(S, mn, ps.r, 0.001f, w.closest, rec, Ls, ref, msp, w.hdone);
                         if (st == 1u) w.hnode = kMeshPC;  // w.closest = the hit's t, w.hdone set
                         phase = st != 0u ? PH_DONE : PH_WALK;
                     }
+#endif
                 }
                 if ((uint32_t)__popcll(__ballot(phase == PH_WALK)) <= P.walk_min &&
                     (uint32_t)__popcll(__ballot(phase == PH_DONE || (!active && !exhausted))) >= MRT_WALK_OTHER)

@@ -632,6 +632,58 @@ MRT_DFN uint32_t mesh_step(const DScene& S, const mrt_node& n, const Ray& r, flo
     ref = L.mesh[(--msp) * 64 + L.lane];
     return 0u;
 }
+// Leaf postponing (Aila & Laine 2009's speculative traversal) for the resumable mesh walk, as an
+// A/B variant of mesh_step<TREE, true> (MRT_MESH_SPEC): a lane that reaches a leaf run parks it in
+// `pref` and walks on through inner nodes in DFS order (the stack's next entries), stopping at a
+// second leaf or the stack's end; the WAVE chooses per iteration between an inner step (every lane
+// that can take one) and a leaf step (one triangle of every parked run), so an iteration runs one of
+// the two codes instead of both.  Same results: the nodes walked past a parked leaf are the ones DFS
+// visits after it, tested with the same tt (a parked run that hits ends the walk, and the steps
+// taken beyond it are dropped).  kMeshEnd: the stack ran out while a run is parked.
+static constexpr uint32_t kMeshEnd = 0xFFFFFFFFu;
+template <bool TREE = false>
+MRT_DFN uint32_t mesh_step_spec(const DScene& S, const Ray& r, float tmin, float& tt, HitRec& rec, const LStack& L, uint32_t& ref,
+                                uint32_t& pref, uint32_t& msp, bool& in_hit, bool leaf_iter) {
+    uint32_t res = 0u;
+    if (leaf_iter) {  // one triangle of the parked run (mesh_step's leaf step)
+        if (pref != 0u) {
+            const uint32_t first = pref & 0xFFFFFFu, cnt = (pref >> 24) & 0x7Fu;
+            float t = 0.0f, uu = 0.0f, vv = 0.0f;
+            const bool h = cnt > 0 && tri_hit(S, first, r, tmin, tt, &t, &uu, &vv);
+            in_hit = in_hit || h;
+            tt = h ? t : tt;
+            rec.mat = h ? first : rec.mat;
+            rec.u = h ? uu : rec.u;
+            rec.v = h ? vv : rec.v;
+            const bool more = cnt > 1;
+            pref = more ? (MESH_LEAF | ((cnt - 1) << 24) | (first + 1)) : 0u;
+            res = (!more && in_hit) ? 1u : ((!more && ref == kMeshEnd) ? 2u : 0u);
+        }
+        return res;
+    }
+    if (ref == kMeshEnd) return 0u;  // waits for its parked run
+    if (ref & MESH_LEAF) {
+        if (pref != 0u) return 0u;  // a second leaf: waits
+        pref = ref;                  // parked; the walk goes on with the stack's next entry
+        ref = msp == 0u ? kMeshEnd : L.mesh[(--msp) * 64 + L.lane];
+        return 0u;
+    }
+    const WideNode W = mesh_wide<TREE>(S, ref, L);
+    const bool hl = aabb_hit(W.lmin, W.lmax, r, tmin, tt);
+    const bool hr = aabb_hit(W.rmin, W.rmax, r, tmin, tt);
+    const bool left_first = (W.order & r.mask) != 0;
+    const uint32_t cref = left_first ? W.lref : W.rref, fref = left_first ? W.rref : W.lref;
+    const bool hc = left_first ? hl : hr, hf = left_first ? hr : hl;
+    if (hc && hf) L.mesh[(msp++) * 64 + L.lane] = fref;
+    ref = hc ? cref : (hf ? fref : ref);
+    if (!hc && !hf) {
+        if (msp != 0u) ref = L.mesh[(--msp) * 64 + L.lane];
+        else if (pref != 0u) ref = kMeshEnd;
+        else res = 2u;
+    }
+    return res;
+}
+
 // the record mesh_step<TREE, true> left for mesh_leaf: its closest triangle's point and normal,
 // the mesh's material (the same operations as mesh_step's own completion)
 MRT_DFN void mesh_hit_rec(const DScene& S, const mrt_node& n, const Ray& r, float tt, HitRec& rec) {
