@@ -195,7 +195,7 @@ mrt_status mrt_preview(mrt_scene* s, float* rgb_out, uint32_t* samples_done);
 mrt_status mrt_kernel_ms(mrt_scene* s, float* path_ms, uint32_t* launches);
 
 /* Which path kernel the scene runs: feature bits of the scene (FT_* of mrt_trace.h; bit 11 =
- * linear hit program, DESIGN.md "Kernels"), dynamic LDS bytes per workgroup, grid size in
+ * linear hit program, bit 14 = a volume bounded by a sub-program, DESIGN.md "Kernels"), dynamic LDS bytes per workgroup, grid size in
  * workgroups, threads per workgroup, the BVH nodes each workgroup keeps in LDS, and the build of
  * the kernel for the last render's numerics: MRT_BUILD_* (the tolerance contract runs the fast,
  * the denormal-flushing or the path-exact build per kernel variant). */
