@@ -148,6 +148,18 @@ extern "C" int mrt_debug_bstats(unsigned long long* out, int reset) {
 #endif
 // walk steps between two yield checks of the resumable mesh walk (round 6: 2 against 1, teapot +1.5%,
 // bunny +0.8%; 3: +1.0% / +0.6%, profiles/r06_ab.txt section 8)
+// Path starts batched in the resumable mesh loop (round 6): the lanes whose path ended start new
+// ones only once at least MRT_START_MIN of the wave's lanes are idle (or none is busy), so the path
+// start (claim, PCG seeding, the camera ray with its disk-rejection draws) runs at a wider lane
+// mask; the idle lanes wait for it through a walk.  Measured (profiles/r06_ab.txt section 13):
+// teapot (fast) +0.6% at 8, +2.9% at 16; bunny (path-exact) +0.9% at 8, -1.2% at 16.  The plain loop
+// (bvh_node scenes: book2 -0.1% / -1.0%, random spheres +0.5% / -0.3%) keeps 1 (MRT_START_MIN_PLAIN).
+#ifndef MRT_START_MIN
+#define MRT_START_MIN (MRT_FAST ? 16u : 8u)
+#endif
+#ifndef MRT_START_MIN_PLAIN
+#define MRT_START_MIN_PLAIN 1u
+#endif
 #ifndef MRT_WALK_UNROLL
 #define MRT_WALK_UNROLL 2
 #endif
@@ -623,10 +635,11 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
             const DScene& S = kernarg_scene();  // (shadows P.sc for this iteration)
             const MRT_CONST_AS LinOp* prog = const_ptr(S.prog);
 #endif
-            take_paths([&](float u, float v) {
-                ps.r = camera_ray(S, ps.rng, u, v);
-                phase = PH_BEGIN;
-            });
+            if (MRT_START_MIN <= 1 || (uint32_t)__popcll(__ballot(!active)) >= MRT_START_MIN || !__any(active))
+                take_paths([&](float u, float v) {
+                    ps.r = camera_ray(S, ps.rng, u, v);
+                    phase = PH_BEGIN;
+                });
             if (!__any(active)) break;
             PH_MARK(ph, 0);
             if (phase == PH_BEGIN) {  // the room's walls (scene_hit_sig's ops 0..6), then the mesh root box
@@ -707,7 +720,8 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
         }
     } else {
         for (;;) {
-            take_paths([&](float u, float v) { ps.r = camera_ray(S, ps.rng, u, v); });
+            if (MRT_START_MIN_PLAIN <= 1 || (uint32_t)__popcll(__ballot(!active)) >= MRT_START_MIN_PLAIN || !__any(active))
+                take_paths([&](float u, float v) { ps.r = camera_ray(S, ps.rng, u, v); });
             if (!__any(active)) break;
             PH_MARK(ph, 0);
 #if MRT_OPAQUE_SCENE
