@@ -163,13 +163,16 @@ extern "C" int mrt_debug_bstats(unsigned long long* out, int reset) {
 #ifndef MRT_WALK_UNROLL
 #define MRT_WALK_UNROLL 2
 #endif
-// leaf postponing in the resumable mesh walk (mrt_trace.h mesh_step_spec; A/B hook): a leaf step
-// once at least MRT_SPEC_LEAF lanes hold a parked run, or when no lane can take an inner step
+// Leaf postponing in the resumable mesh walk (mrt_trace.h mesh_step_spec): the path-exact build
+// (the metal bunny, C4) chooses per step between a leaf step and an inner step by majority
+// (MRT_SPEC_LEAF 0): bunny +0.8%; the fast build (teapot, C3) keeps mesh_step (-5.5% with it); a leaf
+// step once 8 / 16 / 32 / 48 runs are parked: bunny -10% / -2.2% / -19% / -58% (profiles/r06_ab.txt
+// sections 8 and 14)
 #ifndef MRT_MESH_SPEC
-#define MRT_MESH_SPEC 0
+#define MRT_MESH_SPEC MRT_TABLE_PEX
 #endif
 #ifndef MRT_SPEC_LEAF
-#define MRT_SPEC_LEAF 32u
+#define MRT_SPEC_LEAF 0u
 #endif
 #if defined(MRT_EXPERIMENTS) && defined(MRT_WPE)  // experiment hook: override for every variant
 #define MRT_OCC(F) MRT_WPE
@@ -229,13 +232,6 @@ MRT_DFN const DScene& kernarg_scene() {
 #ifndef MRT_OPAQUE_RESUME
 #define MRT_OPAQUE_RESUME 0  // the same in the room + mesh kernels' resumable loop: measured C3 -0.6%, C4 0 (A/B hook)
 #endif
-// A/B hook: the per-lane ray count kept in LDS (1 word per lane, after the wave's other slots), not in
-// a VGPR held across the path loop.  Round 6: neutral on C2 / C3 / C4, book2 -0.4% and random spheres
-// -1.5% (the word comes out of the treelet's LDS), and the exact interpreter at 5 waves keeps 7 of its
-// 8 spilled VGPRs (profiles/r06_ab.txt section 5): off
-#ifndef MRT_LDS_RAYS
-#define MRT_LDS_RAYS 0u
-#endif
 template <uint32_t F> struct PathQ {
     static constexpr bool on = MRT_PATHQ && (F & FT_MESH) == 0 && !TreeOf<F>::on;
     // LDS words per lane slot: o, dir, time, PCG state + inc, index (12); + the wave's claim state
@@ -248,7 +244,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
     // per wave: its stacks and queues ([slot][word][lane])
-    const uint32_t words = (P.lds_frames * 2 + P.lds_rays * 11 + P.lds_mesh + P.lds_save + LK * 4 + PathQ<F>::words + MRT_LDS_RAYS) * 64;
+    const uint32_t words = (P.lds_frames * 2 + P.lds_rays * 11 + P.lds_mesh + P.lds_save + LK * 4 + PathQ<F>::words) * 64;
     uint32_t* wb = lds + wave * words;
     uint32_t* const wmesh = wb + P.lds_frames * 128 + P.lds_rays * 704;
     float4* tree = nullptr;
@@ -335,16 +331,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
         in_tail = ((w >> 16) & 1u) != 0;
     };
     if constexpr (PathQ<F>::on) cold_store();
-#if MRT_LDS_RAYS
-    // each lane's count of the rays its finished paths traced, in the last LDS word of the wave's
-    // slots (ds_add at a path's end) instead of a register held across the path loop
-    uint32_t* const Lrays = wb + words - 64u + lane;
-    *Lrays = 0u;
-#define MRT_COUNT_RAYS(n) __hip_atomic_fetch_add(Lrays, (n), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
-#else
     uint32_t done_rays = 0;
-#define MRT_COUNT_RAYS(n) (done_rays += (n))
-#endif
     PhaseClock ph{};
 #ifdef MRT_PHASES
     ph.t = __builtin_amdgcn_s_memtime();
@@ -463,7 +450,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
         }
 #endif
         if (P.path_rays) P.path_rays[idx] = ps.rays();
-        MRT_COUNT_RAYS(ps.rays());
+        done_rays += ps.rays();
         active = false;
     };
     // mesh variants keep one constructor per branch: the shared-constructor loop spills there
@@ -513,7 +500,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                     st_off = idx * 12u;
                     st_pend = true;
                     if (P.path_rays) P.path_rays[idx] = ps.rays();
-                    MRT_COUNT_RAYS(ps.rays());
+                    done_rays += ps.rays();
                     active = false;
                 } else {
                     want_ray = true;
@@ -680,7 +667,10 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
 #if MRT_MESH_SPEC
                     // the wave's choice: a leaf step once enough runs are parked or no inner step is left
                     const bool can_inner = phase == PH_WALK && ref != kMeshEnd && !((ref & MESH_LEAF) && pref != 0u);
-                    const bool leaf_iter = (uint32_t)__popcll(__ballot(phase == PH_WALK && pref != 0u)) >= MRT_SPEC_LEAF || !__any(can_inner);
+                    // (MRT_SPEC_LEAF 0: a leaf step when at least as many lanes can take one as an inner step)
+                    const uint32_t n_leaf = (uint32_t)__popcll(__ballot(phase == PH_WALK && pref != 0u));
+                    const uint32_t n_inner = (uint32_t)__popcll(__ballot(can_inner));
+                    const bool leaf_iter = MRT_SPEC_LEAF ? (n_leaf >= MRT_SPEC_LEAF || n_inner == 0u) : n_leaf >= n_inner;
                     if (phase == PH_WALK) {
                         const uint32_t st = mesh_step_spec<false>(S, ps.r, 0.001f, w.closest, rec, Ls, ref, pref, msp, w.hdone, leaf_iter);
                         if (st == 1u) w.hnode = kMeshPC;  // w.closest = the hit's t, w.hdone set
@@ -761,11 +751,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
     }
 #endif
     // one 64-bit add per wave
-#if MRT_LDS_RAYS
-    uint64_t my = *Lrays;
-#else
     uint64_t my = done_rays;
-#endif
     for (int off = 32; off > 0; off >>= 1) my += __shfl_xor(my, off);
     if (lane == 0 && my) atomicAdd(P.rays, (unsigned long long)my);
 }
@@ -851,8 +837,7 @@ static KernelTable make_table(const char* numerics, std::index_sequence<I...>) {
                        {PathQ<kVariants[I]>::words...},
                        {kBox6Walk<kVariants[I]>...},
                        {(uint32_t)(kLinSlabOps<kVariants[I]> && MRT_SIG_OF(kVariants[I]) == SIG_NONE)...},
-                       {kfn_retrace<kVariants[I]>()...},
-                       {(uint32_t)(MRT_LDS_RAYS + 0u * kVariants[I])...}};
+                       {kfn_retrace<kVariants[I]>()...}};
 }
 #if MRT_TABLE_PEX
 const KernelTable& mrtd::kernel_table_fast_pex() {

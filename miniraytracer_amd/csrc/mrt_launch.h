@@ -132,7 +132,6 @@ struct KernelTable {
     // the path-exact build's retrace kernel for the tolerance variants that hand rounding-critical
     // paths over (mrt_shade.h light_critical): launched over PathParams::rt after each path kernel
     path_kernel_t retrace[kNumVariants];
-    uint32_t lds_rays[kNumVariants];  // LDS words per lane slot of the per-lane ray count (mrt_kernels.hip MRT_LDS_RAYS)
 };
 const KernelTable& kernel_table_exact();
 const KernelTable& kernel_table_fast();

@@ -51,7 +51,6 @@ static void take_variant(KernelTable& m, const KernelTable& s, uint32_t i) {
     m.pq[i] = s.pq[i];
     m.box6_walk[i] = s.box6_walk[i];
     m.rewrite[i] = s.rewrite[i];
-    m.lds_rays[i] = s.lds_rays[i];
 }
 static const KernelTable& fast_table() {
     static const KernelTable t = [] {
@@ -324,9 +323,6 @@ struct PathLaunch {
     path_kernel_t retrace = nullptr;  // the exact arithmetic for its rounding-critical paths (mrt_retrace_kernel)
     size_t retrace_lds = 0;
     bool handover = false;  // the kernel hands its rounding-critical paths to it (fast arithmetic)
-    // the retrace kernel's waves fit a path-kernel wave's registers (1-wave path groups): under the
-    // async fold it may run on the fold stream in slots the next launch leaves free (kRetraceSide)
-    bool retrace_side = false;
     uint32_t walk_min = 32;  // resumable mesh walk threshold of this build (PathParams::walk_min)
 };
 
@@ -1064,13 +1060,6 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
             L.handover = k == 1 && L.retrace && L.fn != kernel_table_fast_pex().kernel[s->variant] && !(e && *e && atoi(e) == 0);
         }
         L.retrace_lds = (size_t)64 * 4 * (s->lds_frames * 2 + s->lds_rays * 11 + s->lds_mesh + s->lds_save);
-        if (L.handover) {
-            hipFuncAttributes ra{};
-            HIPCHK(hipFuncGetAttributes(&ra, reinterpret_cast<const void*>(L.retrace)));
-            hipFuncAttributes pa{};
-            HIPCHK(hipFuncGetAttributes(&pa, reinterpret_cast<const void*>(L.fn)));
-            L.retrace_side = L.wg == 64u && ((ra.numRegs + 7) & ~7) <= ((pa.numRegs + 7) & ~7);
-        }
         // the path-exact build (the metal bunny under the tolerance contract) yields at 32 walking
         // lanes: 40 -1.2%, 28 -1.7%, 48 -10% (bunny 1024x1024x64, profiles/r04_ab.txt section 13)
         L.walk_min = (!walk_min_env && L.fn == kernel_table_fast_pex().kernel[s->variant]) ? 32u : s->walk_min;
@@ -1081,7 +1070,7 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
         auto groups = [&](size_t lds) { return std::max(1, lds ? std::min<int>(nb_vgpr, (int)((160u * 1024u) / lds)) : nb_vgpr); };
         const size_t lds_core = (size_t)waves_per_wg * 64 * 4 *
                                 (s->lds_frames * 2 + s->lds_rays * 11 + L.lds_mesh + L.lds_save + tabs[k]->lev_k[s->variant] * 4 +
-                                 tabs[k]->pq[s->variant] + tabs[k]->lds_rays[s->variant]);
+                                 tabs[k]->pq[s->variant]);
         L.lds_bytes = lds_core;
         if (L.lds_bytes > (size_t)prop.sharedMemPerBlock) {
             mrt_scene_free(s);
@@ -1185,16 +1174,10 @@ static constexpr uint32_t kRtCap = 1u << 20;
 // one-wave groups of the retrace kernel: 16384 lanes, a path each (more loop); its time is the longest
 // listed path's, plus the launch
 static constexpr uint32_t kRetraceGroups = 256;
-// A/B hook (round 6, off): under MRT_RF_FOLD_ASYNC each launch's retrace on the context's fold stream,
-// beside the next launch's path kernel, in kRetraceSide one-wave groups that the next path kernel
-// leaves free (it is launched with that many fewer one-wave groups; each radiance parity has its own
-// list).  On the render's stream the GPU idles for the retrace's longest path (~0.1 ms per launch) --
-// but the previous launch's fold fills that gap: moved beside the next kernel, the retrace delays the
-// fold behind it on the fold stream (which then has only the free slots), and the launch after next
-// waits for that fold: C2 8.66-8.72 against 8.27 ms per step, the 8-rank share 1.102-1.104 against
-// 1.109-1.130 ms (two contexts) (profiles/r06_ab.txt sections 2 and 7; without the free slots the
-// retrace waited for the next kernel's end: 8.61-8.72 ms).  MRT_RETRACE_SIDE=<groups> turns it on.
-static constexpr uint32_t kRetraceSide = 0;
+// (Round 6: the retrace of an MRT_RF_FOLD_ASYNC launch beside the next launch's path kernel -- on the
+// context's fold stream, and there in one-wave slots the next kernel left free -- measured slower:
+// the previous launch's fold uses the GPU during the retrace's gap on the render's stream, and behind
+// the retrace on the fold stream it got only the free slots, profiles/r06_ab.txt sections 2 and 7.)
 
 #define MRT_GPU_ONLY(s, what) \
     if ((s) && (s)->cpu) return mrt_internal_fail(MRT_ERR_INVALID, what " is a GPU-backend entry point (scene on MRT_DEVICE_CPU)")
@@ -1253,7 +1236,7 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
         for (hipEvent_t& e : s->ev_fold)
             if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
-    // (two lists: one per radiance parity, for the async fold's retrace beside the next launch)
+    // (two lists: one per radiance parity of the async fold)
     if ((d->flags & MRT_RF_FAST) && !(d->flags & MRT_RF_PATH_DEBUG) && s->pl[1].handover &&
         (st = grow(s, (void**)&s->d_rt, &s->rt_cap, (size_t)2 * kRtCap * sizeof(uint32_t))))
         return st;
@@ -1385,13 +1368,9 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         s->prev_epoch++;
     }
     // the rounding-critical paths' hand-over: tolerance contract, not the per-path debug output
-    // (whose radiance is the fast kernel's own); under the async fold its retrace beside the next
-    // launch (kRetraceSide) where its waves fit the path kernel's slots
+    // (whose radiance is the fast kernel's own)
     const bool handover = PL.handover && !(d->flags & MRT_RF_PATH_DEBUG);
-    uint32_t side = (handover && async && PL.retrace_side) ? kRetraceSide : 0u;
-    if (const char* e = getenv("MRT_RETRACE_SIDE"))  // A/B hook
-        if (*e && handover && async && PL.retrace_side) side = (uint32_t)atoi(e);
-    const int grid = PL.grid - (int)std::min<uint32_t>(side, (uint32_t)PL.grid / 2u);  // one-wave groups: its waves' slots left free
+    const int grid = PL.grid;
     for (uint32_t s0 = 0; s0 < ns; s0 += s->chunk) {
         uint32_t s1 = std::min(ns, s0 + s->chunk);
         const uint32_t par = async ? s->lpar : 0u;
@@ -1458,19 +1437,15 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         // this launch's rounding-critical paths, exact, into the radiance buffer before its fold (the
         // exact arithmetic walks the program as compiled: the tolerance contract's rewrite has ops -- a
         // room's slab test, one-step box instances -- only the fast builds compile)
-        PathParams PR = P;
-        PR.sc.prog = s->S.prog;
-        if (handover && !side) {  // on the render's stream, the whole GPU
+        if (handover) {
+            PathParams PR = P;
+            PR.sc.prog = s->S.prog;
             hipLaunchKernelGGL(PL.retrace, dim3(kRetraceGroups), dim3(64), PL.retrace_lds, q, PR);
             HIPCHK(hipGetLastError());
         }
-        if (async) {  // (the retrace and) the fold on the fold stream, beside the next launch's path kernel
+        if (async) {  // the fold on the fold stream, beside the next launch's path kernel
             HIPCHK(hipEventRecord(s->ev_kern, q));
             HIPCHK(hipStreamWaitEvent(s->fstream, s->ev_kern, 0));
-        }
-        if (handover && side) {  // in the slots the next path kernel leaves free (kRetraceSide)
-            hipLaunchKernelGGL(PL.retrace, dim3(side), dim3(64), PL.retrace_lds, s->fstream, PR);
-            HIPCHK(hipGetLastError());
         }
         if (async) {  // the fold beside the next launch's path kernel
             const bool last = s1 == ns;

@@ -515,12 +515,6 @@ MRT_DFN bool mesh_hit(const DScene& S, const mrt_node& n, const Ray& r, float tm
 #endif
 }
 
-// The resumable mesh walk's stack push / pop as selects on every lane instead of divergent
-// branches around the LDS store and load (round 6, VERDICT r05 item 5: the step's exec-mask
-// bookkeeping).  Same nodes, same order, same bits.
-#ifndef MRT_MESH_BF
-#define MRT_MESH_BF 0
-#endif
 // One step of mesh_hit's walk for a lane whose state persists between calls (ref, msp and its LDS
 // stack; inside a leaf: the triangles left in ref, the leaf's running closest in tt, the best
 // triangle so far in rec.mat / rec.u / rec.v, `in_hit` set once one hit).  A step is an inner
@@ -560,30 +554,14 @@ MRT_DFN uint32_t mesh_step(const DScene& S, const mrt_node& n, const Ray& r, flo
             const bool left_first = (W.order & r.mask) != 0;
             const uint32_t cref = left_first ? W.lref : W.rref, fref = left_first ? W.rref : W.lref;
             const bool hc = left_first ? hl : hr, hf = left_first ? hr : hl;
-#if MRT_MESH_BF
-            // branch-free push: the far child is stored at the free slot msp on every lane and kept
-            // only where both boxes were hit (slot msp <= the node's level < the stack's depth bound)
-            L.mesh[msp * 64 + L.lane] = fref;
-            msp += (hc && hf) ? 1u : 0u;
-#else
             if (hc && hf) L.mesh[(msp++) * 64 + L.lane] = fref;
-#endif
             ref = hc ? cref : (hf ? fref : ref);
             pop = !hc && !hf;
         }
-#if MRT_MESH_BF
-        // branch-free pop: the top slot read on every lane (slot 0 when the stack is empty), the
-        // walk state updated by selects
-        const uint32_t top = L.mesh[(msp == 0u ? 0u : msp - 1u) * 64 + L.lane];
-        res = (pop && msp == 0u) ? 2u : res;
-        ref = (pop && msp != 0u) ? top : ref;
-        msp -= (pop && msp != 0u) ? 1u : 0u;
-#else
         if (pop) {
             if (msp == 0) res = 2u;
             else ref = L.mesh[(--msp) * 64 + L.lane];
         }
-#endif
         return res;
     }
     if (ref & MESH_LEAF) {
@@ -839,9 +817,6 @@ MRT_DFN void bvhw_leaf_rec(const DScene& S, uint32_t prim, const Ray& r, float t
     (void)again;
 }
 
-#ifndef MRT_BVHW_BF
-#define MRT_BVHW_BF 0
-#endif
 // bvh_node::hit (scene_object.h:208-244) over wide nodes: the root's own box, then depth-first,
 // closer child first (node_order & dirMask), the first child subtree that hits ends the walk.
 // A child's box is tested at its parent with the (tmin, tmax) the reference uses when it visits
@@ -867,24 +842,12 @@ MRT_DFN bool bvhw_hit(const DScene& S, const mrt_node& n, const Ray& r, float tm
             const bool left_first = (W.order & r.mask) != 0;
             const uint32_t cref = left_first ? W.lref : W.rref, fref = left_first ? W.rref : W.lref;
             const bool hc = left_first ? hl : hr, hf = left_first ? hr : hl;
-#if MRT_BVHW_BF
-            // branch-free push / pop (as mesh_step, MRT_MESH_BF): the far child stored at the free slot
-            // sp on every lane, kept where both boxes were hit; the top slot read on every lane
-            L.mesh[sp * 64 + L.lane] = fref;
-            sp += (hc && hf && fref != cref) ? 1u : 0u;  // n == 1: left == right, a repeat misses again
-            const bool pop = !hc && !hf;
-            if (pop && sp == 0) return false;
-            const uint32_t top = L.mesh[(sp == 0u ? 0u : sp - 1u) * 64 + L.lane];
-            ref = pop ? top : (hc ? cref : fref);
-            sp -= pop ? 1u : 0u;
-#else
             if (hc && hf && fref != cref) L.mesh[(sp++) * 64 + L.lane] = fref;  // n == 1: left == right, a repeat misses again
             ref = hc ? cref : fref;
             if (!hc && !hf) {
                 if (sp == 0) return false;
                 ref = L.mesh[(--sp) * 64 + L.lane];
             }
-#endif
         }
         if (bvhw_leaf<F>(S, ref, r, tmin, tmax, rec, full)) return true;
         if (sp == 0) return false;

@@ -866,16 +866,13 @@ def test_rounding_critical_paths_retraced_exactly(gpu, monkeypatch, walk):
     assert err_a < err_b
 
 
-@pytest.mark.parametrize("side", ["32", "0"])
-def test_async_retrace_beside_next_launch(gpu, monkeypatch, side):
-    """Under MRT_RF_FOLD_ASYNC each launch's rounding-critical paths are retraced on the render's
-    stream (MRT_RETRACE_SIDE=0, the default) or, as an A/B hook, on the context's fold stream beside
-    the next launch's path kernel, in one-wave slots that kernel leaves free (mrt_render.hip
-    kRetraceSide; each radiance parity with its own list).  Back-to-back async renders of a C2 size
-    that lists a few hundred paths per launch (three launches per render: both lists in use) equal
-    the blocking render bit for bit, with the same count of handed-over paths per render."""
+def test_async_retrace_lists_per_parity(gpu):
+    """Under MRT_RF_FOLD_ASYNC each radiance parity has its own list of rounding-critical paths, which
+    the launch's retrace (the exact arithmetic) empties before the launch's fold.  Back-to-back async
+    renders of a C2 size that lists a few hundred paths per launch (three launches per render: both
+    lists in use) equal the blocking render bit for bit, with the same count of handed-over paths per
+    render."""
     import torch
-    monkeypatch.setenv("MRT_RETRACE_SIDE", side)
     w, h, spp = 250, 250, 192
     sc = gpu.select_scene(5, 1.0)
     r0 = gpu.Renderer(sc, 0)
