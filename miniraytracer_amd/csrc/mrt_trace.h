@@ -827,7 +827,9 @@ MRT_DFN bool bvhw_hit(const DScene& S, const mrt_node& n, const Ray& r, float tm
                                          const LStack& L) {
     if (!aabb_hit(n.f, n.f + 3, r, tmin, tmax)) return false;
     uint32_t ref = n.a, sp = 0;
-#ifndef MRT_IFIF
+    // (Leaf postponing by majority -- a lane parks its first leaf and walks on, as the path-exact
+    // mesh walk does -- measured and removed: scene 2 +7.3%, random spheres +0.5% / -2.1% exact,
+    // scenes 1 / 3 / 4 -3.2% / -1% / -1%, book2 -5.7%, profiles/r06_ab.txt section 17.)
     // "while-while" (Aila & Laine 2009): each lane descends through inner nodes until it holds a
     // leaf, and the leaves are tested together, instead of one inner-or-leaf step per iteration
     // with the two branches serialised whenever lanes disagree (book2, C5: +14%).  Each lane
@@ -853,31 +855,6 @@ MRT_DFN bool bvhw_hit(const DScene& S, const mrt_node& n, const Ray& r, float tm
         if (sp == 0) return false;
         ref = L.mesh[(--sp) * 64 + L.lane];
     }
-#else
-    for (;;) {
-        if (ref & BVHW_LEAF) {
-            if (bvhw_leaf<F>(S, ref, r, tmin, tmax, rec, full)) return true;
-        } else {
-            const WideNode W = wide_at<TreeOf<F>::on>(S.bwide, ref, L);
-            const bool hl = !(W.flags & 1u) || aabb_hit(W.lmin, W.lmax, r, tmin, tmax);
-            const bool hr = !(W.flags & 2u) || aabb_hit(W.rmin, W.rmax, r, tmin, tmax);
-            const bool left_first = (W.order & r.mask) != 0;
-            const uint32_t cref = left_first ? W.lref : W.rref, fref = left_first ? W.rref : W.lref;
-            const bool hc = left_first ? hl : hr, hf = left_first ? hr : hl;
-            if (hc) {
-                if (hf && fref != cref) L.mesh[(sp++) * 64 + L.lane] = fref;  // n == 1: left == right, a repeat misses again
-                ref = cref;
-                continue;
-            }
-            if (hf) {
-                ref = fref;
-                continue;
-            }
-        }
-        if (sp == 0) return false;
-        ref = L.mesh[(--sp) * 64 + L.lane];
-    }
-#endif
 }
 
 template <uint32_t F>
