@@ -187,6 +187,20 @@ MRT_DFN bool any_lane(bool p) {
     return p;
 #endif
 }
+// a ? b : c for lane booleans as lane-mask logic (SALU and / andn2 / or on the wave's masks): the
+// compiler's select of two booleans materialised each as 0 / 1 in a VGPR and compared it back
+// (4-6 VALU per BVH child pair).  MRT_SEL_MASK 0: the plain select (A/B hook).
+#ifndef MRT_SEL_MASK
+#define MRT_SEL_MASK 1
+#endif
+MRT_DFN bool sel_b(bool a, bool b, bool c) {
+#if defined(__HIP_DEVICE_COMPILE__) && MRT_SEL_MASK
+    const uint64_t ma = __builtin_amdgcn_ballot_w64(a), mb = __builtin_amdgcn_ballot_w64(b), mc = __builtin_amdgcn_ballot_w64(c);
+    return __builtin_amdgcn_inverse_ballot_w64((ma & mb) | (~ma & mc));
+#else
+    return a ? b : c;
+#endif
+}
 // |x| as an unsigned key (sign shifted out): 2^e -> (e + 127) << 24, 0 -> 0, inf/NaN above all finite
 MRT_DFN uint32_t mag2(float x) { return __float_as_uint(x) << 1; }
 #define MRT_MAG2(e) ((uint32_t)((e) + 127) << 24)
@@ -438,8 +452,9 @@ MRT_DFN float sel3(uint32_t a, float x, float y, float z) {
 }
 MRT_DFN f3 eval(const Ray& r, float t) { return add(r.o, fmul(t, r.d)); }
 
-// aabb::hit, active SSE branch (aabb.h:49-76)
-MRT_DFN bool aabb_hit(const float* bmin, const float* bmax, const Ray& r, float tmin, float tmax) {
+// aabb::hit, active SSE branch (aabb.h:49-76).  `bad`: some lane of the wave may hold a ray that is
+// not nice (wave-uniform; a walk computes it once for all its box tests instead of per test)
+MRT_DFN bool aabb_hit_b(const float* bmin, const float* bmax, const Ray& r, float tmin, float tmax, bool bad) {
 #if MRT_FAST_SLAB
     // tolerance contract: (b - o) * inv as fma(b, inv, -(o * inv)); the products o * inv are shared
     // by every box a walk step tests with the same ray (one multiply-add per slab instead of two)
@@ -456,17 +471,26 @@ MRT_DFN bool aabb_hit(const float* bmin, const float* bmax, const Ray& r, float 
     // the zero signs min/max may pick do not matter.
     float lo = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0z, t1z)), fmaxf(fminf(t0y, t1y), tmin));
     float hi = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0z, t1z)), fminf(fmaxf(t0y, t1y), tmax));
-    bool h = hi > lo;
-    if (__builtin_expect(any_lane(!r.nice), 0)) {
+    if (__builtin_expect(bad, 0)) {
         bool lx = r.inv.x < 0.0f, ly = r.inv.y < 0.0f, lz = r.inv.z < 0.0f;
         float ax = lx ? t1x : t0x, bx = lx ? t0x : t1x;
         float ay = ly ? t1y : t0y, by = ly ? t0y : t1y;
         float az = lz ? t1z : t0z, bz = lz ? t0z : t1z;
         float lo2 = maxps(maxps(ax, az), maxps(ay, tmin));
         float hi2 = minps(minps(bx, bz), minps(by, tmax));
-        h = r.nice ? h : hi2 > lo2;
+        // (the bounds merged, one comparison after the branch: a merged boolean cost two VALU
+        // copies per test)
+        lo = r.nice ? lo : lo2;
+        hi = r.nice ? hi : hi2;
     }
-    return h;
+    return hi > lo;
+}
+MRT_DFN bool aabb_hit(const float* bmin, const float* bmax, const Ray& r, float tmin, float tmax) {
+    return aabb_hit_b(bmin, bmax, r, tmin, tmax, any_lane(!r.nice));
+}
+MRT_DFN bool aabb_hit_b(f3 bmin, f3 bmax, const Ray& r, float tmin, float tmax, bool bad) {
+    const float b[6] = {bmin.x, bmin.y, bmin.z, bmax.x, bmax.y, bmax.z};
+    return aabb_hit_b(b, b + 3, r, tmin, tmax, bad);
 }
 
 MRT_DFN bool aabb_hit(f3 bmin, f3 bmax, const Ray& r, float tmin, float tmax) {

@@ -662,6 +662,8 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
             // at least one step per iteration for every walking lane (no lane starves), then more
             // while enough lanes walk or too few have anything else to do
             while (__any(phase == PH_WALK)) {
+                // some walking lane's ray is not nice (the box tests' slow path; wave-uniform)
+                const bool bad = any_lane(phase == PH_WALK && !ps.r.nice);
 #pragma unroll
                 for (int u = 0; u < MRT_WALK_UNROLL; u++) {  // (A/B hook: steps between two yield checks)
 #if MRT_MESH_SPEC
@@ -672,14 +674,14 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                     const uint32_t n_inner = (uint32_t)__popcll(__ballot(can_inner));
                     const bool leaf_iter = MRT_SPEC_LEAF ? (n_leaf >= MRT_SPEC_LEAF || n_inner == 0u) : n_leaf >= n_inner;
                     if (phase == PH_WALK) {
-                        const uint32_t st = mesh_step_spec<false>(S, ps.r, 0.001f, w.closest, rec, Ls, ref, pref, msp, w.hdone, leaf_iter);
+                        const uint32_t st = mesh_step_spec<false>(S, ps.r, 0.001f, w.closest, rec, Ls, ref, pref, msp, w.hdone, leaf_iter, bad);
                         if (st == 1u) w.hnode = kMeshPC;  // w.closest = the hit's t, w.hdone set
                         phase = st != 0u ? PH_DONE : PH_WALK;
                     }
 #else
                     if (phase == PH_WALK) {
                         const mrt_node mn = ld_node(const_ptr(S.nodes) + prog[kMeshPC].node);
-                        const uint32_t st = mesh_step<false, true>(S, mn, ps.r, 0.001f, w.closest, rec, Ls, ref, msp, w.hdone);
+                        const uint32_t st = mesh_step<false, true>(S, mn, ps.r, 0.001f, w.closest, rec, Ls, ref, msp, w.hdone, bad);
                         if (st == 1u) w.hnode = kMeshPC;  // w.closest = the hit's t, w.hdone set
                         phase = st != 0u ? PH_DONE : PH_WALK;
                     }

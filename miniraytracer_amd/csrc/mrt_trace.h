@@ -255,6 +255,9 @@ MRT_DFN WideNode load_wide_lds(const float4* tree, uint32_t ref) {
     n.flags = __float_as_uint(d.w);
     return n;
 }
+#ifndef MRT_WIDE_OFF32
+#define MRT_WIDE_OFF32 1  // (C4 +3.7% with the mask-logic selects, +1.6% alone; profiles/r06_ab.txt section 21)
+#endif
 // wide node `ref` of a BvhWide / MeshWide array: from the LDS treelet when it holds it
 template <bool TREE, typename W>
 MRT_DFN WideNode wide_at(const W* base, uint32_t ref, const LStack& L) {
@@ -269,7 +272,13 @@ MRT_DFN WideNode wide_at(const W* base, uint32_t ref, const LStack& L) {
 #endif
     } else {
         (void)L;
+#if MRT_WIDE_OFF32
+        // the node's byte offset as 32 bits (refs < 2^24): a scalar base plus a per-lane 32-bit
+        // offset, one shift per visit instead of a 64-bit shift and add
+        return load_wide(reinterpret_cast<const W*>(reinterpret_cast<const char*>(base) + (size_t)(ref * 64u)));
+#else
         return load_wide(base + ref);
+#endif
     }
 }
 
@@ -463,17 +472,18 @@ MRT_DFN bool mesh_hit(const DScene& S, const mrt_node& n, const Ray& r, float tm
         if (!aabb_hit(root.bmin, root.bmax, r, tmin, tmax)) return false;
     }
     uint32_t ref = n.b, msp = 0;
+    const bool bad = any_lane(!r.nice);  // (once per walk: aabb_hit_b)
 #ifdef MRT_MESH_WW
     // "while-while" (Aila & Laine 2009), as bvhw_hit: measured 20% slower on the bunny (C4) and 1%
     // on the teapot (C3) than the one-step-per-iteration walk below, so kept as an experiment.
     for (;;) {
         while (!(ref & MESH_LEAF)) {
             const WideNode W = mesh_wide<false>(S, ref, L);
-            const bool hl = aabb_hit(W.lmin, W.lmax, r, tmin, tmax);
-            const bool hr = aabb_hit(W.rmin, W.rmax, r, tmin, tmax);
+            const bool hl = aabb_hit_b(W.lmin, W.lmax, r, tmin, tmax, bad);
+            const bool hr = aabb_hit_b(W.rmin, W.rmax, r, tmin, tmax, bad);
             const bool left_first = (W.order & r.mask) != 0;
             const uint32_t cref = left_first ? W.lref : W.rref, fref = left_first ? W.rref : W.lref;
-            const bool hc = left_first ? hl : hr, hf = left_first ? hr : hl;
+            const bool hc = sel_b(left_first, hl, hr), hf = sel_b(left_first, hr, hl);
             if (hc) {
                 if (hf) L.mesh[(msp++) * 64 + L.lane] = fref;
                 ref = cref;
@@ -494,11 +504,11 @@ MRT_DFN bool mesh_hit(const DScene& S, const mrt_node& n, const Ray& r, float tm
             if (mesh_leaf(S, ref, n, r, tmin, tmax, rec, full)) return true;
         } else {
             const WideNode W = mesh_wide<false>(S, ref, L);
-            const bool hl = aabb_hit(W.lmin, W.lmax, r, tmin, tmax);
-            const bool hr = aabb_hit(W.rmin, W.rmax, r, tmin, tmax);
+            const bool hl = aabb_hit_b(W.lmin, W.lmax, r, tmin, tmax, bad);
+            const bool hr = aabb_hit_b(W.rmin, W.rmax, r, tmin, tmax, bad);
             const bool left_first = (W.order & r.mask) != 0;
             const uint32_t cref = left_first ? W.lref : W.rref, fref = left_first ? W.rref : W.lref;
-            const bool hc = left_first ? hl : hr, hf = left_first ? hr : hl;
+            const bool hc = sel_b(left_first, hl, hr), hf = sel_b(left_first, hr, hl);
             if (hc) {
                 if (hf) L.mesh[(msp++) * 64 + L.lane] = fref;
                 ref = cref;
@@ -528,7 +538,7 @@ MRT_DFN bool mesh_hit(const DScene& S, const mrt_node& n, const Ray& r, float tm
 // in and out of each step's branches).
 template <bool TREE = false, bool DEFER = false>
 MRT_DFN uint32_t mesh_step(const DScene& S, const mrt_node& n, const Ray& r, float tmin, float& tt, HitRec& rec,
-                                              const LStack& L, uint32_t& ref, uint32_t& msp, bool& in_hit) {
+                                              const LStack& L, uint32_t& ref, uint32_t& msp, bool& in_hit, bool bad) {
     if constexpr (DEFER) {
         // the same step with the walk state updated by selects where mesh_step branches and
         // returns: each branch's results otherwise merged in copies of every state register
@@ -549,11 +559,11 @@ MRT_DFN uint32_t mesh_step(const DScene& S, const mrt_node& n, const Ray& r, flo
             pop = !more && !in_hit;
         } else {
             const WideNode W = mesh_wide<TREE>(S, ref, L);
-            const bool hl = aabb_hit(W.lmin, W.lmax, r, tmin, tt);
-            const bool hr = aabb_hit(W.rmin, W.rmax, r, tmin, tt);
+            const bool hl = aabb_hit_b(W.lmin, W.lmax, r, tmin, tt, bad);
+            const bool hr = aabb_hit_b(W.rmin, W.rmax, r, tmin, tt, bad);
             const bool left_first = (W.order & r.mask) != 0;
             const uint32_t cref = left_first ? W.lref : W.rref, fref = left_first ? W.rref : W.lref;
-            const bool hc = left_first ? hl : hr, hf = left_first ? hr : hl;
+            const bool hc = sel_b(left_first, hl, hr), hf = sel_b(left_first, hr, hl);
             if (hc && hf) L.mesh[(msp++) * 64 + L.lane] = fref;
             ref = hc ? cref : (hf ? fref : ref);
             pop = !hc && !hf;
@@ -591,11 +601,11 @@ MRT_DFN uint32_t mesh_step(const DScene& S, const mrt_node& n, const Ray& r, flo
         }
     } else {
         const WideNode W = mesh_wide<TREE>(S, ref, L);
-        const bool hl = aabb_hit(W.lmin, W.lmax, r, tmin, tt);
-        const bool hr = aabb_hit(W.rmin, W.rmax, r, tmin, tt);
+        const bool hl = aabb_hit_b(W.lmin, W.lmax, r, tmin, tt, bad);
+        const bool hr = aabb_hit_b(W.rmin, W.rmax, r, tmin, tt, bad);
         const bool left_first = (W.order & r.mask) != 0;
         const uint32_t cref = left_first ? W.lref : W.rref, fref = left_first ? W.rref : W.lref;
-        const bool hc = left_first ? hl : hr, hf = left_first ? hr : hl;
+        const bool hc = sel_b(left_first, hl, hr), hf = sel_b(left_first, hr, hl);
         if (hc) {
             if (hf) L.mesh[(msp++) * 64 + L.lane] = fref;
             ref = cref;
@@ -621,7 +631,7 @@ MRT_DFN uint32_t mesh_step(const DScene& S, const mrt_node& n, const Ray& r, flo
 static constexpr uint32_t kMeshEnd = 0xFFFFFFFFu;
 template <bool TREE = false>
 MRT_DFN uint32_t mesh_step_spec(const DScene& S, const Ray& r, float tmin, float& tt, HitRec& rec, const LStack& L, uint32_t& ref,
-                                uint32_t& pref, uint32_t& msp, bool& in_hit, bool leaf_iter) {
+                                uint32_t& pref, uint32_t& msp, bool& in_hit, bool leaf_iter, bool bad) {
     uint32_t res = 0u;
     if (leaf_iter) {  // one triangle of the parked run (mesh_step's leaf step)
         if (pref != 0u) {
@@ -647,11 +657,11 @@ MRT_DFN uint32_t mesh_step_spec(const DScene& S, const Ray& r, float tmin, float
         return 0u;
     }
     const WideNode W = mesh_wide<TREE>(S, ref, L);
-    const bool hl = aabb_hit(W.lmin, W.lmax, r, tmin, tt);
-    const bool hr = aabb_hit(W.rmin, W.rmax, r, tmin, tt);
+    const bool hl = aabb_hit_b(W.lmin, W.lmax, r, tmin, tt, bad);
+    const bool hr = aabb_hit_b(W.rmin, W.rmax, r, tmin, tt, bad);
     const bool left_first = (W.order & r.mask) != 0;
     const uint32_t cref = left_first ? W.lref : W.rref, fref = left_first ? W.rref : W.lref;
-    const bool hc = left_first ? hl : hr, hf = left_first ? hr : hl;
+    const bool hc = sel_b(left_first, hl, hr), hf = sel_b(left_first, hr, hl);
     if (hc && hf) L.mesh[(msp++) * 64 + L.lane] = fref;
     ref = hc ? cref : (hf ? fref : ref);
     if (!hc && !hf) {
@@ -827,6 +837,7 @@ MRT_DFN bool bvhw_hit(const DScene& S, const mrt_node& n, const Ray& r, float tm
                                          const LStack& L) {
     if (!aabb_hit(n.f, n.f + 3, r, tmin, tmax)) return false;
     uint32_t ref = n.a, sp = 0;
+    const bool bad = any_lane(!r.nice);  // (once per walk: aabb_hit_b)
     // (Leaf postponing by majority -- a lane parks its first leaf and walks on, as the path-exact
     // mesh walk does -- measured and removed: scene 2 +7.3%, random spheres +0.5% / -2.1% exact,
     // scenes 1 / 3 / 4 -3.2% / -1% / -1%, book2 -5.7%, profiles/r06_ab.txt section 17.)
@@ -839,11 +850,11 @@ MRT_DFN bool bvhw_hit(const DScene& S, const mrt_node& n, const Ray& r, float tm
             const WideNode W = wide_at<TreeOf<F>::on>(S.bwide, ref, L);
             // (both boxes tested on every lane, `|` rather than `||`: a box-less slot's test is
             // ignored, and the walk keeps no branch around each test)
-            const bool hl = !(W.flags & 1u) | aabb_hit(W.lmin, W.lmax, r, tmin, tmax);
-            const bool hr = !(W.flags & 2u) | aabb_hit(W.rmin, W.rmax, r, tmin, tmax);
+            const bool hl = !(W.flags & 1u) | aabb_hit_b(W.lmin, W.lmax, r, tmin, tmax, bad);
+            const bool hr = !(W.flags & 2u) | aabb_hit_b(W.rmin, W.rmax, r, tmin, tmax, bad);
             const bool left_first = (W.order & r.mask) != 0;
             const uint32_t cref = left_first ? W.lref : W.rref, fref = left_first ? W.rref : W.lref;
-            const bool hc = left_first ? hl : hr, hf = left_first ? hr : hl;
+            const bool hc = sel_b(left_first, hl, hr), hf = sel_b(left_first, hr, hl);
             if (hc && hf && fref != cref) L.mesh[(sp++) * 64 + L.lane] = fref;  // n == 1: left == right, a repeat misses again
             ref = hc ? cref : fref;
             if (!hc && !hf) {
