@@ -232,16 +232,6 @@ MRT_DFN const DScene& kernarg_scene() {
 #ifndef MRT_OPAQUE_RESUME
 #define MRT_OPAQUE_RESUME 0  // the same in the room + mesh kernels' resumable loop: measured C3 -0.6%, C4 0 (A/B hook)
 #endif
-// a path-kernel wave is done: the listening retrace (mrt_retrace_listen_kernel) counts the waves
-// that can still list paths.  Release: the wave's list entries and their count come first.
-template <uint32_t F>
-MRT_DFN void rt_wave_done(const PathParams& P, uint32_t lane) {
-    if constexpr (kCrit<F>) {
-        if (lane == 0 && P.rt.fin) __hip_atomic_fetch_add(P.rt.fin, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        (void)P, (void)lane;
-    }
-}
 template <uint32_t F> struct PathQ {
     static constexpr bool on = MRT_PATHQ && (F & FT_MESH) == 0 && !TreeOf<F>::on;
     // LDS words per lane slot: o, dir, time, PCG state + inc, index (12); + the wave's claim state
@@ -280,10 +270,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
 
     // main.cpp:180/235 stop on !G_isRunning: a launch of a cancelled render does no work (mrt_render
     // splits a cancellable render into several launches)
-    if (__hip_atomic_load(P.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
-        rt_wave_done<F>(P, lane);
-        return;
-    }
+    if (__hip_atomic_load(P.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return;
 #if defined(MRT_EXPERIMENTS) && defined(MRT_WTIMES)
     uint64_t wt0 = 0, wt_ex = 0, wt1 = 0, wt_f = 0, wt_aok = 0, wt_afail = 0, wt_n = 0;
     WT_MARK(wt0);
@@ -506,7 +493,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                         dst[2] = st_v.z;
                     }
                     st_pend = false;
-                }, CritSink{&idx, kCritOff<F>});
+                }, CritSink{idx, kCritOff<F>});
                 PH_MARK(ph, 2);
                 if (ended) {
                     st_v = end_path(ps, lev, L);
@@ -713,7 +700,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                     W::template derive<0>(prog, w, ps.r, ps.r, rec);
                 }
                 f3 L{0.0f, 0.0f, 0.0f};
-                const bool ended = shade_hit<F, LK>(S, ps, P.max_bounces, lev, w.hnode != MRT_NONE, rec, &L, ph, CritSink{&idx, kCritOff<F>});
+                const bool ended = shade_hit<F, LK>(S, ps, P.max_bounces, lev, w.hnode != MRT_NONE, rec, &L, ph, CritSink{idx, kCritOff<F>});
                 PH_MARK(ph, 2);
                 phase = PH_BEGIN;
                 if (ended) {
@@ -739,7 +726,7 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
 #endif
             if (active) {
                 f3 L{0.0f, 0.0f, 0.0f};
-                const bool ended = trace_segment<F, LK>(Sseg, ps, P.max_bounces, lev, Ls, &L, ph, CritSink{&idx, kCritOff<F>});
+                const bool ended = trace_segment<F, LK>(Sseg, ps, P.max_bounces, lev, Ls, &L, ph, CritSink{idx, kCritOff<F>});
                 PH_MARK(ph, 2);
                 if (ended) finish_path(L);
             }
@@ -769,7 +756,6 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
     uint64_t my = done_rays;
     for (int off = 32; off > 0; off >>= 1) my += __shfl_xor(my, off);
     if (lane == 0 && my) atomicAdd(P.rays, (unsigned long long)my);
-    rt_wave_done<F>(P, lane);
 }
 
 // The exact arithmetic (the path-exact build: the reference's, forward fold) for the paths a
@@ -782,7 +768,6 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
 template <uint32_t F>
 static constexpr bool kRetrace = MRT_TABLE_PEX && MRT_FWD_FOLD && (F & FT_BIASED) != 0 && !kPathExact<F>;
 #if MRT_TABLE_PEX
-static constexpr uint32_t kRtFree = 0xFFFFFFFFu;  // a free list entry (mrt_retrace_listen_kernel)
 template <uint32_t F>
 __global__ void __launch_bounds__(64) mrt_retrace_kernel(PathParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -799,7 +784,6 @@ __global__ void __launch_bounds__(64) mrt_retrace_kernel(PathParams P) {
     if (blockIdx.x == 0 && lane == 0 && listed > n) atomicAdd(P.rt.lost, (unsigned long long)(listed - n));  // (kept fast)
     for (uint32_t i = blockIdx.x * 64u + lane; i < n; i += gridDim.x * 64u) {
         const uint32_t idx = P.rt.idx[i];
-        P.rt.idx[i] = kRtFree;  // (entries start free: mrt_retrace_listen_kernel)
         uint32_t lp, sl;
         path_coords(P, idx, &lp, &sl);
         PathState ps;
@@ -824,127 +808,10 @@ __global__ void __launch_bounds__(64) mrt_retrace_kernel(PathParams P) {
     }
 }
 #endif
-// The same retrace BESIDE the path kernel ("The listening retrace"): a few
-// one-wave groups launched with the path kernel into slots its grid leaves free take each listed
-// path as soon as the fast kernel lists it, one path per lane, a lane starting its next path when its
-// last ends, so a launch's retrace no longer waits for the path kernel's end and then for its
-// longest listed path.  The fast kernel stores a listed path's own radiance to the trash slot
-// (crit_check), so the exact radiance written here is the only one.  An entry is claimed by one
-// lane (the `taken` counter) and read once the fast kernel has written it (entries start as
-// kRtFree and are freed again when read); the listener ends when every path-kernel wave has ended
-// (`fin`), every entry is taken and no lane holds a path.  (A safety exit after ~10 s without the
-// path kernel's end: a path kernel that never ran must not leave it spinning.)
-#if MRT_TABLE_PEX
-// (at the path kernel's own occupancy: its registers fit the slots the path kernel leaves)
-template <uint32_t F>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MRT_OCC(F)))) mrt_retrace_listen_kernel(PathParams P) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const uint32_t lane = threadIdx.x & 63u;
-    uint32_t* const wb = lds;
-    uint32_t* const wmesh = wb + P.lds_frames * 128 + P.lds_rays * 704;
-    const LStack Ls{wb, (float*)(wb + P.lds_frames * 128), wmesh, (float*)(wmesh + P.lds_mesh * 64), lane, nullptr, 0u};
-    const LevStore<0> lev{nullptr, 0u, 0u, 0u};
-    const DScene& S = P.sc;
-    PhaseClock ph{};
-    auto ld = [](uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-    auto uni = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
-    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-    bool active = false;
-    uint32_t kp = kRtFree;  // a claimed entry not read yet
-    uint32_t idx = 0;
-    PathState ps;
-    f3 L{0.0f, 0.0f, 0.0f};
-    for (;;) {
-        if (kp != kRtFree) {
-            const uint32_t v = ld(P.rt.idx + kp);
-            if (v != kRtFree) {
-                __hip_atomic_store(P.rt.idx + kp, kRtFree, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                kp = kRtFree;
-                idx = v;
-                uint32_t lp, sl;
-                path_coords(P, idx, &lp, &sl);
-                float u, v2;
-                path_key_at(P, lp, P.s0 + sl, ps.rng, &u, &v2);
-                ps.r = camera_ray(S, ps.rng, u, v2);
-                ps.depth = 0;
-                ps.nlev = 0;
-                ps.T = f3{1.0f, 1.0f, 1.0f};
-                L = f3{0.0f, 0.0f, 0.0f};
-                active = true;
-            }
-        }
-        if (active && trace_segment<F, 0>(S, ps, P.max_bounces, lev, Ls, &L, ph)) {
-            L = end_path(ps, lev, L);
-            float* dst = P.rad + (size_t)idx * 3u;
-            dst[0] = L.x;
-            dst[1] = L.y;
-            dst[2] = L.z;
-            active = false;
-        }
-        const uint64_t idle = __ballot(!active && kp == kRtFree);
-        if (idle) {
-            uint32_t n = 0, t = 0;
-            if (lane == 0) {
-                n = min(ld(P.rt.n), P.rt.cap);
-                t = ld(P.rt.taken);
-            }
-            n = uni(n);
-            t = uni(t);
-            const uint32_t c = n > t ? min(n - t, (uint32_t)__popcll(idle)) : 0u;
-            if (c) {
-                uint32_t k0 = 0;
-                if (lane == 0) k0 = atomicAdd(P.rt.taken, c);
-                k0 = uni(k0);
-                const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                if (!active && kp == kRtFree && r < c) kp = k0 + r;
-            }
-        }
-        if (!__any(active)) {
-            uint32_t f = 0;
-            if (lane == 0) f = __hip_atomic_load(P.rt.fin, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-            f = uni(f);
-            const bool timeout = __builtin_amdgcn_s_memrealtime() - t_start > 1000000000ull;
-            if (f >= P.rt.waves || timeout) {
-                // every lister has ended: the count is final; entries claimed beyond it never come
-                uint32_t n = 0, t = 0;
-                if (lane == 0) {
-                    n = min(ld(P.rt.n), P.rt.cap);
-                    t = ld(P.rt.taken);
-                }
-                n = uni(n);
-                t = uni(t);
-                if (kp != kRtFree && (kp >= n || timeout)) kp = kRtFree;
-                if (!__any(kp != kRtFree) && (t >= n || timeout)) break;
-            } else if (!__any(kp != kRtFree)) {
-                __builtin_amdgcn_s_sleep(8);
-            }
-        }
-    }
-    // the last listener wave out: the launch's totals, and the list's counters cleared for the
-    // next launch of this parity (which waits for this kernel through the fold)
-    if (lane == 0 && atomicAdd(P.rt.done, 1u) == gridDim.x - 1u) {
-        const uint32_t listed = ld(P.rt.n);
-        const uint32_t n = min(listed, P.rt.cap);
-        if (n) atomicAdd(P.rt.total, (unsigned long long)n);
-        if (listed > n) atomicAdd(P.rt.lost, (unsigned long long)(listed - n));
-        atomicExch(P.rt.n, 0u);
-        atomicExch(P.rt.taken, 0u);
-        atomicExch(P.rt.fin, 0u);
-        atomicExch(P.rt.done, 0u);
-    }
-}
-#endif
 template <uint32_t F>
 static constexpr path_kernel_t kfn_retrace() {
 #if MRT_TABLE_PEX
     if constexpr (kRetrace<F>) return mrt_retrace_kernel<F>;
-#endif
-    return nullptr;
-}
-template <uint32_t F>
-static constexpr path_kernel_t kfn_listen() {
-#if MRT_TABLE_PEX
-    if constexpr (kRetrace<F>) return mrt_retrace_listen_kernel<F>;
 #endif
     return nullptr;
 }
@@ -972,8 +839,7 @@ static KernelTable make_table(const char* numerics, std::index_sequence<I...>) {
                        {PathQ<kVariants[I]>::words...},
                        {kBox6Walk<kVariants[I]>...},
                        {(uint32_t)(kLinSlabOps<kVariants[I]> && MRT_SIG_OF(kVariants[I]) == SIG_NONE)...},
-                       {kfn_retrace<kVariants[I]>()...},
-                       {kfn_listen<kVariants[I]>()...}};
+                       {kfn_retrace<kVariants[I]>()...}};
 }
 #if MRT_TABLE_PEX
 const KernelTable& mrtd::kernel_table_fast_pex() {

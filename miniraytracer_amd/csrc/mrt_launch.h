@@ -132,9 +132,6 @@ struct KernelTable {
     // the path-exact build's retrace kernel for the tolerance variants that hand rounding-critical
     // paths over (mrt_shade.h light_critical): launched over PathParams::rt after each path kernel
     path_kernel_t retrace[kNumVariants];
-    // the same beside the path kernel (mrt_retrace_listen_kernel): launched with it into slots its
-    // grid leaves free, it retraces each listed path as soon as it is listed
-    path_kernel_t listen[kNumVariants];
 };
 const KernelTable& kernel_table_exact();
 const KernelTable& kernel_table_fast();

@@ -66,7 +66,6 @@ static const KernelTable& fast_table() {
             else if (z.kernel[i] && !off("MRT_FTZ")) take_variant(m, z, i);
             // the exact arithmetic for the rounding-critical paths of the fast variants (mrt_retrace_kernel)
             m.retrace[i] = x.retrace[i];
-            m.listen[i] = x.listen[i];
         }
         return m;
     }();
@@ -100,7 +99,6 @@ struct FoldEnd {
     unsigned long long* hprog;       // their progress snapshots in host memory (or null)
     uint32_t nreset;                 // counter slots to reset (MRT_CNT_SLOTS per launch)
     uint32_t nprog;                  // progress snapshots to reset (MRT_NPART per launch)
-    uint32_t pend;                   // the listening retrace may still write paths marked kRtPend (async fold)
 };
 // what the render's path kernels consumed, reset for the context's next render in stream order
 // after them: the counter slots (word (k * MRT_CNT_SLOTS + slot) * MRT_COUNTER_STRIDE) and the
@@ -164,23 +162,6 @@ __global__ void __launch_bounds__(256) mrt_fold_kernel(const float* __restrict__
 #ifndef MRT_FOLD_ASYNC_WPE
 #define MRT_FOLD_ASYNC_WPE 8  // (register cap 64: FOLD_ASYNC_DEPTH 8 takes 46)
 #endif
-// a path the listening retrace has not written yet (its radiance marked kRtPend): wait for it
-// (the listener, beside, writes it; a 20-s bound so a lost write cannot hang the fold)
-MRT_DFN f3 pend_wait(f3 v, const float* e) {
-    auto pending = [](f3 x) {
-        return __float_as_uint(x.x) == kRtPend || __float_as_uint(x.y) == kRtPend || __float_as_uint(x.z) == kRtPend;
-    };
-    if (__builtin_expect(pending(v), 0)) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        float* m = const_cast<float*>(e);
-        do {
-            __builtin_amdgcn_s_sleep(4);
-            v = f3{__hip_atomic_load(m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), __hip_atomic_load(m + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                   __hip_atomic_load(m + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)};
-        } while (pending(v) && __builtin_amdgcn_s_memrealtime() - t0 < 2000000000ull);
-    }
-    return v;
-}
 __global__ void __launch_bounds__(MRT_FOLD_ASYNC_WG) __attribute__((amdgpu_waves_per_eu(MRT_FOLD_ASYNC_WPE)))
 mrt_fold_async_kernel(const float* __restrict__ rad, float4* __restrict__ acc, uint32_t npix, uint32_t s0, uint32_t s1, uint32_t mode,
                       float max_lum, FoldEnd fe) {
@@ -204,18 +185,12 @@ mrt_fold_async_kernel(const float* __restrict__ rad, float4* __restrict__ acc, u
                 const float* e = q + (size_t)(s - s0 + k) * stride;
                 v[k] = f3{__builtin_nontemporal_load(e), __builtin_nontemporal_load(e + 1), __builtin_nontemporal_load(e + 2)};
             }
-            if (fe.pend) {
-#pragma unroll
-                for (int k = 0; k < FOLD_ASYNC_DEPTH; k++) v[k] = pend_wait(v[k], q + (size_t)(s - s0 + k) * stride);
-            }
 #pragma unroll
             for (int k = 0; k < FOLD_ASYNC_DEPTH; k++) c = fold_sample(c, v[k], s + k, mode, max_lum);
         }
         for (; s < s1; s++) {
             const float* e = q + (size_t)(s - s0) * stride;
-            f3 v{e[0], e[1], e[2]};
-            if (fe.pend) v = pend_wait(v, e);
-            c = fold_sample(c, v, s, mode, max_lum);
+            c = fold_sample(c, f3{e[0], e[1], e[2]}, s, mode, max_lum);
         }
         if (fe.out) {
             c = final_pixel(c, fe.ns, mode, max_lum);
@@ -348,15 +323,8 @@ struct PathLaunch {
     path_kernel_t retrace = nullptr;  // the exact arithmetic for its rounding-critical paths (mrt_retrace_kernel)
     size_t retrace_lds = 0;
     bool handover = false;  // the kernel hands its rounding-critical paths to it (fast arithmetic)
-    // the retrace beside the path kernel (mrt_retrace_listen_kernel): its one-wave groups, launched
-    // with the path kernel into the slots its grid (grid - listen_groups) leaves free; 0: the retrace
-    // kernel after the path kernel
-    path_kernel_t listen = nullptr;
-    int listen_groups = 0;
     uint32_t walk_min = 32;  // resumable mesh walk threshold of this build (PathParams::walk_min)
 };
-// one-wave groups of the listening retrace (mrt_retrace_listen_kernel), taken from the path kernel's grid
-static constexpr int kListenGroups = 16;
 
 // Wide nodes renumbered breadth-first over all roots together (level 0 of every tree, then level
 // 1, ...), so the first K nodes of the array are the top levels of the scene's BVHs -- what a
@@ -421,10 +389,9 @@ struct mrt_scene {
     std::vector<uint32_t> prev_px;   // local pixel -> row-major pixel of the previewed render
     uint32_t prev_w = 0, prev_h = 0;
     uint32_t lev_rows = 0;
-    uint64_t* d_counter = nullptr;   // 128 B scratch: [0] paths handed to the exact arithmetic since upload, [2] ray total of mrt_render, [4] cancel flag,
+    uint64_t* d_counter = nullptr;   // 64 B scratch: [0] paths handed to the exact arithmetic since upload, [2] ray total of mrt_render, [4] cancel flag,
                                      // [1] rounding-critical paths listed (u32), [3] retrace groups done (u32), [5] listed beyond the cap since upload,
-                                     // [6] the parity-1 list's count (u32) and retrace groups done (u32), [8] / [9] the parity-0 / 1
-                                     // list's entries taken and path-kernel waves finished (u32 each; mrt_retrace_listen_kernel)
+                                     // [6] the parity-1 list's count (u32) and retrace groups done (u32)
     uint32_t* d_rt = nullptr;        // rounding-critical paths listed for the retrace kernel (path indices)
     size_t rt_cap = 0;
     uint64_t* d_counters = nullptr;  // one work counter per chunk launch (progress reads them)
@@ -452,11 +419,6 @@ struct mrt_scene {
     // run in order on fstream, so it also orders every earlier fold)
     hipStream_t fstream = nullptr;
     hipEvent_t ev_kern = nullptr;
-    // the listening retrace's own stream (not the fold stream: behind the previous launch's fold it
-    // would start only when its path kernel ended) and its end, which the launch's fold waits for
-    hipStream_t lstream = nullptr;
-    hipEvent_t ev_listen[2] = {nullptr, nullptr};
-    bool listen_pending[2] = {false, false};
     hipEvent_t ev_fold[2] = {nullptr, nullptr};
     bool fold_pending[2] = {false, false};
     uint32_t lpar = 0, rpar = 0;
@@ -1051,10 +1013,10 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
     void* p;
     if ((st = upload(s, &s->S, sizeof(DScene), &p))) { mrt_scene_free(s); return st; }
     s->d_S = (DScene*)p;
-    if ((st = dev_alloc(s, &p, 128))) { mrt_scene_free(s); return st; }
+    if ((st = dev_alloc(s, &p, 64))) { mrt_scene_free(s); return st; }
     s->d_counter = (uint64_t*)p;
     s->d_rays = (unsigned long long*)((char*)p + 16);
-    HIPCHK(hipMemset(p, 0, 128));  // the cancel flag (d_counter + 4) starts clear
+    HIPCHK(hipMemset(p, 0, 64));  // the cancel flag (d_counter + 4) starts clear
     // kernel variant + LDS stacks sized from the scene graph (top frame lives in registers)
     s->features = T.features;
     s->variant = pick_variant(s->features);
@@ -1098,7 +1060,6 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
             L.handover = k == 1 && L.retrace && L.fn != kernel_table_fast_pex().kernel[s->variant] && !(e && *e && atoi(e) == 0);
         }
         L.retrace_lds = (size_t)64 * 4 * (s->lds_frames * 2 + s->lds_rays * 11 + s->lds_mesh + s->lds_save);
-        L.listen = L.handover ? tabs[k]->listen[s->variant] : nullptr;
         // the path-exact build (the metal bunny under the tolerance contract) yields at 32 walking
         // lanes: 40 -1.2%, 28 -1.7%, 48 -10% (bunny 1024x1024x64, profiles/r04_ab.txt section 13)
         L.walk_min = (!walk_min_env && L.fn == kernel_table_fast_pex().kernel[s->variant]) ? 32u : s->walk_min;
@@ -1135,19 +1096,6 @@ extern "C" mrt_status mrt_scene_upload(int device, const mrt_scene_view* v, mrt_
             if (*e) nb = std::max(1, atoi(e));
 #endif
         L.grid = prop.multiProcessorCount * nb;
-        // the listening retrace: kListenGroups one-wave groups in slots the path kernel's grid leaves
-        // free -- they fit any such slot when the path kernel's groups are one wave and the
-        // listener's registers and LDS are no more than its own (MRT_LISTEN=0: the retrace after the
-        // path kernel, A/B)
-        if (L.listen) {
-            hipFuncAttributes la{};
-            HIPCHK(hipFuncGetAttributes(&la, reinterpret_cast<const void*>(L.listen)));
-            int groups = kListenGroups;
-            if (const char* e = getenv("MRT_LISTEN"))
-                if (*e) groups = atoi(e) > 1 ? atoi(e) : (atoi(e) == 0 ? 0 : groups);
-            const bool fits = L.wg == 64u && ((la.numRegs + 7) & ~7) <= vg && L.retrace_lds <= L.lds_bytes && groups < L.grid / 2;
-            L.listen_groups = fits ? groups : 0;
-        }
         // every work partition needs waves of its own: a wave leaves its partition only once it is
         // handed out, and visits at most MRT_STEAL_TRIES partitions (mrt_kernels.hip)
         if (L.grid < (int)MRT_NPART) return mrt_internal_fail(MRT_ERR_HIP, "path kernel grid smaller than the work partitions");
@@ -1175,8 +1123,7 @@ extern "C" void mrt_scene_free(mrt_scene* s) {
     if (s->h_seq) (void)hipHostFree(s->h_seq);
     if (s->ev_done) (void)hipEventDestroy(s->ev_done);
     if (s->fstream) (void)hipStreamDestroy(s->fstream);
-    if (s->lstream) (void)hipStreamDestroy(s->lstream);
-    for (hipEvent_t e : {s->ev_kern, s->ev_listen[0], s->ev_listen[1], s->ev_fold[0], s->ev_fold[1]})
+    for (hipEvent_t e : {s->ev_kern, s->ev_fold[0], s->ev_fold[1]})
         if (e) (void)hipEventDestroy(e);
     for (void* p : {(void*)s->d_rad2, (void*)s->d_counters, (void*)s->d_pixels, (void*)s->d_sdist, (void*)s->d_rad, (void*)s->d_path_rays, (void*)s->d_acc,
                     (void*)s->d_lev, (void*)s->d_out, (void*)s->d_prev, (void*)s->d_rt})
@@ -1279,29 +1226,20 @@ extern "C" mrt_status mrt_prepare(mrt_scene* s, const mrt_render_desc* d) {
     if (chunk != s->chunk && (st = quiesce(s))) return st;  // the fold of a running render reads `chunk` rows
     s->chunk = chunk;
     size_t paths = (size_t)s->npix * s->chunk;
-    // (+ one path: the trash slot a listed path's fast radiance goes to, RetraceList::trash)
-    if ((st = grow(s, (void**)&s->d_rad, &s->rad_cap, (paths + 1) * 12))) return st;
+    if ((st = grow(s, (void**)&s->d_rad, &s->rad_cap, paths * 12))) return st;
     if (d->flags & MRT_RF_FOLD_ASYNC) {
         if (d->flags & (MRT_RF_PREVIEW | MRT_RF_PATH_DEBUG | MRT_RF_FOLD_BEHIND))
             return mrt_internal_fail(MRT_ERR_INVALID, "MRT_RF_FOLD_ASYNC: no preview, debug or lean fold");
-        if ((st = grow(s, (void**)&s->d_rad2, &s->rad2_cap, (paths + 1) * 12))) return st;
+        if ((st = grow(s, (void**)&s->d_rad2, &s->rad2_cap, paths * 12))) return st;
         if (!s->fstream) HIPCHK(hipStreamCreateWithFlags(&s->fstream, hipStreamNonBlocking));
         if (!s->ev_kern) HIPCHK(hipEventCreateWithFlags(&s->ev_kern, hipEventDisableTiming));
         for (hipEvent_t& e : s->ev_fold)
             if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     // (two lists: one per radiance parity of the async fold)
-    if ((d->flags & MRT_RF_FAST) && !(d->flags & MRT_RF_PATH_DEBUG) && s->pl[1].handover) {
-        uint32_t* const before = s->d_rt;
-        if ((st = grow(s, (void**)&s->d_rt, &s->rt_cap, (size_t)2 * kRtCap * sizeof(uint32_t)))) return st;
-        // every entry starts free (kRtFree); the retrace kernels free each one they read
-        if (s->d_rt != before) HIPCHK(hipMemset(s->d_rt, 0xFF, s->rt_cap));
-        if (s->pl[1].listen_groups) {
-            if (!s->lstream) HIPCHK(hipStreamCreateWithFlags(&s->lstream, hipStreamNonBlocking));
-            for (hipEvent_t& e : s->ev_listen)
-                if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        }
-    }
+    if ((d->flags & MRT_RF_FAST) && !(d->flags & MRT_RF_PATH_DEBUG) && s->pl[1].handover &&
+        (st = grow(s, (void**)&s->d_rt, &s->rt_cap, (size_t)2 * kRtCap * sizeof(uint32_t))))
+        return st;
     if ((st = grow(s, (void**)&s->d_acc, &s->acc_cap, (size_t)s->npix * 16))) return st;
     if ((st = grow(s, (void**)&s->d_out, &s->out_cap, (size_t)s->npix * 16 + 16))) return st;
     if (d->flags & MRT_RF_PREVIEW) {
@@ -1414,10 +1352,8 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
     const uint32_t rpar = async ? s->rpar : 0u;
     if (async) s->rpar ^= 1u;
     if (!async)
-        for (uint32_t p = 0; p < 2; p++) {
+        for (uint32_t p = 0; p < 2; p++)
             if (s->fold_pending[p]) HIPCHK(hipStreamWaitEvent(q, s->ev_fold[p], 0));
-            if (s->listen_pending[p]) HIPCHK(hipStreamWaitEvent(q, s->ev_listen[p], 0));
-        }
     {
         std::lock_guard<std::mutex> lk(s->prog_mu);
         s->prog_base = rpar * s->slot_half;
@@ -1434,17 +1370,13 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
     // the rounding-critical paths' hand-over: tolerance contract, not the per-path debug output
     // (whose radiance is the fast kernel's own)
     const bool handover = PL.handover && !(d->flags & MRT_RF_PATH_DEBUG);
-    // the listening retrace takes its slots from the path kernel's grid
-    const bool listen = handover && PL.listen_groups > 0;
-    const int grid = listen ? PL.grid - PL.listen_groups : PL.grid;
+    const int grid = PL.grid;
     for (uint32_t s0 = 0; s0 < ns; s0 += s->chunk) {
         uint32_t s1 = std::min(ns, s0 + s->chunk);
         const uint32_t par = async ? s->lpar : 0u;
         if (async) {
             s->lpar ^= 1u;
             if (s->fold_pending[par]) HIPCHK(hipStreamWaitEvent(q, s->ev_fold[par], 0));
-            // (the list of this parity: its listener has cleared it)
-            if (s->listen_pending[par]) HIPCHK(hipStreamWaitEvent(q, s->ev_listen[par], 0));
         }
         float* const d_rad = par ? s->d_rad2 : s->d_rad;
         PathParams P{};
@@ -1493,14 +1425,10 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         P.lev_rows = s->lev_rows;
         // the list of the launch's radiance parity: entries at par * kRtCap, its count and its groups-done
         // word at d_counter[1] / [3] (parity 0) or the two halves of d_counter[6] (parity 1)
-        // (listening: its entries taken and the path kernel's waves finished at d_counter[8 + par])
         if (handover)
             P.rt = RetraceList{s->d_rt + (size_t)par * kRtCap, par ? (uint32_t*)(s->d_counter + 6) : (uint32_t*)(s->d_counter + 1), kRtCap,
                                par ? (uint32_t*)(s->d_counter + 6) + 1 : (uint32_t*)(s->d_counter + 3), (unsigned long long*)s->d_counter,
-                               (unsigned long long*)(s->d_counter + 5),
-                               listen ? (uint32_t*)(s->d_counter + 8 + par) : nullptr,
-                               listen ? (uint32_t*)(s->d_counter + 8 + par) + 1 : nullptr,
-                               (uint32_t)grid * (PL.wg / 64u), P.n_paths, listen && async ? d_rad : nullptr};
+                               (unsigned long long*)(s->d_counter + 5)};
         HIPCHK(hipEventRecord(s->ev[2 * s->n_launch], q));
         hipLaunchKernelGGL(PL.fn, dim3(grid), dim3(PL.wg), PL.lds_bytes, q, P);
         HIPCHK(hipGetLastError());
@@ -1509,19 +1437,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         // this launch's rounding-critical paths, exact, into the radiance buffer before its fold (the
         // exact arithmetic walks the program as compiled: the tolerance contract's rewrite has ops -- a
         // room's slab test, one-step box instances -- only the fast builds compile)
-        if (listen) {
-            // beside the path kernel, from its start, on its own stream; the launch's fold waits for it
-            PathParams PR = P;
-            PR.sc.prog = s->S.prog;
-            HIPCHK(hipStreamWaitEvent(s->lstream, s->ev[2 * (s->n_launch - 1)], 0));
-            hipLaunchKernelGGL(PL.listen, dim3(PL.listen_groups), dim3(64), PL.retrace_lds, s->lstream, PR);
-            HIPCHK(hipGetLastError());
-            HIPCHK(hipEventRecord(s->ev_listen[par], s->lstream));
-            s->listen_pending[par] = true;
-            // a blocking render's fold waits for it; an async launch's fold does not (it waits per
-            // path for the ones marked pending, pend_wait) -- the next launch of this parity does
-            if (!async) HIPCHK(hipStreamWaitEvent(q, s->ev_listen[par], 0));
-        } else if (handover) {
+        if (handover) {
             PathParams PR = P;
             PR.sc.prog = s->S.prog;
             hipLaunchKernelGGL(PL.retrace, dim3(kRetraceGroups), dim3(64), PL.retrace_lds, q, PR);
@@ -1534,7 +1450,7 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
         if (async) {  // the fold beside the next launch's path kernel
             const bool last = s1 == ns;
             FoldEnd fe{last ? (float4*)d_local : nullptr, ns, last ? d_cnt : nullptr, last ? h_prog : nullptr,
-                       last ? launches * MRT_CNT_SLOTS : 0u, last ? launches * MRT_NPART : 0u, listen ? 1u : 0u};
+                       last ? launches * MRT_CNT_SLOTS : 0u, last ? launches * MRT_NPART : 0u};
             hipLaunchKernelGGL(mrt_fold_async_kernel, dim3(s->n_cu * MRT_FOLD_ASYNC_GROUPS), dim3(MRT_FOLD_ASYNC_WG), 0, s->fstream, d_rad, s->d_acc, s->npix,
                                s0, s1, d->mode, d->max_luminance, fe);
             HIPCHK(hipGetLastError());
@@ -1577,9 +1493,6 @@ extern "C" mrt_status mrt_render_device(mrt_scene* s, const mrt_render_desc* d, 
                            d->max_luminance, (unsigned long long*)s->d_counters, (unsigned long long*)s->h_prog, nreset, launches * MRT_NPART);
         HIPCHK(hipGetLastError());
     }
-    if (async)  // (the render's end includes its listeners' ends: their totals and the lists' reset)
-        for (uint32_t p = 0; p < 2; p++)
-            if (s->listen_pending[p]) HIPCHK(hipStreamWaitEvent(s->fstream, s->ev_listen[p], 0));
     HIPCHK(hipEventRecord(s->ev_done, async ? s->fstream : q));
     s->ev_done_pending = true;
     s->n_chunks.store(launches, std::memory_order_release);  // progress reads start once every launch and its events are enqueued

@@ -224,27 +224,14 @@ struct RetraceList {
     uint32_t* __restrict__ done;             // retrace groups finished (the last one clears n)
     unsigned long long* __restrict__ total;  // paths listed since the scene's upload (mrt_kernel_info)
     unsigned long long* __restrict__ lost;   // entries beyond cap since the upload (mrt_kernel_info.handover_lost)
-    // the listening retrace (mrt_retrace_listen_kernel, beside the path kernel): entries claimed,
-    // path-kernel waves finished (null: the retrace runs after the path kernel), the path kernel's
-    // waves, and the path index whose radiance nobody reads (n_paths) -- a listed path's own store
-    // goes there, so only the exact arithmetic writes the listed path's radiance
-    uint32_t* __restrict__ taken;
-    uint32_t* __restrict__ fin;
-    uint32_t waves;
-    uint32_t trash;
-    // listening: the launch's radiance buffer, where a listed path's radiance is marked pending
-    // (kRtPend) until the listener writes it -- the async fold waits there for that path only
-    float* __restrict__ pend;
 };
-// a radiance component not written yet (a NaN payload no arithmetic produces)
-static constexpr uint32_t kRtPend = 0x7fc0deadu;
 // where a shading step lists its path when its light sample is rounding-critical: the path's index
 // and the byte offset of the launch's RetraceList in the kernel's argument segment (a compile-time
 // constant; 0: no hand-over compiled in).  The list is read from the argument segment only where a
 // path is listed (a null list: no hand-over this launch), so nothing of it is held in registers
 // across the path loop (held there, it cost the Cornell kernel 1.3% with the hand-over off).
 struct CritSink {
-    uint32_t* idx;  // the path's index; a listed path's becomes the list's trash index
+    uint32_t idx;
     uint32_t rt_off;
 };
 MRT_DFN void crit_check(const CritSink& cs, bool light, f3 origin, f3 gen, bool edge, f3 n) {
@@ -255,18 +242,9 @@ MRT_DFN void crit_check(const CritSink& cs, bool light, f3 origin, f3 gen, bool 
         const MRT_CONST_AS char* ka = (const MRT_CONST_AS char*)__builtin_amdgcn_kernarg_segment_ptr();
         asm volatile("" : "+s"(ka));  // (the list's fields are loaded here, not hoisted out of the loop)
         const MRT_CONST_AS RetraceList& rl = *(const MRT_CONST_AS RetraceList*)(ka + cs.rt_off);
-        // (a path listed once: its later bounces are not listed again; one that did not fit the
-        // list keeps its fast radiance)
-        if (rl.idx && *cs.idx != rl.trash) {
+        if (rl.idx) {
             const uint32_t k = atomicAdd(rl.n, 1u);
-            if (k < rl.cap) {
-                if (rl.pend) {  // (marked before the entry is published: release)
-                    float* d = rl.pend + (size_t)*cs.idx * 3u;
-                    d[0] = d[1] = d[2] = __uint_as_float(kRtPend);
-                }
-                __hip_atomic_store(rl.idx + k, *cs.idx, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                *cs.idx = rl.trash;
-            }
+            if (k < rl.cap) rl.idx[k] = cs.idx;
         }
     }
 #else
@@ -399,7 +377,7 @@ MRT_DFN void camera_ray_args(const DScene& S, Pcg& rng, float s, float t, f3* o,
 // is then in *L.
 template <uint32_t F, uint32_t LK>
 MRT_DFN bool shade_hit(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev, bool hit,
-                                          const HitRec& rec, f3* L, PhaseClock& ph, const CritSink& cs = CritSink{nullptr, 0u}) {
+                                          const HitRec& rec, f3* L, PhaseClock& ph, const CritSink& cs = CritSink{0u, 0u}) {
     Ray& r = ps.r;
     if (!hit) {
         if ((F & FT_SKY) && S.sky) {  // main.cpp:113-115
@@ -508,7 +486,7 @@ MRT_DFN bool shade_hit(const DScene& S, PathState& ps, uint32_t max_bounces, con
 // One segment.  Returns true when the path has ended; its radiance is then in *L.
 template <uint32_t F, uint32_t LK>
 MRT_DFN bool trace_segment(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev,
-                                              const LStack& Ls, f3* L, PhaseClock& ph, const CritSink& cs = CritSink{nullptr, 0u}) {
+                                              const LStack& Ls, f3* L, PhaseClock& ph, const CritSink& cs = CritSink{0u, 0u}) {
     HitRec rec;
     bool hit;
     if constexpr (MRT_SIG_OF(F) != SIG_NONE) hit = scene_hit_sig<F>(S, ps.r, 0.001f, rec, Ls);
@@ -574,7 +552,7 @@ MRT_DFN void dielectric_scatter(const DMat& M, const Ray& r, f3 n, Pcg& rng, Pen
 // previous path's radiance store there).
 template <uint32_t F, uint32_t LK, typename FLUSH>
 MRT_DFN bool trace_split(const DScene& S, PathState& ps, uint32_t max_bounces, const LevStore<LK>& lev,
-                                            const LStack& Ls, f3* L, PendRay* pr, PhaseClock& ph, FLUSH&& flush, const CritSink& cs = CritSink{nullptr, 0u}) {
+                                            const LStack& Ls, f3* L, PendRay* pr, PhaseClock& ph, FLUSH&& flush, const CritSink& cs = CritSink{0u, 0u}) {
     HitRec rec;
     Ray& r = ps.r;
     bool hit;
