@@ -840,6 +840,7 @@ mrt_status mrt_internal_scene_tables(const mrt_scene_view* v, SceneTables* T) {
             }
             const uint32_t cnt = (uint32_t)bprims.size() - first;
             if (cnt > BVHW_MAX_RUN || first > BVHW_FIRST_MASK) leaves_ok = false;
+            if ((BVHW_LEAF | (cnt << 24) | (first & BVHW_FIRST_MASK)) == kBvhwEmpty) leaves_ok = false;  // (the walk's empty-stack mark)
             return BVHW_LEAF | (cnt << 24) | (first & BVHW_FIRST_MASK);
         };
         std::function<uint32_t(uint32_t, int)> build = [&](uint32_t i, int depth) -> uint32_t {

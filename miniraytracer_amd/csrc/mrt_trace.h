@@ -50,6 +50,12 @@ struct BvhWide {
 #define BVHW_LEAF 0x80000000u
 #define BVHW_MAX_RUN 0x7Fu
 #define BVHW_FIRST_MASK 0xFFFFFFu
+// the bvh_node walk's empty-stack mark (bvhw_hit): a leaf ref no scene emits (the host refuses a
+// run of BVHW_MAX_RUN records starting at BVHW_FIRST_MASK)
+static constexpr uint32_t kBvhwEmpty = 0xFFFFFFFFu;
+#ifndef MRT_BVHW_SENT
+#define MRT_BVHW_SENT 1
+#endif
 
 // A wide node (MeshWide / BvhWide: both children's boxes, refs, order, flags) fetched whole: four
 // 16-byte loads issued together, so one memory round trip per node visit.  (Read field by field,
@@ -836,7 +842,15 @@ template <uint32_t F>
 MRT_DFN bool bvhw_hit(const DScene& S, const mrt_node& n, const Ray& r, float tmin, float tmax, HitRec& rec, bool full,
                                          const LStack& L) {
     if (!aabb_hit(n.f, n.f + 3, r, tmin, tmax)) return false;
+#if MRT_BVHW_SENT
+    // the stack's bottom holds kBvhwEmpty, popped when the walk is over: a lane leaves the inner
+    // loop by its leaf test alone, with no `return` inside it (the host sizes the stack with the
+    // slot to spare: the deepest leaf's inner ancestors are bvhw_depth - 1)
+    uint32_t ref = n.a, sp = 1;
+    L.mesh[L.lane] = kBvhwEmpty;
+#else
     uint32_t ref = n.a, sp = 0;
+#endif
     const bool bad = any_lane(!r.nice);  // (once per walk: aabb_hit_b)
     // (Leaf postponing by majority -- a lane parks its first leaf and walks on, as the path-exact
     // mesh walk does -- measured and removed: scene 2 +7.3%, random spheres +0.5% / -2.1% exact,
@@ -857,13 +871,22 @@ MRT_DFN bool bvhw_hit(const DScene& S, const mrt_node& n, const Ray& r, float tm
             const bool hc = sel_b(left_first, hl, hr), hf = sel_b(left_first, hr, hl);
             if (hc && hf && fref != cref) L.mesh[(sp++) * 64 + L.lane] = fref;  // n == 1: left == right, a repeat misses again
             ref = hc ? cref : fref;
+#if MRT_BVHW_SENT
+            if (!hc && !hf) ref = L.mesh[(--sp) * 64 + L.lane];
+#else
             if (!hc && !hf) {
                 if (sp == 0) return false;
                 ref = L.mesh[(--sp) * 64 + L.lane];
             }
+#endif
         }
+#if MRT_BVHW_SENT
+        if (ref == kBvhwEmpty) return false;
+        if (bvhw_leaf<F>(S, ref, r, tmin, tmax, rec, full)) return true;
+#else
         if (bvhw_leaf<F>(S, ref, r, tmin, tmax, rec, full)) return true;
         if (sp == 0) return false;
+#endif
         ref = L.mesh[(--sp) * 64 + L.lane];
     }
 }
