@@ -652,7 +652,12 @@ __global__ void __launch_bounds__(TreeOf<F>::wg) __attribute__((amdgpu_waves_per
                 const bool enter = in && aabb_hit(f3{rt.bmin[0], rt.bmin[1], rt.bmin[2]}, f3{rt.bmax[0], rt.bmax[1], rt.bmax[2]}, ps.r,
                                                   0.001f, w.closest);
                 ref = mn.b;
+#if MRT_MESH_SENT
+                Ls.mesh[lane] = kMeshEmpty;  // the stack's bottom (mrt_trace.h kMeshEmpty)
+                msp = 1;
+#else
                 msp = 0;
+#endif
 #if MRT_MESH_SPEC
                 pref = 0;
 #endif

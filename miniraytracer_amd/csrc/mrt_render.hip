@@ -748,6 +748,7 @@ mrt_status mrt_internal_scene_tables(const mrt_scene_view* v, SceneTables* T) {
             const uint32_t cnt = m.count_order & 0xFFFFFFu;
             if (cnt == 0) return wide_of[i];
             if (cnt > 0x7Fu || m.left_or_first > 0xFFFFFFu) ok = false;
+            if ((MESH_LEAF | (cnt << 24) | m.left_or_first) >= kMeshEmpty) ok = false;  // (the walk's marks)
             return MESH_LEAF | (cnt << 24) | m.left_or_first;
         };
         for (uint32_t i = 0; i < v->n_mesh_nodes && ok; i++) {

@@ -56,6 +56,13 @@ static constexpr uint32_t kBvhwEmpty = 0xFFFFFFFFu;
 #ifndef MRT_BVHW_SENT
 #define MRT_BVHW_SENT 1
 #endif
+// The resumable mesh walk's empty-stack mark (MRT_MESH_SENT, as kBvhwEmpty): the caller starts a
+// walk with it at the stack's bottom (msp 1), so a pop needs no empty-stack test first; popping it
+// ends the walk.  A leaf ref no mesh emits (the host refuses a run of 127 triangles at 0xFFFFFE).
+static constexpr uint32_t kMeshEmpty = 0xFFFFFFFEu;
+#ifndef MRT_MESH_SENT
+#define MRT_MESH_SENT 0  // (A/B hook: profiles/r06_ab.txt section 25)
+#endif
 
 // A wide node (MeshWide / BvhWide: both children's boxes, refs, order, flags) fetched whole: four
 // 16-byte loads issued together, so one memory round trip per node visit.  (Read field by field,
@@ -575,8 +582,13 @@ MRT_DFN uint32_t mesh_step(const DScene& S, const mrt_node& n, const Ray& r, flo
             pop = !hc && !hf;
         }
         if (pop) {
+#if MRT_MESH_SENT
+            ref = L.mesh[(--msp) * 64 + L.lane];
+            res = ref == kMeshEmpty ? 2u : res;
+#else
             if (msp == 0) res = 2u;
             else ref = L.mesh[(--msp) * 64 + L.lane];
+#endif
         }
         return res;
     }
@@ -659,7 +671,12 @@ MRT_DFN uint32_t mesh_step_spec(const DScene& S, const Ray& r, float tmin, float
     if (ref & MESH_LEAF) {
         if (pref != 0u) return 0u;  // a second leaf: waits
         pref = ref;                  // parked; the walk goes on with the stack's next entry
+#if MRT_MESH_SENT
+        ref = L.mesh[(--msp) * 64 + L.lane];
+        ref = ref == kMeshEmpty ? kMeshEnd : ref;
+#else
         ref = msp == 0u ? kMeshEnd : L.mesh[(--msp) * 64 + L.lane];
+#endif
         return 0u;
     }
     const WideNode W = mesh_wide<TREE>(S, ref, L);
@@ -671,9 +688,16 @@ MRT_DFN uint32_t mesh_step_spec(const DScene& S, const Ray& r, float tmin, float
     if (hc && hf) L.mesh[(msp++) * 64 + L.lane] = fref;
     ref = hc ? cref : (hf ? fref : ref);
     if (!hc && !hf) {
+#if MRT_MESH_SENT
+        ref = L.mesh[(--msp) * 64 + L.lane];
+        const bool end = ref == kMeshEmpty;
+        ref = end && pref != 0u ? kMeshEnd : ref;
+        res = end && pref == 0u ? 2u : res;
+#else
         if (msp != 0u) ref = L.mesh[(--msp) * 64 + L.lane];
         else if (pref != 0u) ref = kMeshEnd;
         else res = 2u;
+#endif
     }
     return res;
 }
