@@ -56,6 +56,9 @@ static constexpr uint32_t kBvhwEmpty = 0xFFFFFFFFu;
 #ifndef MRT_BVHW_SENT
 #define MRT_BVHW_SENT 1
 #endif
+#ifndef MRT_BVHW_PUSH_ALWAYS
+#define MRT_BVHW_PUSH_ALWAYS 0
+#endif
 // The resumable mesh walk's empty-stack mark (MRT_MESH_SENT, as kBvhwEmpty): the caller starts a
 // walk with it at the stack's bottom (msp 1), so a pop needs no empty-stack test first; popping it
 // ends the walk.  A leaf ref no mesh emits (the host refuses a run of 127 triangles at 0xFFFFFE).
@@ -893,7 +896,14 @@ MRT_DFN bool bvhw_hit(const DScene& S, const mrt_node& n, const Ray& r, float tm
             const bool left_first = (W.order & r.mask) != 0;
             const uint32_t cref = left_first ? W.lref : W.rref, fref = left_first ? W.rref : W.lref;
             const bool hc = sel_b(left_first, hl, hr), hf = sel_b(left_first, hr, hl);
+#if MRT_BVHW_PUSH_ALWAYS
+            // (A/B hook: the far child stored by every lane above its stack's top, kept by the
+            // pointer's increment alone -- an inner node's lane has sp <= its depth < the stack's size)
+            L.mesh[sp * 64 + L.lane] = fref;
+            sp += (hc && hf && fref != cref) ? 1u : 0u;
+#else
             if (hc && hf && fref != cref) L.mesh[(sp++) * 64 + L.lane] = fref;  // n == 1: left == right, a repeat misses again
+#endif
             ref = hc ? cref : fref;
 #if MRT_BVHW_SENT
             if (!hc && !hf) ref = L.mesh[(--sp) * 64 + L.lane];
